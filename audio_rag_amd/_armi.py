@@ -1,0 +1,140 @@
+"""ctypes binding of libarmi.so (the C ABI declared in include/armi.h).
+
+This is the only way the package reaches the GPU: there is no CPU or PyTorch fallback for the
+retrieval kernels. If the library is missing or fails to load, every caller gets
+``ArmiUnavailable`` immediately (build it with ``python -m audio_rag_amd.build`` or
+``__graft_entry__.build()``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libarmi.so"
+
+ARMI_OK = 0
+ARMI_FLAG_CERTIFIED = 1
+ARMI_FLAG_FALLBACK = 2
+ABI_VERSION = 1
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_size_t = ctypes.c_size_t
+c_float = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/armi.h exactly
+SIGNATURES: dict[str, tuple] = {
+    "armi_last_error": (ctypes.c_char_p, []),
+    "armi_abi_version": (c_int, []),
+    "armi_index_create": (c_int, [c_int, c_void_p, c_int64, c_int, c_int64, ctypes.POINTER(c_void_p), c_void_p]),
+    "armi_index_destroy": (c_int, [c_void_p]),
+    "armi_index_rows": (c_int64, [c_void_p]),
+    "armi_index_dim": (c_int, [c_void_p]),
+    "armi_index_invalid_rows": (c_int64, [c_void_p]),
+    "armi_index_norms": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
+    "armi_dense_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
+    "armi_dense_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "armi_dense_exact_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
+    "armi_dense_exact_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "armi_topk_merge_shards": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                       c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "armi_scan_timing_enable": (c_int, [c_int]),
+    "armi_scan_timing_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
+    "armi_sparse_index_create": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
+                                         c_int64, ctypes.POINTER(c_void_p), c_void_p]),
+    "armi_sparse_index_destroy": (c_int, [c_void_p]),
+    "armi_sparse_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
+    "armi_sparse_topk": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "armi_rrf_fuse": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "armi_enc_layernorm_residual": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                            c_int, c_float, c_void_p]),
+    "armi_enc_masked_softmax": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p]),
+    "armi_enc_bias_gelu": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "armi_enc_embed": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_int, c_int, c_int, c_int, c_float, c_void_p]),
+    "armi_enc_cls_head_sigmoid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_int, c_int, c_int, c_void_p]),
+}
+
+
+class ArmiUnavailable(RuntimeError):
+    """libarmi.so is missing or unloadable: the MI355X path cannot run."""
+
+
+class ArmiError(RuntimeError):
+    """A libarmi call returned a non-zero status."""
+
+    def __init__(self, fn: str, code: int, message: str):
+        super().__init__(f"{fn} failed (status {code}): {message}")
+        self.fn = fn
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+
+def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Loads libarmi.so once. torch is imported first so that the library binds to the same
+    HIP runtime instance (libamdhip64.so.7) that owns torch's device allocations."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (binds the process to torch's HIP runtime first)
+
+        p = Path(path) if path else LIB_PATH
+        if not p.exists():
+            raise ArmiUnavailable(
+                f"{p} not found: build it with `python -m audio_rag_amd.build` (hipcc, gfx950)")
+        try:
+            lib = ctypes.CDLL(str(p))
+        except OSError as e:
+            raise ArmiUnavailable(f"cannot load {p}: {e}") from e
+        for name, (restype, argtypes) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        if lib.armi_abi_version() != ABI_VERSION:
+            raise ArmiUnavailable(f"{p}: ABI version {lib.armi_abi_version()} != {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args) -> int:
+    """Calls an int-status entry point and raises ArmiError on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != ARMI_OK:
+        msg = lib.armi_last_error().decode(errors="replace")
+        raise ArmiError(name, rc, msg)
+    return rc
+
+
+def query(name: str, *args):
+    """Calls a non-status entry point (sizes, counters) and returns its value."""
+    return getattr(load(), name)(*args)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    """hipStream_t of a torch.cuda.Stream (default: the current stream)."""
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,142 @@
+// Shared host + device helpers of libarmi (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/armi.h"
+
+namespace armi {
+
+// ----------------------------------------------------------------------------------- errors
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define ARMI_HIP(call)                                   \
+  do {                                                   \
+    hipError_t _e = (call);                              \
+    if (_e != hipSuccess) return armi::hip_fail(_e, #call); \
+  } while (0)
+
+#define ARMI_LAUNCHED(what)                              \
+  do {                                                   \
+    hipError_t _e = hipGetLastError();                   \
+    if (_e != hipSuccess) return armi::hip_fail(_e, what); \
+  } while (0)
+
+#define ARMI_REQUIRE(cond, msg)                          \
+  do {                                                   \
+    if (!(cond)) return armi::fail(ARMI_ERR_INVALID, msg); \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Carves consecutive 256-B aligned sub-buffers out of one caller workspace.
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+  template <typename T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+};
+
+// ------------------------------------------------------------------------------- numerics
+
+// Exact integer image of an IEEE binary16 value: x * 2^24 (every finite fp16 is an integer
+// multiple of 2^-24). Callers guarantee exponent field <= 15 (|x| < 2), so |result| < 2^25.
+__device__ __forceinline__ int32_t fp16_to_fixed24(uint32_t h) {
+  const int32_t e = (h >> 10) & 31;
+  const int32_t m = h & 1023;
+  const int32_t v = (e == 0) ? m : ((1024 | m) << (e - 1));
+  return (h & 0x8000u) ? -v : v;
+}
+
+__device__ __forceinline__ bool fp16_in_domain(uint32_t h) { return ((h >> 10) & 31) <= 15; }
+
+// Total order used by every dense ranking: key descending, then ordinal ascending.
+__device__ __forceinline__ bool rank_better(double ka, int64_t ia, double kb, int64_t ib) {
+  return ka > kb || (ka == kb && ia < ib);
+}
+__device__ __forceinline__ bool approx_better(float ka, int32_t ia, float kb, int32_t ib) {
+  return ka > kb || (ka == kb && ia < ib);
+}
+
+// In-LDS bitonic sort of n (power of two) entries into descending rank order, executed by the
+// whole workgroup. Entries: (double key, int64 ordinal).
+__device__ inline void lds_sort_rank_desc(double* key, int64_t* ord, int n) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const double klo = key[lo], khi = key[hi];
+        const int64_t olo = ord[lo], ohi = ord[hi];
+        const bool hi_better = rank_better(khi, ohi, klo, olo);
+        if (hi_better == desc) {
+          key[lo] = khi; key[hi] = klo;
+          ord[lo] = ohi; ord[hi] = olo;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Same for (float approx key, int32 row) entries.
+__device__ inline void lds_sort_approx_desc(float* key, int32_t* row, int n) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const float klo = key[lo], khi = key[hi];
+        const int32_t rlo = row[lo], rhi = row[hi];
+        const bool hi_better = approx_better(khi, rhi, klo, rlo);
+        if (hi_better == desc) {
+          key[lo] = khi; key[hi] = klo;
+          row[lo] = rhi; row[hi] = rlo;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Wave-level (64 lanes) bitonic sort, one entry per lane, descending by (key, row asc).
+__device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float ok = __shfl_xor(key, stride);
+      const int32_t orow = __shfl_xor(row, stride);
+      const bool lower = (lane & stride) == 0;
+      const bool desc = (lane & size) == 0;
+      const bool other_better = approx_better(ok, orow, key, row);
+      // lower lane of a descending pair keeps the better entry
+      const bool take_other = (lower == desc) ? other_better : !other_better;
+      if (take_other) { key = ok; row = orow; }
+    }
+  }
+}
+
+__host__ __device__ inline int pow2_at_least(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace armi

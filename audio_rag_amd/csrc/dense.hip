@@ -1,0 +1,936 @@
+// Dense cosine top-k over a fp16 chunk store (gfx950).
+//
+// Restates Qdrant's COSINE search as called by QdrantRetriever.search
+// (src/audio_rag/retrieval/qdrant.py:284-288 dense prefetch of hybrid search, 316-332 dense
+// query) over vectors produced by BGEM3Embedder (src/audio_rag/embeddings/bge.py:104-157,
+// fp16 on GPU: bge.py:54). Ranking is the exact cosine of the fp16 inputs; ties are broken by
+// ascending chunk ordinal.
+//
+// Pipeline per call (all on one stream, no host synchronisation):
+//   1. dense_scan: one 512-thread workgroup per CU streams a contiguous range of 32-row tiles
+//      straight from HBM into VGPRs (each corpus byte is read once and used by exactly one
+//      wave), multiplies it against up to 64 queries held in LDS with
+//      v_mfma_f32_32x32x16_f16 (fp32 accumulate), scales by the fp32 inverse norm and keeps a
+//      4-deep top list per lane and query in registers. The 16 lane lists of a query are merged
+//      in LDS by a wave bitonic sort into 16 candidates per workgroup, plus the largest score
+//      any list discarded ("bound").
+//   2. dense_merge: one workgroup per query pools all workgroup candidates, keeps the KC best
+//      approximate scores, rescores them EXACTLY (int64 dot of the 2^24 fixed-point images),
+//      sorts by (exact key desc, ordinal asc) and certifies the answer: every discarded row has
+//      approximate score <= bound and |approx - exact| <= delta, so when the k-th exact key
+//      exceeds bound + delta no discarded row can belong to the top-k.
+//   3. dense_exact_scan + merge_lists: for queries that could not be certified, an exhaustive
+//      exact scan (workgroups of certified queries exit immediately).
+#include <cmath>
+#include <limits>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "armi_index.h"
+
+namespace {
+
+using armi::TILE_ROWS;
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+constexpr int kQB = 64;       // queries per scan pass (LDS holds their fragment image)
+constexpr int kLaneList = 4;  // top entries kept per lane and query
+constexpr int kKW = 16;       // candidates per workgroup and query
+constexpr int kDepth = 4;     // 64-byte groups in flight per lane
+constexpr float kNegInf = -std::numeric_limits<float>::infinity();
+constexpr double kNegInfD = -std::numeric_limits<double>::infinity();
+constexpr int64_t kNoOrd = std::numeric_limits<int64_t>::max();
+constexpr int kMaxK = 240;
+constexpr int kMergeThreads = 256;
+constexpr int kMaxPool = 4096;  // pooled candidates per query in the merge kernels
+// delta = kDeltaSafety * dim * 2^-24 * |q|: the fp32 accumulation error bound gamma_dim * |q|
+// (|sum| <= sum |q_i x_i| <= |q||x|) with a 4x allowance for the MFMA's internal ordering.
+constexpr double kDeltaSafety = 4.0;
+
+template <int M>
+__device__ __forceinline__ void topm_insert(float x, int32_t id, float (&s)[M], int32_t (&ix)[M],
+                                            float& disc) {
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const bool c = x > s[j];
+    const float ts = c ? x : s[j];
+    const int32_t ti = c ? id : ix[j];
+    x = c ? s[j] : x;
+    id = c ? ix[j] : id;
+    s[j] = ts;
+    ix[j] = ti;
+  }
+  disc = fmaxf(disc, x);
+}
+
+__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a),
+                                                __builtin_bit_cast(half8, b), c, 0, 0, 0);
+}
+
+// LDS bytes of the scan kernel: the query fragment image, later overlaid by the merge scratch.
+template <int DIM>
+constexpr int scan_lds_bytes() {
+  constexpr int img = (DIM / 16) * 2 * kQB * 16;
+  constexpr int scratch = kQB * 64 * 4 * 2 + kQB * 16 * 4;
+  return img > scratch ? img : scratch;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(kThreads) void dense_scan_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
+    const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+  constexpr int KSTEPS = DIM / 16;
+  constexpr int GROUPS = DIM / 64;
+  static_assert(GROUPS % kDepth == 0, "prefetch ring must divide the tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
+
+  // 1. Query fragment image. K-step s, lane half h takes the 8 elements of chunk
+  //    c = 8*(s/4) + 4*h + s%4, matching the corpus chunk that lane half loads (any k order
+  //    is valid for a dot product as long as A and B agree).
+  for (int e = threadIdx.x; e < KSTEPS * 2 * kQB; e += kThreads) {
+    const int q = e & (kQB - 1);
+    const int sh = e >> 6;
+    const int h = sh & 1;
+    const int s = sh >> 1;
+    const int c = 8 * (s >> 2) + 4 * h + (s & 3);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 8 * c);
+    qimg[e] = v;
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t t_begin = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
+
+  float s0[kLaneList], s1[kLaneList];
+  int32_t i0[kLaneList], i1[kLaneList];
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
+  }
+  float d0 = kNegInf, d1 = kNegInf;
+
+  int64_t t = t_begin + wave;
+  if (t < t_end) {
+    auto row_ptr = [&](int64_t tile) -> const u32x4* {
+      int64_t rr = tile * TILE_ROWS + r;
+      rr = rr < n_rows ? rr : n_rows - 1;
+      return reinterpret_cast<const u32x4*>(rows + rr * DIM) + 4 * h;
+    };
+    const u32x4* cur = row_ptr(t);
+    u32x4 buf[kDepth][4];
+#pragma unroll
+    for (int g = 0; g < kDepth; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[g][i] = cur[8 * g + i];
+
+    for (; t < t_end; t += kWaves) {
+      const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
+      const u32x4* nxt = row_ptr(tn);
+      // The fragment image is loop-invariant; an opaque per-tile offset keeps the compiler from
+      // hoisting all 2*KSTEPS fragment reads out of the tile loop (512 VGPRs -> scratch).
+      int qoff = h * kQB + r;
+      asm volatile("" : "+v"(qoff));
+      const u32x4* qv = qimg + qoff;
+      f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+      for (int g = 0; g < GROUPS; ++g) {
+        u32x4 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = buf[g % kDepth][i];
+        if (g + kDepth < GROUPS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) buf[g % kDepth][i] = cur[8 * (g + kDepth) + i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) buf[g % kDepth][i] = nxt[8 * (g + kDepth - GROUPS) + i];
+        }
+        // Pin the refill here: without it the scheduler sinks each load next to its first use
+        // (kDepth groups later) and every group waits a full HBM round trip.
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int s = 4 * g + i;
+          const u32x4 b0 = qv[s * 2 * kQB];
+          const u32x4 b1 = qv[s * 2 * kQB + 32];
+          acc0 = mfma16(a[i], b0, acc0);
+          acc1 = mfma16(a[i], b1, acc1);
+        }
+      }
+      cur = nxt;
+
+      // Epilogue: lane holds rows (j&3) + 8*(j>>2) + 4*h of the tile, queries r and 32 + r.
+      const int64_t row0 = t * TILE_ROWS;
+      float inv[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(inv_norm32 + row0 + 8 * q + 4 * h);
+        inv[4 * q + 0] = v.x; inv[4 * q + 1] = v.y; inv[4 * q + 2] = v.z; inv[4 * q + 3] = v.w;
+      }
+      uint32_t mbits = 0xffffffffu;
+      if (row_mask) mbits = (uint32_t)(row_mask[row0 >> 6] >> (row0 & 63));
+      float x0[16], x1[16];
+      float mx0 = kNegInf, mx1 = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int rt = (j & 3) + 8 * (j >> 2) + 4 * h;
+        const float a0 = acc0[j] * inv[j];
+        const float a1 = acc1[j] * inv[j];
+        const bool ok = ((mbits >> rt) & 1u) && (a0 == a0) && (a1 == a1);
+        x0[j] = ok ? a0 : kNegInf;
+        x1[j] = ok ? a1 : kNegInf;
+        mx0 = fmaxf(mx0, x0[j]);
+        mx1 = fmaxf(mx1, x1[j]);
+      }
+      const int32_t rbase = (int32_t)row0 + 4 * h;
+      if (__any(mx0 > s0[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          topm_insert<kLaneList>(x0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+      } else {
+        d0 = fmaxf(d0, mx0);
+      }
+      if (__any(mx1 > s1[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          topm_insert<kLaneList>(x1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+      } else {
+        d1 = fmaxf(d1, mx1);
+      }
+    }
+  }
+
+  // 2. Workgroup merge (the query image is dead: overlay it).
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][64]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * 64 * 4);        // [kQB][64]
+  float* ldisc = reinterpret_cast<float*>(smem + kQB * 64 * 8);           // [kQB][16]
+  const int slot = wave * 2 + h;
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    lkey[r * 64 + slot * kLaneList + j] = s0[j];
+    lrow[r * 64 + slot * kLaneList + j] = i0[j];
+    lkey[(32 + r) * 64 + slot * kLaneList + j] = s1[j];
+    lrow[(32 + r) * 64 + slot * kLaneList + j] = i1[j];
+  }
+  ldisc[r * 16 + slot] = d0;
+  ldisc[(32 + r) * 16 + slot] = d1;
+  __syncthreads();
+  for (int qq = 0; qq < kQB / kWaves; ++qq) {
+    const int q = wave * (kQB / kWaves) + qq;
+    if (q >= nq) break;
+    float key = lkey[q * 64 + lane];
+    int32_t row = lrow[q * 64 + lane];
+    armi::wave_sort_approx_desc(key, row);
+    const size_t base = (size_t)blockIdx.x * kQB + q;
+    if (lane < kKW) {
+      cand_key[base * kKW + lane] = key;
+      cand_row[base * kKW + lane] = row;
+    }
+    float b = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
+    if (lane == kKW) b = fmaxf(b, key);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+    if (lane == 0) cand_bound[base] = b;
+  }
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// This lane's DIM/64 contiguous fp16 elements of a vector, as raw 8-byte words.
+template <int DIM>
+__device__ __forceinline__ void load_raw(const uint16_t* __restrict__ v, int lane,
+                                         u32x2 (&raw)[DIM / 256]) {
+  constexpr int E = DIM / 64;
+  const u32x2* p = reinterpret_cast<const u32x2*>(v + lane * E);
+#pragma unroll
+  for (int i = 0; i < E / 4; ++i) raw[i] = p[i];
+}
+
+template <int DIM>
+__device__ __forceinline__ void raw_to_fixed(const u32x2 (&raw)[DIM / 256],
+                                             int32_t (&out)[DIM / 64]) {
+#pragma unroll
+  for (int i = 0; i < DIM / 256; ++i) {
+    out[4 * i + 0] = armi::fp16_to_fixed24(raw[i][0] & 0xffffu);
+    out[4 * i + 1] = armi::fp16_to_fixed24(raw[i][0] >> 16);
+    out[4 * i + 2] = armi::fp16_to_fixed24(raw[i][1] & 0xffffu);
+    out[4 * i + 3] = armi::fp16_to_fixed24(raw[i][1] >> 16);
+  }
+}
+
+// Exact 2^24 fixed-point image of this lane's DIM/64 contiguous elements.
+template <int DIM>
+__device__ __forceinline__ void load_fixed(const uint16_t* __restrict__ v, int lane,
+                                           int32_t (&out)[DIM / 64]) {
+  u32x2 raw[DIM / 256];
+  load_raw<DIM>(v, lane, raw);
+  raw_to_fixed<DIM>(raw, out);
+}
+
+// Exact int64 dot of this lane's slice, reduced over the wave.
+template <int DIM>
+__device__ __forceinline__ int64_t dot_fixed(const int32_t (&qf)[DIM / 64],
+                                             const u32x2 (&raw)[DIM / 256]) {
+  int32_t xf[DIM / 64];
+  raw_to_fixed<DIM>(raw, xf);
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)xf[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  return acc;
+}
+
+template <int DIM>
+__device__ __forceinline__ int64_t wave_dot_exact(const int32_t (&qf)[DIM / 64],
+                                                  const uint16_t* __restrict__ row, int lane) {
+  u32x2 raw[DIM / 256];
+  load_raw<DIM>(row, lane, raw);
+  return dot_fixed<DIM>(qf, raw);
+}
+
+// Per-query exact norm: writes 1/sqrt(norm2) (0 for a zero query) and |q| in real units.
+template <int DIM>
+__global__ __launch_bounds__(64) void query_norms_kernel(const uint16_t* __restrict__ queries,
+                                                         int nq, double* __restrict__ inv_q,
+                                                         double* __restrict__ qnorm_real) {
+  const int q = blockIdx.x;
+  if (q >= nq) return;
+  const int lane = threadIdx.x;
+  int32_t qf[DIM / 64];
+  load_fixed<DIM>(queries + (size_t)q * DIM, lane, qf);
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)qf[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) {
+    inv_q[q] = acc > 0 ? 1.0 / sqrt((double)acc) : 0.0;
+    qnorm_real[q] = sqrt((double)acc) * (1.0 / 16777216.0);
+  }
+}
+
+// One workgroup per query of the pass: select, exact rescore, certify, emit.
+//   Each scan workgroup's list is sorted, so its first entry is its maximum. The kc-th largest of
+//   those maxima, t0, is a lower bound of the pooled kc-th best, hence every entry of the pooled
+//   top-kc is >= t0: only entries >= t0 are kept (typically ~2*kc of n_wg*kKW) and sorted.
+//   Entries below t0 are discards and join the bound.
+constexpr int kSelCap = 1024;  // kept entries per query; overflow -> uncertified (exact fallback)
+constexpr int kRescoreBatch = 4;
+
+template <int DIM>
+__global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
+    const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
+    const float* __restrict__ cand_bound, int n_wg, int q_first, const uint16_t* __restrict__ rows,
+    const double* __restrict__ inv_norm, const uint16_t* __restrict__ queries,
+    const double* __restrict__ inv_q, const double* __restrict__ qnorm_real, int k, int kc,
+    int64_t ordinal_base, float* __restrict__ out_scores, int64_t* __restrict__ out_ids,
+    double* __restrict__ out_rank, int32_t* __restrict__ out_count,
+    uint32_t* __restrict__ out_flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* skey = reinterpret_cast<float*>(smem);                              // [kSelCap]
+  int32_t* srow = reinterpret_cast<int32_t*>(smem + kSelCap * 4);            // [kSelCap]
+  double* rkey = reinterpret_cast<double*>(smem + kSelCap * 8);              // [256]
+  int64_t* rord = reinterpret_cast<int64_t*>(smem + kSelCap * 8 + 256 * 8);  // [256]
+  float* mx = reinterpret_cast<float*>(smem + kSelCap * 8 + 256 * 16);       // [256]
+  int32_t* mxr = reinterpret_cast<int32_t*>(smem + kSelCap * 8 + 256 * 20);  // [256]
+  float* red = reinterpret_cast<float*>(smem + kSelCap * 8 + 256 * 24);      // [8]
+  int* ctr = reinterpret_cast<int*>(smem + kSelCap * 8 + 256 * 24 + 32);     // [4]
+
+  const int ql = blockIdx.x;
+  const int qg = q_first + ql;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int pool = n_wg * kKW;
+
+  // maxima + bound of the scan workgroups
+  float b = kNegInf;
+  for (int g = tid; g < 256; g += kMergeThreads) {
+    float m = kNegInf;
+    if (g < n_wg) {
+      m = cand_key[((size_t)g * kQB + ql) * kKW];
+      b = fmaxf(b, cand_bound[(size_t)g * kQB + ql]);
+    }
+    mx[g] = m;
+    mxr[g] = g;
+  }
+  if (tid == 0) ctr[0] = 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+  if (lane == 0) red[wave] = b;
+  armi::lds_sort_approx_desc(mx, mxr, 256);
+  const float t0 = (n_wg >= kc) ? mx[kc - 1] : kNegInf;
+
+  // filter the pool
+  float dmax = kNegInf;
+  for (int e = tid; e < pool; e += kMergeThreads) {
+    const size_t src = ((size_t)(e / kKW) * kQB + ql) * kKW + (e % kKW);
+    const float kk = cand_key[src];
+    if (kk == kNegInf) continue;
+    if (kk >= t0) {
+      const int slot = atomicAdd(&ctr[0], 1);
+      if (slot < kSelCap) {
+        skey[slot] = kk;
+        srow[slot] = cand_row[src];
+      }
+    } else {
+      dmax = fmaxf(dmax, kk);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
+  if (lane == 0) red[4 + wave] = dmax;
+  __syncthreads();
+  const int n_sel = ctr[0];
+  const bool overflow = n_sel > kSelCap;
+  const int n_keep = overflow ? kSelCap : n_sel;
+  const int n2 = armi::pow2_at_least(n_keep > kc ? n_keep : kc);
+  for (int e = n_keep + tid; e < n2; e += kMergeThreads) {
+    skey[e] = kNegInf;
+    srow[e] = 0x7fffffff;
+  }
+  armi::lds_sort_approx_desc(skey, srow, n2);
+  float bound = red[0];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
+  if (n2 > kc) bound = fmaxf(bound, skey[kc]);
+
+  // exact rescore of the kc best, kRescoreBatch rows in flight per wave
+  int32_t qf[DIM / 64];
+  load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
+  const int per_wave = kc / 4;
+  for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
+    u32x2 raw[kRescoreBatch][DIM / 256];
+    int32_t rr[kRescoreBatch];
+#pragma unroll
+    for (int j = 0; j < kRescoreBatch; ++j) {
+      const int c = wave + 4 * (i0 + j);
+      const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
+      rr[j] = live ? srow[c] : -1;
+      load_raw<DIM>(rows + (size_t)(live ? rr[j] : 0) * DIM, lane, raw[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kRescoreBatch; ++j) {
+      if (i0 + j >= per_wave) break;
+      const int c = wave + 4 * (i0 + j);
+      double key = kNegInfD;
+      int64_t ord = kNoOrd;
+      const int64_t dot = dot_fixed<DIM>(qf, raw[j]);
+      if (rr[j] >= 0) {
+        key = (double)dot * inv_norm[rr[j]];
+        ord = ordinal_base + rr[j];
+      }
+      if (lane == 0) {
+        rkey[c] = key;
+        rord[c] = ord;
+      }
+    }
+  }
+  armi::lds_sort_rank_desc(rkey, rord, kc);
+
+  if (tid == 0) {
+    int nv = 0;
+    while (nv < kc && rord[nv] != kNoOrd) ++nv;
+    ctr[1] = nv;
+  }
+  __syncthreads();
+  const int n_valid = ctr[1];
+  bool certified;
+  int n_out;
+  if (n_valid >= k) {
+    const double kth = rkey[k - 1] * (1.0 / 16777216.0);
+    const double delta = kDeltaSafety * (double)DIM * (1.0 / 16777216.0) * qnorm_real[qg];
+    certified = kth > (double)bound + delta;
+    n_out = k;
+  } else {
+    certified = (bound == kNegInf);
+    n_out = n_valid;
+  }
+  certified = certified && !overflow;
+  if (certified) {
+    const double iq = inv_q[qg];
+    for (int c = tid; c < k; c += kMergeThreads) {
+      const size_t o = (size_t)qg * k + c;
+      if (c < n_out) {
+        out_scores[o] = (float)(rkey[c] * iq);
+        out_ids[o] = rord[c];
+        if (out_rank) out_rank[o] = rkey[c];
+      } else {
+        out_scores[o] = kNegInf;
+        out_ids[o] = -1;
+        if (out_rank) out_rank[o] = kNegInfD;
+      }
+    }
+  }
+  if (tid == 0) {
+    out_count[qg] = certified ? n_out : 0;
+    out_flags[qg] = certified ? ARMI_FLAG_CERTIFIED : 0u;
+  }
+}
+
+constexpr size_t kMergeLds = kSelCap * 8 + 256 * 24 + 64;
+
+// Exhaustive exact scan: grid (n_blocks, nq); block b scores rows [b*rpb, (b+1)*rpb) and keeps
+// its best `cap` (power of two) entries. Queries whose flag says CERTIFIED are skipped.
+template <int DIM>
+__global__ __launch_bounds__(256) void dense_exact_scan_kernel(
+    const uint16_t* __restrict__ rows, const double* __restrict__ inv_norm,
+    const int64_t* __restrict__ norm2, const uint64_t* __restrict__ row_mask, int64_t n_rows,
+    int64_t rows_per_block, const uint16_t* __restrict__ queries, const uint32_t* __restrict__ flags,
+    int cap, int64_t ordinal_base, double* __restrict__ ex_key, int64_t* __restrict__ ex_ord) {
+  const int q = blockIdx.y;
+  if (flags && (flags[q] & ARMI_FLAG_CERTIFIED)) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* key = reinterpret_cast<double*>(smem);               // [2*cap]
+  int64_t* ord = reinterpret_cast<int64_t*>(smem + 2 * cap * 8);  // [2*cap]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  for (int e = tid; e < 2 * cap; e += 256) {
+    key[e] = kNegInfD;
+    ord[e] = kNoOrd;
+  }
+  int32_t qf[DIM / 64];
+  load_fixed<DIM>(queries + (size_t)q * DIM, lane, qf);
+  const int64_t lo = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t hi = min(lo + rows_per_block, n_rows);
+  __syncthreads();
+  for (int64_t c0 = lo; c0 < hi; c0 += cap) {
+    for (int i = wave; i < cap; i += 4) {
+      const int64_t row = c0 + i;
+      double kk = kNegInfD;
+      int64_t oo = kNoOrd;
+      if (row < hi) {
+        const bool on = (!row_mask || ((row_mask[row >> 6] >> (row & 63)) & 1ull)) && norm2[row] >= 0;
+        if (on) {
+          const int64_t dot = wave_dot_exact<DIM>(qf, rows + (size_t)row * DIM, lane);
+          kk = (double)dot * inv_norm[row];
+          oo = ordinal_base + row;
+        }
+      }
+      if (lane == 0) {
+        key[cap + i] = kk;
+        ord[cap + i] = oo;
+      }
+    }
+    armi::lds_sort_rank_desc(key, ord, 2 * cap);
+  }
+  const size_t base = ((size_t)q * gridDim.x + blockIdx.x) * cap;
+  for (int e = tid; e < cap; e += 256) {
+    ex_key[base + e] = key[e];
+    ex_ord[base + e] = ord[e];
+  }
+}
+
+// Generic merge of sorted-or-unsorted (key, ordinal) lists. Element j of list s for query q
+// sits at s*stride_s + q*stride_q + j; lists hold `width` slots of which counts (nullable)
+// say how many are valid (otherwise ordinal == kNoOrd marks an empty slot).
+// only_uncertified: skip queries whose flag has CERTIFIED, mark the others FALLBACK.
+__global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
+    const double* __restrict__ in_key, const float* __restrict__ in_score,
+    const int64_t* __restrict__ in_ord, const int32_t* __restrict__ in_count,
+    int64_t stride_s, int64_t stride_q, int64_t count_stride_s, int n_lists, int width,
+    int pool2, const double* __restrict__ inv_q, int k_out, double* __restrict__ out_key,
+    float* __restrict__ out_score, int64_t* __restrict__ out_ord, int32_t* __restrict__ out_count,
+    uint32_t* __restrict__ flags, int only_uncertified) {
+  const int q = blockIdx.x;
+  if (only_uncertified && (flags[q] & ARMI_FLAG_CERTIFIED)) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* key = reinterpret_cast<double*>(smem);
+  int64_t* ord = reinterpret_cast<int64_t*>(smem + pool2 * 8);
+  float* sc = reinterpret_cast<float*>(smem + pool2 * 16);
+  const int tid = threadIdx.x;
+  const int pool = n_lists * width;
+  // sort (key, ord) and look scores up afterwards through a (list, slot) payload packed in ord's
+  // companion array: keep scores in LDS addressed by the pooled index.
+  int32_t* src = reinterpret_cast<int32_t*>(smem + pool2 * 20);
+  for (int e = tid; e < pool2; e += kMergeThreads) {
+    double kk = kNegInfD;
+    int64_t oo = kNoOrd;
+    float ss = kNegInf;
+    if (e < pool) {
+      const int s = e / width, j = e % width;
+      const int cnt = in_count ? in_count[(size_t)s * count_stride_s + q] : width;
+      if (j < cnt) {
+        const size_t at = (size_t)s * stride_s + (size_t)q * stride_q + j;
+        oo = in_ord[at];
+        if (oo != kNoOrd && oo >= 0) {
+          kk = in_key[at];
+          ss = in_score ? in_score[at] : 0.0f;
+        } else {
+          oo = kNoOrd;
+        }
+      }
+    }
+    key[e] = kk;
+    ord[e] = oo;
+    sc[e] = ss;
+    src[e] = e;
+  }
+  __syncthreads();
+  // bitonic sort carrying the source index (so scores follow their entry)
+  for (int size = 2; size <= pool2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < pool2 / 2; t += kMergeThreads) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const bool hi_better = armi::rank_better(key[hi], ord[hi], key[lo], ord[lo]);
+        if (hi_better == desc) {
+          const double tk = key[lo]; key[lo] = key[hi]; key[hi] = tk;
+          const int64_t to = ord[lo]; ord[lo] = ord[hi]; ord[hi] = to;
+          const int32_t ts = src[lo]; src[lo] = src[hi]; src[hi] = ts;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  int* s_valid_p = reinterpret_cast<int*>(smem + pool2 * 24);
+  if (tid == 0) {
+    int nv = 0;
+    while (nv < pool2 && nv < k_out && ord[nv] != kNoOrd) ++nv;
+    *s_valid_p = nv;
+  }
+  __syncthreads();
+  const int nv = *s_valid_p;
+  const double iq = inv_q ? inv_q[q] : 0.0;
+  for (int c = tid; c < k_out; c += kMergeThreads) {
+    const size_t o = (size_t)q * k_out + c;
+    if (c < nv) {
+      out_key[o] = key[c];
+      out_ord[o] = ord[c];
+      out_score[o] = in_score ? sc[src[c]] : (float)(key[c] * iq);
+    } else {
+      out_key[o] = kNegInfD;
+      out_ord[o] = -1;
+      out_score[o] = kNegInf;
+    }
+  }
+  if (tid == 0) {
+    out_count[q] = nv;
+    if (only_uncertified) flags[q] = ARMI_FLAG_FALLBACK;
+  }
+}
+
+size_t merge_lds_bytes(int pool2) { return (size_t)pool2 * 24 + 16; }
+
+struct ScanPlan {
+  int n_wg = 0;
+  int tiles_per_wg = 0;
+  int pool2 = 0;
+  int kc = 0;
+};
+
+ScanPlan plan_scan(const armi_index* idx, int k) {
+  ScanPlan p;
+  const int64_t tiles = std::max<int64_t>(idx->n_tiles, 1);
+  const int64_t wgs = std::min<int64_t>(std::min(std::max(idx->num_cus, 1), 256), tiles);
+  p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
+  p.n_wg = (int)((tiles + p.tiles_per_wg - 1) / p.tiles_per_wg);
+  p.pool2 = armi::pow2_at_least(p.n_wg * kKW);
+  p.kc = std::max(4, std::min(armi::pow2_at_least(k + 8), 256));
+  return p;
+}
+
+struct ExactPlan {
+  int cap = 0;
+  int n_blocks = 0;
+  int64_t rows_per_block = 0;
+  int pool2 = 0;
+};
+
+ExactPlan plan_exact(const armi_index* idx, int k) {
+  ExactPlan p;
+  p.cap = std::max(64, armi::pow2_at_least(k));
+  const int max_blocks = std::max(1, kMaxPool / p.cap);
+  const int64_t want = (idx->n_rows + 4095) / 4096;  // >= 4k rows per block
+  p.n_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(max_blocks, want));
+  p.rows_per_block = (idx->n_rows + p.n_blocks - 1) / p.n_blocks;
+  if (p.rows_per_block == 0) p.rows_per_block = 1;
+  p.pool2 = armi::pow2_at_least(p.n_blocks * p.cap);
+  return p;
+}
+
+struct Workspace {
+  float* cand_key;
+  int32_t* cand_row;
+  float* cand_bound;
+  double* inv_q;
+  double* qnorm;
+  double* ex_key;
+  int64_t* ex_ord;
+  size_t bytes;
+};
+
+Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
+  armi::Carver cv(base);
+  Workspace w{};
+  if (fast) {
+    const ScanPlan sp = plan_scan(idx, k);
+    w.cand_key = cv.take<float>((size_t)sp.n_wg * kQB * kKW);
+    w.cand_row = cv.take<int32_t>((size_t)sp.n_wg * kQB * kKW);
+    w.cand_bound = cv.take<float>((size_t)sp.n_wg * kQB);
+  }
+  w.inv_q = cv.take<double>(nq);
+  w.qnorm = cv.take<double>(nq);
+  const ExactPlan ep = plan_exact(idx, k);
+  w.ex_key = cv.take<double>((size_t)nq * ep.n_blocks * ep.cap);
+  w.ex_ord = cv.take<int64_t>((size_t)nq * ep.n_blocks * ep.cap);
+  w.bytes = cv.off + 256;
+  return w;
+}
+
+// Enables > 64 KiB of dynamic LDS for a kernel (once per instantiation).
+template <typename K>
+int allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 65536) return ARMI_OK;
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return ARMI_OK;
+}
+
+// out_rank must be non-null (callers substitute workspace scratch).
+template <int DIM>
+int launch_exact(const armi_index* idx, const uint16_t* queries, int nq, int k,
+                 const uint64_t* row_mask, float* out_scores, int64_t* out_ids, double* out_rank,
+                 int32_t* out_count, uint32_t* flags, int only_uncertified, const Workspace& w,
+                 hipStream_t stream) {
+  const ExactPlan ep = plan_exact(idx, k);
+  const size_t lds_merge = merge_lds_bytes(ep.pool2);
+  if (int rc = allow_lds(merge_lists_kernel, lds_merge)) return rc;
+  dense_exact_scan_kernel<DIM><<<dim3(ep.n_blocks, nq), dim3(256), (size_t)ep.cap * 32, stream>>>(
+      idx->rows, idx->inv_norm, idx->norm2, row_mask, idx->n_rows, ep.rows_per_block, queries,
+      only_uncertified ? flags : nullptr, ep.cap, idx->ordinal_base, w.ex_key, w.ex_ord);
+  ARMI_LAUNCHED("dense_exact_scan_kernel");
+  merge_lists_kernel<<<dim3(nq), dim3(kMergeThreads), lds_merge, stream>>>(
+      w.ex_key, nullptr, w.ex_ord, nullptr, /*stride_s=*/ep.cap,
+      /*stride_q=*/(int64_t)ep.n_blocks * ep.cap, 0, ep.n_blocks, ep.cap, ep.pool2, w.inv_q, k,
+      out_rank, out_scores, out_ids, out_count, flags, only_uncertified);
+  ARMI_LAUNCHED("merge_lists_kernel(exact)");
+  return ARMI_OK;
+}
+
+// Optional live timing of the scan kernel (bench.py's roofline): a HIP event pair around every
+// dense_scan launch while enabled; read back (synchronising) by armi_scan_timing_read.
+struct ScanTiming {
+  bool enabled = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> spare;
+  std::mutex mu;
+};
+ScanTiming& scan_timing() {
+  static ScanTiming t;
+  return t;
+}
+
+int timing_begin(hipStream_t stream, std::pair<hipEvent_t, hipEvent_t>* ev) {
+  ScanTiming& st = scan_timing();
+  std::lock_guard<std::mutex> g(st.mu);
+  if (!st.enabled) return 0;
+  if (st.spare.empty()) {
+    hipEvent_t a, b;
+    ARMI_HIP(hipEventCreate(&a));
+    ARMI_HIP(hipEventCreate(&b));
+    st.spare.emplace_back(a, b);
+  }
+  *ev = st.spare.back();
+  st.spare.pop_back();
+  ARMI_HIP(hipEventRecord(ev->first, stream));
+  return 1;
+}
+
+int timing_end(hipStream_t stream, const std::pair<hipEvent_t, hipEvent_t>& ev) {
+  ScanTiming& st = scan_timing();
+  std::lock_guard<std::mutex> g(st.mu);
+  ARMI_HIP(hipEventRecord(ev.second, stream));
+  st.pending.push_back(ev);
+  return ARMI_OK;
+}
+
+template <int DIM>
+int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int k,
+                    const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                    double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                    const Workspace& w, hipStream_t stream) {
+  const ScanPlan sp = plan_scan(idx, k);
+  if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
+  query_norms_kernel<DIM><<<dim3(nq), dim3(64), 0, stream>>>(queries, nq, w.inv_q, w.qnorm);
+  ARMI_LAUNCHED("query_norms_kernel");
+  for (int q0 = 0; q0 < nq; q0 += kQB) {
+    const int nqp = std::min(kQB, nq - q0);
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    const int timed = timing_begin(stream, &ev);
+    if (timed < 0) return ARMI_ERR_HIP;
+    dense_scan_kernel<DIM><<<dim3(sp.n_wg), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
+        idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
+        queries + (size_t)q0 * DIM, nqp, w.cand_key, w.cand_row, w.cand_bound);
+    ARMI_LAUNCHED("dense_scan_kernel");
+    if (timed == 1)
+      if (int rc = timing_end(stream, ev)) return rc;
+    dense_merge_kernel<DIM><<<dim3(nqp), dim3(kMergeThreads), kMergeLds, stream>>>(
+        w.cand_key, w.cand_row, w.cand_bound, sp.n_wg, q0, idx->rows, idx->inv_norm, queries,
+        w.inv_q, w.qnorm, k, sp.kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
+        out_flags);
+    ARMI_LAUNCHED("dense_merge_kernel");
+  }
+  return launch_exact<DIM>(idx, queries, nq, k, row_mask, out_scores, out_ids, out_rank,
+                           out_count, out_flags, 1, w, stream);
+}
+
+template <typename F>
+int dispatch_dim(int dim, F&& f) {
+  switch (dim) {
+    case 256: return f(std::integral_constant<int, 256>{});
+    case 512: return f(std::integral_constant<int, 512>{});
+    case 768: return f(std::integral_constant<int, 768>{});
+    case 1024: return f(std::integral_constant<int, 1024>{});
+    default: return armi::fail(ARMI_ERR_INVALID, "unsupported dim");
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Workspace layout: [carved buffers][rank scratch nq*k doubles][flags nq u32]
+size_t armi_dense_workspace_bytes(const armi_index* idx, int n_queries, int k) {
+  if (!idx || n_queries <= 0 || k <= 0) return 0;
+  k = std::min(k, kMaxK);
+  const Workspace w = carve(nullptr, idx, n_queries, k, true);
+  return armi::align_up(w.bytes, 256) + armi::align_up((size_t)n_queries * k * 8, 256) +
+         armi::align_up((size_t)n_queries * 4, 256);
+}
+
+int armi_dense_topk(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                    const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                    double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
+                    size_t workspace_bytes, hipStream_t stream) {
+  ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
+  ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
+  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
+  if (n_queries == 0) return ARMI_OK;
+  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && out_flags && workspace,
+               "armi_dense_topk: null pointer argument");
+  ARMI_REQUIRE(workspace_bytes >= armi_dense_workspace_bytes(idx, n_queries, k),
+               "armi_dense_topk: workspace too small");
+  ARMI_HIP(hipSetDevice(idx->device));
+  if (idx->n_rows == 0) {
+    ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
+    ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
+    ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
+    return ARMI_OK;
+  }
+  const Workspace w = carve(workspace, idx, n_queries, k, true);
+  double* rank = out_rank;
+  if (!rank)
+    rank = reinterpret_cast<double*>(static_cast<char*>(workspace) + armi::align_up(w.bytes, 256));
+  return dispatch_dim(idx->dim, [&](auto D) {
+    constexpr int DIM = decltype(D)::value;
+    return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
+                                out_count, out_flags, w, stream);
+  });
+}
+
+size_t armi_dense_exact_workspace_bytes(const armi_index* idx, int n_queries, int k) {
+  if (!idx || n_queries <= 0 || k <= 0) return 0;
+  k = std::min(k, kMaxK);
+  const Workspace w = carve(nullptr, idx, n_queries, k, false);
+  return armi::align_up(w.bytes, 256) + armi::align_up((size_t)n_queries * k * 8, 256) +
+         armi::align_up((size_t)n_queries * 4, 256);
+}
+
+int armi_dense_exact_topk(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                          double* out_rank, int32_t* out_count, void* workspace,
+                          size_t workspace_bytes, hipStream_t stream) {
+  ARMI_REQUIRE(idx != nullptr, "armi_dense_exact_topk: index is null");
+  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_exact_topk: k must be in [1, 240]");
+  if (n_queries <= 0) return ARMI_OK;
+  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && workspace,
+               "armi_dense_exact_topk: null pointer argument");
+  ARMI_REQUIRE(workspace_bytes >= armi_dense_exact_workspace_bytes(idx, n_queries, k),
+               "armi_dense_exact_topk: workspace too small");
+  ARMI_HIP(hipSetDevice(idx->device));
+  if (idx->n_rows == 0) {
+    ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
+    ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
+    return ARMI_OK;
+  }
+  const Workspace w = carve(workspace, idx, n_queries, k, false);
+  char* tail = static_cast<char*>(workspace) + armi::align_up(w.bytes, 256);
+  double* rank = out_rank ? out_rank : reinterpret_cast<double*>(tail);
+  uint32_t* flags =
+      reinterpret_cast<uint32_t*>(tail + armi::align_up((size_t)n_queries * k * 8, 256));
+  ARMI_HIP(hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_queries, stream));
+  return dispatch_dim(idx->dim, [&](auto D) {
+    constexpr int DIM = decltype(D)::value;
+    query_norms_kernel<DIM><<<dim3(n_queries), dim3(64), 0, stream>>>(queries, n_queries,
+                                                                      w.inv_q, w.qnorm);
+    ARMI_LAUNCHED("query_norms_kernel");
+    return launch_exact<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
+                             out_count, flags, 0, w, stream);
+  });
+}
+
+int armi_scan_timing_enable(int enable) {
+  ScanTiming& st = scan_timing();
+  std::lock_guard<std::mutex> g(st.mu);
+  st.enabled = enable != 0;
+  return ARMI_OK;
+}
+
+int armi_scan_timing_read(double* total_ms, int64_t* launches) {
+  ARMI_REQUIRE(total_ms && launches, "armi_scan_timing_read: null pointer argument");
+  ScanTiming& st = scan_timing();
+  std::lock_guard<std::mutex> g(st.mu);
+  double sum = 0.0;
+  for (auto& ev : st.pending) {
+    ARMI_HIP(hipEventSynchronize(ev.second));
+    float ms = 0.f;
+    ARMI_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+    sum += ms;
+    st.spare.push_back(ev);
+  }
+  *total_ms = sum;
+  *launches = (int64_t)st.pending.size();
+  st.pending.clear();
+  return ARMI_OK;
+}
+
+int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const int64_t* in_ids,
+                           const int32_t* in_count, int n_shards, int n_queries, int k_in,
+                           int k_out, double* out_rank, float* out_scores, int64_t* out_ids,
+                           int32_t* out_count, hipStream_t stream) {
+  ARMI_REQUIRE(n_shards >= 1 && k_in >= 1 && k_out >= 1, "armi_topk_merge_shards: bad sizes");
+  ARMI_REQUIRE((int64_t)n_shards * k_in <= kMaxPool,
+               "armi_topk_merge_shards: n_shards * k_in must be <= 4096");
+  if (n_queries <= 0) return ARMI_OK;
+  ARMI_REQUIRE(in_rank && in_scores && in_ids && in_count && out_rank && out_scores && out_ids &&
+                   out_count,
+               "armi_topk_merge_shards: null pointer argument");
+  const int pool2 = armi::pow2_at_least(n_shards * k_in);
+  if (int rc = allow_lds(merge_lists_kernel, merge_lds_bytes(pool2))) return rc;
+  merge_lists_kernel<<<dim3(n_queries), dim3(kMergeThreads), merge_lds_bytes(pool2), stream>>>(
+      in_rank, in_scores, in_ids, in_count, (int64_t)n_queries * k_in, k_in, n_queries, n_shards,
+      k_in, pool2, nullptr, k_out, out_rank, out_scores, out_ids, out_count, nullptr, 0);
+  ARMI_LAUNCHED("merge_lists_kernel(shards)");
+  return ARMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,267 @@
+// Non-GEMM ops of the XLM-RoBERTa cross-encoder that BGEReranker runs through
+// sentence-transformers' CrossEncoder.predict (src/audio_rag/reranking/bge.py:119-123;
+// model BAAI/bge-reranker-base, max_length=512 at bge.py:53; num_labels=1 => sigmoid).
+// fp32 activations, row-major, one wave per row (widths up to 1024, rows up to 512 keys).
+#include <cmath>
+#include <limits>
+
+#include "armi_common.h"
+
+namespace {
+
+constexpr int kMaxPerLane = 16;  // width <= 1024
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+
+// LayerNorm of a row held as kMaxPerLane strided values per lane (two-pass mean / variance,
+// as torch.nn.functional.layer_norm computes it).
+__device__ __forceinline__ void layernorm_row(float (&v)[kMaxPerLane], int width, int lane,
+                                              const float* __restrict__ gamma,
+                                              const float* __restrict__ beta, float eps,
+                                              float* __restrict__ out) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i)
+    if (lane + 64 * i < width) s += v[i];
+  const float mean = wave_sum(s) / (float)width;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i)
+    if (lane + 64 * i < width) {
+      const float d = v[i] - mean;
+      ss += d * d;
+    }
+  const float var = wave_sum(ss) / (float)width;
+  const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i) {
+    const int c = lane + 64 * i;
+    if (c < width) out[c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void layernorm_residual_kernel(
+    const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ out, int64_t n_rows, int width, float eps) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* xr = x + row * width;
+  const float* rr = res ? res + row * width : nullptr;
+  float v[kMaxPerLane];
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = 0.f;
+    if (c < width) v[i] = xr[c] + (rr ? rr[c] : 0.f);
+  }
+  layernorm_row(v, width, lane, gamma, beta, eps, out + row * width);
+}
+
+// scores [n_seq][heads][L][L]; one wave per (seq, head, query row)
+__global__ __launch_bounds__(256) void masked_softmax_kernel(float* __restrict__ scores,
+                                                             const int32_t* __restrict__ mask,
+                                                             int n_seq, int heads, int L,
+                                                             float scale) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t n_rows = (int64_t)n_seq * heads * L;
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int seq = (int)(row / ((int64_t)heads * L));
+  float* p = scores + row * L;
+  const int32_t* m = mask + (int64_t)seq * L;
+  constexpr int kMaxKeys = 512 / 64;
+  float v[kMaxKeys];
+  float mx = -std::numeric_limits<float>::infinity();
+#pragma unroll
+  for (int i = 0; i < kMaxKeys; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = -std::numeric_limits<float>::infinity();
+    if (c < L && m[c] != 0) v[i] = p[c] * scale;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxKeys; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = (c < L && v[i] != -std::numeric_limits<float>::infinity()) ? expf(v[i] - mx) : 0.f;
+    s += v[i];
+  }
+  s = wave_sum(s);
+  const float inv = s > 0.f ? 1.0f / s : 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxKeys; ++i) {
+    const int c = lane + 64 * i;
+    if (c < L) p[c] = v[i] * inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_kernel(float* __restrict__ x,
+                                                        const float* __restrict__ bias,
+                                                        int64_t n, int width) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  float4* p = reinterpret_cast<float4*>(x + i4);
+  float4 v = *p;
+  float e[4] = {v.x, v.y, v.z, v.w};
+  const int c0 = (int)(i4 % width);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float t = e[j] + (bias ? bias[c0 + j] : 0.f);
+    e[j] = 0.5f * t * (1.0f + erff(t * 0.70710678118654752440f));
+  }
+  *p = make_float4(e[0], e[1], e[2], e[3]);
+}
+
+// XLM-R embeddings (transformers create_position_ids_from_input_ids): position id of token t is
+// padding_idx + number of non-pad tokens in [0, t] for a non-pad token, padding_idx for a pad.
+__global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
+                                                    const float* __restrict__ word,
+                                                    const float* __restrict__ pos,
+                                                    const float* __restrict__ type0,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta,
+                                                    float* __restrict__ out, int n_seq, int L,
+                                                    int width, int pad_id, float eps) {
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= (int64_t)n_seq * L) return;
+  const int lane = threadIdx.x & 63;
+  const int seq = (int)(tok / L);
+  const int t = (int)(tok % L);
+  const int32_t* row_ids = ids + (int64_t)seq * L;
+  int count = 0;
+  for (int c0 = 0; c0 <= t; c0 += 64) {
+    const int c = c0 + lane;
+    const bool nonpad = (c <= t) && (row_ids[c] != pad_id);
+    count += __popcll(__ballot(nonpad));
+  }
+  const int id = row_ids[t];
+  const int pid = (id != pad_id) ? pad_id + count : pad_id;
+  const float* w = word + (int64_t)id * width;
+  const float* pp = pos + (int64_t)pid * width;
+  float v[kMaxPerLane];
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = 0.f;
+    if (c < width) v[i] = w[c] + pp[c] + type0[c];
+  }
+  layernorm_row(v, width, lane, gamma, beta, eps, out + tok * width);
+}
+
+// One workgroup per sequence: h = tanh(W1 x0 + b1); logit = w2 . h + b2; out = sigmoid(logit).
+__global__ __launch_bounds__(256) void cls_head_kernel(const float* __restrict__ hidden,
+                                                       const float* __restrict__ dense_w,
+                                                       const float* __restrict__ dense_b,
+                                                       const float* __restrict__ out_w,
+                                                       const float* __restrict__ out_b,
+                                                       float* __restrict__ out, int L,
+                                                       int width) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // [width] x0, [width] h, [4] red
+  const int seq = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const float* x0 = hidden + (int64_t)seq * L * width;
+  float* xs = sh;
+  float* hs = sh + width;
+  float* red = sh + 2 * width;
+  for (int c = threadIdx.x; c < width; c += 256) xs[c] = x0[c];
+  __syncthreads();
+  for (int o = wave; o < width; o += 4) {
+    const float* wr = dense_w + (int64_t)o * width;
+    float s = 0.f;
+    for (int c = lane; c < width; c += 64) s += wr[c] * xs[c];
+    s = wave_sum(s);
+    if (lane == 0) hs[o] = tanhf(s + dense_b[o]);
+  }
+  __syncthreads();
+  float s = 0.f;
+  for (int c = threadIdx.x; c < width; c += 256) s += out_w[c] * hs[c];
+  s = wave_sum(s);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float logit = red[0] + red[1] + red[2] + red[3] + out_b[0];
+    out[seq] = 1.0f / (1.0f + expf(-logit));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int armi_enc_layernorm_residual(const float* x, const float* res, const float* gamma,
+                                const float* beta, float* out, int64_t n_rows, int width,
+                                float eps, hipStream_t stream) {
+  ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane, "layernorm: width must be in [1, 1024]");
+  if (n_rows <= 0) return ARMI_OK;
+  ARMI_REQUIRE(x && gamma && beta && out, "layernorm: null pointer argument");
+  layernorm_residual_kernel<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, stream>>>(
+      x, res, gamma, beta, out, n_rows, width, eps);
+  ARMI_LAUNCHED("layernorm_residual_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_masked_softmax(float* scores, const int32_t* mask, int n_seq, int heads, int L,
+                            float scale, hipStream_t stream) {
+  ARMI_REQUIRE(L >= 1 && L <= 512, "masked_softmax: L must be in [1, 512]");
+  if (n_seq <= 0 || heads <= 0) return ARMI_OK;
+  ARMI_REQUIRE(scores && mask, "masked_softmax: null pointer argument");
+  const int64_t rows = (int64_t)n_seq * heads * L;
+  masked_softmax_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream>>>(
+      scores, mask, n_seq, heads, L, scale);
+  ARMI_LAUNCHED("masked_softmax_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_bias_gelu(float* x, const float* bias, int64_t n_rows, int width,
+                       hipStream_t stream) {
+  ARMI_REQUIRE(width >= 4 && width % 4 == 0, "bias_gelu: width must be a multiple of 4");
+  if (n_rows <= 0) return ARMI_OK;
+  ARMI_REQUIRE(x != nullptr, "bias_gelu: x is null");
+  const int64_t n = n_rows * width;
+  bias_gelu_kernel<<<dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, stream>>>(x, bias, n,
+                                                                                     width);
+  ARMI_LAUNCHED("bias_gelu_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
+                   const float* gamma, const float* beta, float* out, int n_seq, int L,
+                   int width, int pad_id, float eps, hipStream_t stream) {
+  ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane, "embed: width must be in [1, 1024]");
+  ARMI_REQUIRE(L >= 1, "embed: L must be >= 1");
+  if (n_seq <= 0) return ARMI_OK;
+  ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
+               "embed: null pointer argument");
+  const int64_t toks = (int64_t)n_seq * L;
+  embed_kernel<<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
+      ids, word, pos, type0, gamma, beta, out, n_seq, L, width, pad_id, eps);
+  ARMI_LAUNCHED("embed_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const float* dense_b,
+                              const float* out_w, const float* out_b, float* out, int n_seq,
+                              int L, int width, hipStream_t stream) {
+  ARMI_REQUIRE(width >= 1 && width <= 4096, "cls_head: width must be in [1, 4096]");
+  if (n_seq <= 0) return ARMI_OK;
+  ARMI_REQUIRE(hidden && dense_w && dense_b && out_w && out_b && out,
+               "cls_head: null pointer argument");
+  cls_head_kernel<<<dim3(n_seq), dim3(256), (size_t)(2 * width + 4) * sizeof(float), stream>>>(
+      hidden, dense_w, dense_b, out_w, out_b, out, L, width);
+  ARMI_LAUNCHED("cls_head_kernel");
+  return ARMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+// Dense chunk-store construction: validation and exact per-row norms.
+//
+// Reference behaviour restated: Qdrant's COSINE distance normalises every vector at insert
+// (QdrantRetriever._ensure_collection, src/audio_rag/retrieval/qdrant.py:93-109, and the
+// per-point upserts of QdrantRetriever.add, qdrant.py:183-220). Instead of storing a rounded
+// normalised copy, the store keeps the fp16 vector the encoder produced and an exact norm, so
+// the search ranks by the exact cosine of those fp16 values.
+#include <cmath>
+
+#include "armi_index.h"
+
+namespace {
+
+// One wave per row: exact int64 sum of squares of the fixed-point (x * 2^24) image.
+__global__ __launch_bounds__(256) void row_norms_kernel(const uint16_t* __restrict__ rows,
+                                                        int64_t n_rows, int64_t n_padded,
+                                                        int dim, int64_t* __restrict__ norm2,
+                                                        double* __restrict__ inv_norm,
+                                                        float* __restrict__ inv_norm32,
+                                                        unsigned long long* __restrict__ invalid) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_padded) return;
+  if (row >= n_rows) {  // tile padding: never a result
+    if (lane == 0) {
+      norm2[row] = -1;
+      inv_norm[row] = 0.0;
+      inv_norm32[row] = __builtin_nanf("");
+    }
+    return;
+  }
+  const uint16_t* src = rows + row * (int64_t)dim;
+  int64_t acc = 0;
+  bool ok = true;
+  for (int i = lane; i < dim; i += 64) {
+    const uint32_t h = src[i];
+    ok &= armi::fp16_in_domain(h);
+    const int64_t v = armi::fp16_to_fixed24(h);
+    acc += v * v;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const bool row_ok = __all(ok);
+  if (lane == 0) {
+    if (!row_ok) {
+      norm2[row] = -1;
+      inv_norm[row] = 0.0;
+      inv_norm32[row] = __builtin_nanf("");
+      atomicAdd(invalid, 1ull);
+    } else {
+      norm2[row] = acc;
+      const double inv = acc > 0 ? 1.0 / sqrt((double)acc) : 0.0;
+      inv_norm[row] = inv;
+      inv_norm32[row] = (float)(inv * 16777216.0);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
+                      int64_t ordinal_base, armi_index** out, hipStream_t stream) {
+  ARMI_REQUIRE(out != nullptr, "armi_index_create: out is null");
+  *out = nullptr;
+  ARMI_REQUIRE(rows != nullptr || n_rows == 0, "armi_index_create: rows is null");
+  ARMI_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31) - 64,
+               "armi_index_create: n_rows must be in [0, 2^31 - 64)");
+  ARMI_REQUIRE(dim == 256 || dim == 512 || dim == 768 || dim == 1024,
+               "armi_index_create: dim must be 256, 512, 768 or 1024");
+  ARMI_HIP(hipSetDevice(device));
+  armi_index* idx = new armi_index();
+  idx->device = device;
+  idx->rows = rows;
+  idx->n_rows = n_rows;
+  idx->n_tiles = (n_rows + armi::TILE_ROWS - 1) / armi::TILE_ROWS;
+  idx->dim = dim;
+  idx->ordinal_base = ordinal_base;
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) { delete idx; return armi::hip_fail(e, "hipGetDeviceProperties"); }
+  idx->num_cus = prop.multiProcessorCount;
+  const int64_t padded = std::max<int64_t>(idx->n_tiles * armi::TILE_ROWS, 1);
+  e = hipMalloc(&idx->norm2, padded * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&idx->inv_norm, padded * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&idx->inv_norm32, padded * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&idx->invalid, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemsetAsync(idx->invalid, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "armi_index_create alloc"); }
+  const int64_t blocks = (padded + 3) / 4;
+  row_norms_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+      rows, n_rows, padded, dim, idx->norm2, idx->inv_norm, idx->inv_norm32, idx->invalid);
+  e = hipGetLastError();
+  if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "row_norms_kernel"); }
+  *out = idx;
+  return ARMI_OK;
+}
+
+int armi_index_destroy(armi_index* idx) {
+  if (!idx) return ARMI_OK;
+  hipFree(idx->norm2);
+  hipFree(idx->inv_norm);
+  hipFree(idx->inv_norm32);
+  hipFree(idx->invalid);
+  delete idx;
+  return ARMI_OK;
+}
+
+int64_t armi_index_rows(const armi_index* idx) { return idx ? idx->n_rows : -1; }
+
+int armi_index_dim(const armi_index* idx) { return idx ? idx->dim : -1; }
+
+int64_t armi_index_invalid_rows(const armi_index* idx) {
+  if (!idx) return -1;
+  unsigned long long v = 0;
+  if (hipMemcpy(&v, idx->invalid, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (int64_t)v;
+}
+
+int armi_index_norms(const armi_index* idx, const int64_t** norm2, const double** inv_norm,
+                     const float** inv_norm32) {
+  ARMI_REQUIRE(idx != nullptr, "armi_index_norms: index is null");
+  if (norm2) *norm2 = idx->norm2;
+  if (inv_norm) *inv_norm = idx->inv_norm;
+  if (inv_norm32) *inv_norm32 = idx->inv_norm32;
+  return ARMI_OK;
+}
+
+}  // extern "C"

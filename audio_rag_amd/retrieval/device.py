@@ -1,0 +1,242 @@
+"""Device-side chunk-store handles over libarmi (torch tensors in, torch tensors out).
+
+Everything here runs on the GPU through the C ABI in include/armi.h; torch only provides device
+memory and the stream. Results stay on the device until the caller materialises them.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from audio_rag_amd import _armi
+from audio_rag_amd._armi import call, ptr, query, stream_handle
+
+MAX_K = 240
+QUERY_BLOCK = 64  # queries per scan pass of armi_dense_topk
+
+
+@dataclass
+class TopK:
+    """Per-query top-k on the device. ids are chunk ordinals (-1 past count)."""
+
+    scores: torch.Tensor  # float32 [B, k]
+    ids: torch.Tensor     # int64   [B, k]
+    rank: torch.Tensor    # float64 [B, k] ranking key (dense only; RRF score for fused lists)
+    count: torch.Tensor   # int32   [B]
+    flags: torch.Tensor | None = None  # int32 [B] ARMI_FLAG_* bits (dense only)
+
+
+def _check_fp16_2d(t: torch.Tensor, name: str, dim: int | None = None) -> None:
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.float16 or t.dim() != 2:
+        raise ValueError(f"{name} must be a 2-D float16 tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must live on the GPU")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dim is not None and t.shape[1] != dim:
+        raise ValueError(f"{name} has dim {t.shape[1]}, index has {dim}")
+
+
+class DenseIndex:
+    """The Qdrant named vector "dense" (VectorParams(size=dim, distance=COSINE)) of
+    src/audio_rag/retrieval/qdrant.py:93-109, as an fp16 row store in HBM.
+
+    rows: [N, dim] float16 on the device (kept alive by this object)."""
+
+    def __init__(self, rows: torch.Tensor, ordinal_base: int = 0):
+        _check_fp16_2d(rows, "rows")
+        self.rows = rows
+        self.dim = int(rows.shape[1])
+        self.n_rows = int(rows.shape[0])
+        self.ordinal_base = int(ordinal_base)
+        self.device = rows.device
+        self._handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("armi_index_create", self.device.index or 0, ptr(rows), self.n_rows, self.dim,
+                 self.ordinal_base, ctypes.byref(self._handle), stream_handle())
+
+    def close(self) -> None:
+        if self._handle and self._handle.value:
+            torch.cuda.synchronize(self.device)
+            _armi.call("armi_index_destroy", self._handle)
+            self._handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._handle
+
+    def invalid_rows(self) -> int:
+        torch.cuda.current_stream(self.device).synchronize()
+        return int(query("armi_index_invalid_rows", self._handle))
+
+    def norms(self) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(norm2 int64, inv_norm float64, inv_norm32 float32) copies of the index's arrays."""
+        p2, pi, p32 = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        call("armi_index_norms", self._handle, ctypes.byref(p2), ctypes.byref(pi), ctypes.byref(p32))
+        n = self.n_rows
+        out = (torch.empty(n, dtype=torch.int64, device=self.device),
+               torch.empty(n, dtype=torch.float64, device=self.device),
+               torch.empty(n, dtype=torch.float32, device=self.device))
+        torch.cuda.current_stream(self.device).synchronize()
+        for src, dst in zip((p2, pi, p32), out):
+            _device_copy(dst.data_ptr(), src.value, dst.numel() * dst.element_size())
+        return out
+
+    def workspace_bytes(self, n_queries: int, k: int, exact: bool = False) -> int:
+        fn = "armi_dense_exact_workspace_bytes" if exact else "armi_dense_workspace_bytes"
+        return int(query(fn, self._handle, n_queries, k))
+
+    def topk(self, queries: torch.Tensor, k: int, row_mask: torch.Tensor | None = None,
+             exact: bool = False, workspace: torch.Tensor | None = None,
+             out: TopK | None = None) -> TopK:
+        """Cosine top-k of every query row. row_mask: int64 tensor holding a bitmask of enabled
+        rows (bit r of word r // 64), or None."""
+        _check_fp16_2d(queries, "queries", self.dim)
+        if not 1 <= k <= MAX_K:
+            raise ValueError(f"k must be in [1, {MAX_K}]")
+        b = int(queries.shape[0])
+        dev = self.device
+        if row_mask is not None:
+            need = (self.n_rows + 63) // 64
+            if row_mask.dtype != torch.int64 or row_mask.numel() < need or not row_mask.is_cuda:
+                raise ValueError(f"row_mask must be an int64 device tensor of >= {need} words")
+        if out is None:
+            out = TopK(scores=torch.empty((b, k), dtype=torch.float32, device=dev),
+                       ids=torch.empty((b, k), dtype=torch.int64, device=dev),
+                       rank=torch.empty((b, k), dtype=torch.float64, device=dev),
+                       count=torch.empty(b, dtype=torch.int32, device=dev),
+                       flags=torch.empty(b, dtype=torch.int32, device=dev))
+        need = self.workspace_bytes(max(b, 1), k, exact)
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        s = stream_handle()
+        if exact:
+            call("armi_dense_exact_topk", self._handle, ptr(queries), b, k, ptr(row_mask),
+                 ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(workspace),
+                 workspace.numel(), s)
+            if out.flags is not None:
+                out.flags.fill_(_armi.ARMI_FLAG_FALLBACK)
+        else:
+            call("armi_dense_topk", self._handle, ptr(queries), b, k, ptr(row_mask),
+                 ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(out.flags),
+                 ptr(workspace), workspace.numel(), s)
+        return out
+
+
+class SparseIndex:
+    """The Qdrant sparse vector "sparse" (SparseVectorParams(index=SparseIndexParams(on_disk=
+    False)), no IDF modifier) of src/audio_rag/retrieval/qdrant.py:103-107, as a CSR in HBM.
+
+    indptr int64 [N+1], indices int32 (ascending within a row), values float32; device tensors
+    kept alive by this object."""
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                 vocab: int, ordinal_base: int = 0):
+        for t, dt, name in ((indptr, torch.int64, "indptr"), (indices, torch.int32, "indices"),
+                            (values, torch.float32, "values")):
+            if t.dtype != dt or t.dim() != 1 or not t.is_cuda or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous 1-D {dt} device tensor")
+        self.indptr, self.indices, self.values = indptr, indices, values
+        self.n_rows = int(indptr.numel()) - 1
+        self.vocab = int(vocab)
+        self.ordinal_base = int(ordinal_base)
+        self.device = indptr.device
+        self._handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("armi_sparse_index_create", self.device.index or 0, ptr(indptr), ptr(indices),
+                 ptr(values), self.n_rows, int(indices.numel()), self.vocab, self.ordinal_base,
+                 ctypes.byref(self._handle), stream_handle())
+
+    def close(self) -> None:
+        if self._handle and self._handle.value:
+            torch.cuda.synchronize(self.device)
+            _armi.call("armi_sparse_index_destroy", self._handle)
+            self._handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def workspace_bytes(self, n_queries: int, k: int) -> int:
+        return int(query("armi_sparse_workspace_bytes", self._handle, n_queries, k))
+
+    def topk(self, q_indptr: torch.Tensor, q_indices: torch.Tensor, q_values: torch.Tensor, k: int,
+             row_mask: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> TopK:
+        """Sparse dot top-k for a query CSR (q_indptr int32 [B+1], ascending q_indices int32,
+        q_values float32, all on the device)."""
+        if not 1 <= k <= MAX_K:
+            raise ValueError(f"k must be in [1, {MAX_K}]")
+        b = int(q_indptr.numel()) - 1
+        dev = self.device
+        out = TopK(scores=torch.empty((b, k), dtype=torch.float32, device=dev),
+                   ids=torch.empty((b, k), dtype=torch.int64, device=dev),
+                   rank=torch.empty((0,), dtype=torch.float64, device=dev),
+                   count=torch.empty(b, dtype=torch.int32, device=dev),
+                   flags=torch.empty(b, dtype=torch.int32, device=dev))
+        if b == 0:
+            return out
+        need = self.workspace_bytes(b, k)
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        call("armi_sparse_topk", self._handle, ptr(q_indptr), ptr(q_indices), ptr(q_values), b, k,
+             ptr(row_mask), ptr(out.scores), ptr(out.ids), ptr(out.count), ptr(out.flags),
+             ptr(workspace), workspace.numel(), stream_handle())
+        out.rank = out.scores.double()
+        return out
+
+
+def merge_shards(rank: torch.Tensor, scores: torch.Tensor, ids: torch.Tensor, count: torch.Tensor,
+                 k_out: int) -> TopK:
+    """Global top-k from per-shard lists [S, B, k_in] (+ count [S, B]) gathered from all ranks."""
+    s, b, k_in = ids.shape
+    dev = ids.device
+    out = TopK(scores=torch.empty((b, k_out), dtype=torch.float32, device=dev),
+               ids=torch.empty((b, k_out), dtype=torch.int64, device=dev),
+               rank=torch.empty((b, k_out), dtype=torch.float64, device=dev),
+               count=torch.empty(b, dtype=torch.int32, device=dev))
+    call("armi_topk_merge_shards", ptr(rank.contiguous()), ptr(scores.contiguous()),
+         ptr(ids.contiguous()), ptr(count.contiguous()), s, b, k_in, k_out, ptr(out.rank),
+         ptr(out.scores), ptr(out.ids), ptr(out.count), stream_handle())
+    return out
+
+
+def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
+    """FusionQuery(RRF) of two prefetch lists (qdrant.py:295). rank/scores hold the fp64 RRF
+    score (scores as float32 for convenience)."""
+    n, ka = a.ids.shape
+    kb = b.ids.shape[1]
+    dev = a.ids.device
+    out_ids = torch.empty((n, limit), dtype=torch.int64, device=dev)
+    out_score = torch.empty((n, limit), dtype=torch.float64, device=dev)
+    out_count = torch.empty(n, dtype=torch.int32, device=dev)
+    call("armi_rrf_fuse", ptr(a.ids.contiguous()), ptr(a.count), ka, ptr(b.ids.contiguous()),
+         ptr(b.count), kb, n, rrf_k, limit, ptr(out_ids), ptr(out_score), ptr(out_count),
+         stream_handle())
+    return TopK(scores=out_score.float(), ids=out_ids, rank=out_score, count=out_count)
+
+
+_hip = None
+
+
+def _device_copy(dst: int, src: int, nbytes: int) -> None:
+    """Synchronous device-to-device copy through the process's HIP runtime (the one torch
+    loaded), for reading the index's internal arrays in tests."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.restype = ctypes.c_int
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rc = _hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3)  # DeviceToDevice
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed: {rc}")

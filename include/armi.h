@@ -1,0 +1,197 @@
+/*
+ * armi.h — C ABI of libarmi.so, the MI355X (gfx950) retrieval hot path of audio-rag.
+ *
+ * Each entry point replaces one piece of arithmetic that the reference delegates to a
+ * third-party engine (all paths relative to the reference checkout):
+ *
+ *   armi_index_create / armi_index_destroy
+ *       the Qdrant named vector "dense" = VectorParams(size=dim, distance=COSINE), filled by
+ *       QdrantRetriever.add   src/audio_rag/retrieval/qdrant.py:93-109, 140-225
+ *   armi_dense_topk
+ *       Qdrant COSINE query_points(query=dense, using="dense", limit=k) and the dense
+ *       Prefetch(limit=2*top_k) of hybrid search     src/audio_rag/retrieval/qdrant.py:284-288, 316-332
+ *   armi_dense_exact_topk
+ *       the same ranking computed by an exhaustive exact scan (fallback + test reference path)
+ *   armi_sparse_*
+ *       Qdrant sparse vector "sparse" (SparseVectorParams, no IDF modifier) and the sparse
+ *       Prefetch / sparse query_points               src/audio_rag/retrieval/qdrant.py:103-107, 289-293, 299-312
+ *   armi_rrf_fuse
+ *       FusionQuery(fusion=Fusion.RRF)               src/audio_rag/retrieval/qdrant.py:295
+ *   armi_topk_merge_shards
+ *       the merge step that follows the RCCL all-gather of per-shard candidates (no reference
+ *       counterpart: the reference runs one Qdrant replica, k8s/helm/audio-rag/values.yaml:137)
+ *   armi_enc_*
+ *       the non-GEMM ops of the XLM-RoBERTa cross-encoder behind CrossEncoder.predict
+ *                                                    src/audio_rag/reranking/bge.py:119-123
+ *
+ * Conventions
+ *   - Every function returns ARMI_OK (0) or a positive error code; the message of the last
+ *     failure on the calling thread is returned by armi_last_error(). No C++ exception crosses
+ *     this boundary.
+ *   - Every array argument is caller-owned DEVICE memory unless the comment says "host".
+ *   - Every launch is asynchronous and ordered on the given stream; nothing synchronises the
+ *     host (graph capture safe). Workspaces are caller-allocated (see *_workspace_bytes).
+ *   - An index is immutable after armi_index_create returns; any number of streams may search
+ *     one index concurrently, each with its own workspace.
+ *   - fp16 values are passed as their IEEE binary16 bit patterns (uint16_t).
+ */
+#ifndef ARMI_H
+#define ARMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARMI_OK 0
+#define ARMI_ERR_INVALID 1     /* bad argument (shape, null pointer, unsupported size) */
+#define ARMI_ERR_HIP 2         /* a HIP runtime call failed */
+#define ARMI_ERR_UNSUPPORTED 3 /* valid request that this build does not implement */
+
+#define ARMI_ABI_VERSION 1
+
+/* flags written per query by the top-k entry points */
+#define ARMI_FLAG_CERTIFIED 1u /* fast path proved its top-k equal to the exact ranking */
+#define ARMI_FLAG_FALLBACK 2u  /* fast path could not prove it; exact scan produced the answer */
+
+const char* armi_last_error(void);
+int armi_abi_version(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Dense chunk store                                                                          */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct armi_index armi_index;
+
+/* rows: [n_rows][dim] fp16, row-major, caller-owned, must outlive the index.
+ * Every component must be finite with |x| < 2 (BGE-M3 emits unit vectors); rows that violate
+ * this are counted in armi_index_invalid_rows() and score as -inf.
+ * dim must be 256, 512, 768 or 1024. ordinal_base is added to every row index to form
+ * the chunk ordinal that the search functions return (corpus shards use base = first row). */
+int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
+                      int64_t ordinal_base, armi_index** out, hipStream_t stream);
+int armi_index_destroy(armi_index* index);
+int64_t armi_index_rows(const armi_index* index);
+int armi_index_dim(const armi_index* index);
+/* number of rows that failed validation (reads back a device counter: synchronises) */
+int64_t armi_index_invalid_rows(const armi_index* index);
+/* device pointers of the per-row norm arrays built at create time:
+ *   norm2[r]     = sum_i (2^24 * x_ri)^2 as an exact int64
+ *   inv_norm[r]  = 1.0 / sqrt((double) norm2[r])       (0.0 for a zero row)
+ *   inv_norm32[r]= (float)(inv_norm[r] * 2^24)          (scale factor of the fast scan) */
+int armi_index_norms(const armi_index* index, const int64_t** norm2, const double** inv_norm,
+                     const float** inv_norm32);
+
+/* Workspace bytes needed by armi_dense_topk for n_queries queries and top-k. */
+size_t armi_dense_workspace_bytes(const armi_index* index, int n_queries, int k);
+
+/* Cosine top-k over the index.
+ *   queries    [n_queries][dim] fp16 (same component rule as rows)
+ *   k          1..240
+ *   row_mask   nullable; bit r of the uint64 bitmask enables row r (metadata pre-filter)
+ * outputs, each [n_queries][k]:
+ *   out_scores  float cosine score (reference: hit.score, an fp32 dot of normalised vectors)
+ *   out_ids     int64 chunk ordinal (ordinal_base + row); -1 past out_count
+ *   out_rank    nullable double ranking key; the ranking is (key desc, ordinal asc)
+ *   out_count   [n_queries] number of valid results (< k when fewer rows are enabled)
+ *   out_flags   [n_queries] ARMI_FLAG_* bits
+ * The result is the exact ranking of the fp16 inputs: key = (double)dot64 * inv_norm[row] where
+ * dot64 = sum_i (2^24 q_i)(2^24 x_ri) is an exact int64 dot product. */
+int armi_dense_topk(const armi_index* index, const uint16_t* queries, int n_queries, int k,
+                    const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                    double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                    void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+size_t armi_dense_exact_workspace_bytes(const armi_index* index, int n_queries, int k);
+/* Exhaustive exact scan with the same outputs and ranking as armi_dense_topk. */
+int armi_dense_exact_topk(const armi_index* index, const uint16_t* queries, int n_queries, int k,
+                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                          double* out_rank, int32_t* out_count, void* workspace,
+                          size_t workspace_bytes, hipStream_t stream);
+
+/* Merge per-shard top-k lists (after an all-gather) into the global top-k.
+ *   in_*: [n_shards][n_queries][k_in], in_count [n_shards][n_queries]
+ *   ranking (key desc, ordinal asc); outputs [n_queries][k_out] + out_count. */
+int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const int64_t* in_ids,
+                           const int32_t* in_count, int n_shards, int n_queries, int k_in,
+                           int k_out, double* out_rank, float* out_scores, int64_t* out_ids,
+                           int32_t* out_count, hipStream_t stream);
+
+/* Live timing of the dense scan kernel for roofline reporting: while enabled, every
+ * dense_scan launch is bracketed by a HIP event pair on its stream. _read synchronises on the
+ * recorded events, returns the summed kernel time and launch count, and clears them. */
+int armi_scan_timing_enable(int enable);
+int armi_scan_timing_read(double* total_ms, int64_t* launches);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Sparse (lexical-weight) store                                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct armi_sparse_index armi_sparse_index;
+
+/* CSR corpus: indptr [n_rows+1] int64, indices [nnz] int32 (strictly ascending per row),
+ * values [nnz] float. Caller-owned, must outlive the index. */
+int armi_sparse_index_create(int device, const int64_t* indptr, const int32_t* indices,
+                             const float* values, int64_t n_rows, int64_t nnz, int32_t vocab,
+                             int64_t ordinal_base, armi_sparse_index** out, hipStream_t stream);
+int armi_sparse_index_destroy(armi_sparse_index* index);
+
+size_t armi_sparse_workspace_bytes(const armi_sparse_index* index, int n_queries, int k);
+/* Sparse dot-product top-k. Query CSR: q_indptr [n_queries+1] int32 (absolute offsets),
+ * q_indices ascending int32 (at most 256 per query; more set flag bit 8), q_values float.
+ * out_flags: ARMI_FLAG_CERTIFIED (merged lists proved exact) or ARMI_FLAG_FALLBACK (answer from
+ * the collecting rescan; bit 4 = more than 4096 rows tied at the threshold, answer truncated). score = sum over shared indices, ascending index order, of
+ * fl32(q*d) accumulated in fp32 (mul and add rounded separately). Only rows that share at
+ * least one index with the query are results. Ranking (score desc, ordinal asc). */
+int armi_sparse_topk(const armi_sparse_index* index, const int32_t* q_indptr,
+                     const int32_t* q_indices, const float* q_values, int n_queries, int k,
+                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                     int32_t* out_count, uint32_t* out_flags, void* workspace,
+                     size_t workspace_bytes, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Reciprocal-rank fusion                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+
+/* For each query: score[id] = sum over the two lists of 1/(rrf_k + pos) (pos 0-based, fp64,
+ * list a added first), sorted by score descending; ties keep first-seen order (all of list a in
+ * order, then the ids only in list b in order). Lists hold ka / kb slots per query, of which
+ * a_count / b_count are valid. Outputs [n_queries][limit] + out_count. */
+int armi_rrf_fuse(const int64_t* a_ids, const int32_t* a_count, int ka, const int64_t* b_ids,
+                  const int32_t* b_count, int kb, int n_queries, int rrf_k, int limit,
+                  int64_t* out_ids, double* out_scores, int32_t* out_count, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Cross-encoder (XLM-RoBERTa) non-GEMM ops; all activations fp32 row-major                    */
+/* ------------------------------------------------------------------------------------------ */
+
+/* out[t] = LayerNorm(x[t] + res[t]) * gamma + beta over the last dim (res nullable). */
+int armi_enc_layernorm_residual(const float* x, const float* res, const float* gamma,
+                                const float* beta, float* out, int64_t n_rows, int width,
+                                float eps, hipStream_t stream);
+/* in-place softmax over the last dim of scores [n_seq][heads][L][L] scaled by `scale`,
+ * keys with mask[seq][key] == 0 excluded. */
+int armi_enc_masked_softmax(float* scores, const int32_t* mask, int n_seq, int heads, int L,
+                            float scale, hipStream_t stream);
+/* in-place exact (erf) GELU of x + bias[col]; bias nullable. */
+int armi_enc_bias_gelu(float* x, const float* bias, int64_t n_rows, int width,
+                       hipStream_t stream);
+/* XLM-R embeddings: word[ids] + pos[padding_idx + cumsum(ids != pad)] + type[0], then
+ * LayerNorm. ids [n_seq][L] int32. */
+int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
+                   const float* gamma, const float* beta, float* out, int n_seq, int L,
+                   int width, int pad_id, float eps, hipStream_t stream);
+/* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)
+ * hidden [n_seq][L][width] -> out [n_seq]. */
+int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const float* dense_b,
+                              const float* out_w, const float* out_b, float* out, int n_seq,
+                              int L, int width, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ARMI_H */

@@ -1,0 +1,175 @@
+"""Dense cosine top-k on the GPU (armi_dense_topk) against the CPU oracle.
+
+Parity bar (integer / index work): ids, counts and the float64 ranking key must be bit-identical
+to oracle.dense_topk; scores are the float32 cast of key * inv_q on both sides, also bitwise.
+Reference call sites: src/audio_rag/retrieval/qdrant.py:284-288 (dense prefetch) and 316-332.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _index(rows_u16, gpu, base=0):
+    from audio_rag_amd.retrieval.device import DenseIndex
+
+    t = _dev(rows_u16.view(np.float16), gpu)
+    return DenseIndex(t, ordinal_base=base)
+
+
+def _run(idx, q_u16, k, gpu, mask=None, exact=False):
+    q = _dev(q_u16.view(np.float16), gpu)
+    m = None if mask is None else _dev(mask.view(np.int64), gpu)
+    out = idx.topk(q, k, row_mask=m, exact=exact)
+    torch.cuda.synchronize()
+    return {f: getattr(out, f).cpu().numpy() for f in ("ids", "scores", "rank", "count", "flags")}
+
+
+def _assert_same(got, ref, k):
+    np.testing.assert_array_equal(got["count"], ref.count)
+    for b in range(ref.count.shape[0]):
+        c = ref.count[b]
+        np.testing.assert_array_equal(got["ids"][b, :c], ref.ids[b, :c], err_msg=f"query {b}")
+        np.testing.assert_array_equal(got["rank"][b, :c], ref.rank[b, :c], err_msg=f"query {b}")
+        np.testing.assert_array_equal(got["scores"][b, :c], ref.scores[b, :c], err_msg=f"query {b}")
+        assert (got["ids"][b, c:] == -1).all()
+
+
+@pytest.mark.parametrize("dim", [256, 1024])
+def test_norms_bitwise(gpu, oracle_mod, dim):
+    rows = oracle_mod.unit_fp16(777, dim, seed=3)
+    idx = _index(rows, gpu)
+    n2, inv, inv32 = (t.cpu().numpy() for t in idx.norms())
+    o2, oinv = oracle_mod.row_norms(rows, dim)
+    np.testing.assert_array_equal(n2, o2)
+    np.testing.assert_array_equal(inv, oinv)  # GPU f64 sqrt/div must round like IEEE
+    np.testing.assert_array_equal(inv32, (oinv * 2.0**24).astype(np.float32))
+
+
+@pytest.mark.parametrize("n,dim,b,k", [
+    (1000, 256, 8, 5), (4099, 1024, 16, 5), (20000, 1024, 64, 40), (3001, 512, 70, 20),
+    (50, 768, 3, 5), (5, 256, 4, 8), (1, 1024, 2, 5)])
+def test_dense_topk_matches_oracle(gpu, oracle_mod, n, dim, b, k):
+    rows = oracle_mod.unit_fp16(n, dim, seed=10 + n)
+    qs = oracle_mod.unit_fp16(b, dim, seed=11 + n)
+    idx = _index(rows, gpu, base=1000)
+    got = _run(idx, qs, k, gpu)
+    ref = oracle_mod.dense_topk(rows, qs, k, ordinal_base=1000)
+    _assert_same(got, ref, k)
+
+
+def test_fast_path_certifies(gpu, oracle_mod):
+    """The MFMA scan + exact rescore must certify random queries itself (the exact fallback
+    would otherwise hide a broken fast path)."""
+    rows = oracle_mod.unit_fp16(60000, 1024, seed=5)
+    qs = oracle_mod.unit_fp16(64, 1024, seed=6)
+    idx = _index(rows, gpu)
+    for k in (5, 40):
+        got = _run(idx, qs, k, gpu)
+        assert (got["flags"] == 1).all(), got["flags"]
+        ref = oracle_mod.dense_topk(rows, qs, k)
+        _assert_same(got, ref, k)
+
+
+def test_exact_entry_point(gpu, oracle_mod):
+    rows = oracle_mod.unit_fp16(9000, 1024, seed=7)
+    qs = oracle_mod.unit_fp16(5, 1024, seed=8)
+    idx = _index(rows, gpu)
+    got = _run(idx, qs, 33, gpu, exact=True)
+    _assert_same(got, oracle_mod.dense_topk(rows, qs, 33), 33)
+
+
+def test_row_mask_and_invalid_rows(gpu, oracle_mod):
+    n = 5000
+    rows = oracle_mod.unit_fp16(n, 256, seed=9).copy()
+    rows[17, 3] = 0x7C00  # +inf: outside the fp16 domain -> never a result
+    rows[4000, 0] = 0x4400  # 4.0: |x| >= 2 -> invalid
+    qs = oracle_mod.unit_fp16(6, 256, seed=10)
+    rng = np.random.default_rng(0)
+    bits = rng.random(n) < 0.3
+    mask = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in np.nonzero(bits)[0]:
+        mask[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    idx = _index(rows, gpu)
+    assert idx.invalid_rows() == 2
+    got = _run(idx, qs, 12, gpu, mask=mask)
+    ref = oracle_mod.dense_topk(rows, qs, 12, row_mask=mask)
+    _assert_same(got, ref, 12)
+    assert not np.isin(got["ids"], [17, 4000]).any()
+
+
+def test_few_enabled_rows_and_exact_ties(gpu, oracle_mod):
+    rows = oracle_mod.unit_fp16(3000, 1024, seed=12).copy()
+    rows[100:140] = rows[7]  # 41 identical rows: exact key ties broken by ordinal
+    qs = np.vstack([rows[7], oracle_mod.unit_fp16(3, 1024, seed=13)])
+    idx = _index(rows, gpu)
+    got = _run(idx, qs, 45, gpu)
+    ref = oracle_mod.dense_topk(rows, qs, 45)
+    _assert_same(got, ref, 45)
+    mask = np.zeros((3000 + 63) // 64, dtype=np.uint64)
+    mask[0] = np.uint64(0b1011)  # 3 rows enabled, k = 5 -> count 3
+    got = _run(idx, qs, 5, gpu, mask=mask)
+    ref = oracle_mod.dense_topk(rows, qs, 5, row_mask=mask)
+    _assert_same(got, ref, 5)
+    assert (got["count"] == 3).all()
+
+
+def test_zero_query_and_empty_index(gpu, oracle_mod):
+    rows = oracle_mod.unit_fp16(500, 256, seed=14)
+    qs = np.zeros((2, 256), dtype=np.uint16)
+    idx = _index(rows, gpu)
+    got = _run(idx, qs, 5, gpu)
+    _assert_same(got, oracle_mod.dense_topk(rows, qs, 5), 5)
+    empty = _index(np.zeros((0, 256), dtype=np.uint16), gpu)
+    got = _run(empty, oracle_mod.unit_fp16(3, 256, seed=1), 5, gpu)
+    assert (got["count"] == 0).all()
+
+
+def test_shard_merge_equals_global(gpu, oracle_mod):
+    from audio_rag_amd.retrieval.device import merge_shards
+
+    rows = oracle_mod.unit_fp16(12000, 1024, seed=15)
+    qs = oracle_mod.unit_fp16(10, 1024, seed=16)
+    k = 20
+    parts = []
+    for s, (a, b) in enumerate([(0, 3000), (3000, 7001), (7001, 12000)]):
+        idx = _index(rows[a:b], gpu, base=a)
+        parts.append(idx.topk(_dev(qs.view(np.float16), gpu), k))
+    stack = lambda f: torch.stack([getattr(p, f) for p in parts])
+    m = merge_shards(stack("rank"), stack("scores"), stack("ids"), stack("count"), k)
+    torch.cuda.synchronize()
+    got = {f: getattr(m, f).cpu().numpy() for f in ("ids", "scores", "rank", "count")}
+    _assert_same(got, oracle_mod.dense_topk(rows, qs, k), k)
+
+
+@pytest.mark.slow
+def test_full_size_fast_equals_exact(gpu, oracle_mod):
+    """BASELINE size (1M x 1024): the certified fast path equals the exhaustive exact scan for a
+    batch, and both equal the C oracle on two queries."""
+    n, dim = 1_000_000, 1024
+    g = torch.Generator(device=gpu).manual_seed(0)
+    x = torch.randn((n, dim), generator=g, device=gpu)
+    rows = (x / x.norm(dim=1, keepdim=True)).half()
+    del x
+    from audio_rag_amd.retrieval.device import DenseIndex
+
+    idx = DenseIndex(rows)
+    qx = torch.randn((64, dim), generator=g, device=gpu)
+    q = (qx / qx.norm(dim=1, keepdim=True)).half()
+    fast = idx.topk(q, 5)
+    exact = idx.topk(q[:4], 5, exact=True)
+    torch.cuda.synchronize()
+    assert (fast.flags.cpu().numpy() == 1).all()
+    np.testing.assert_array_equal(fast.ids[:4].cpu().numpy(), exact.ids.cpu().numpy())
+    np.testing.assert_array_equal(fast.rank[:4].cpu().numpy(), exact.rank.cpu().numpy())
+    rows_u16 = rows.cpu().numpy().view(np.uint16)
+    q_u16 = q[:2].cpu().numpy().view(np.uint16)
+    ref = oracle_mod.dense_topk(rows_u16, q_u16, 5)
+    np.testing.assert_array_equal(fast.ids[:2].cpu().numpy(), ref.ids)
+    np.testing.assert_array_equal(fast.rank[:2].cpu().numpy(), ref.rank)

@@ -1,0 +1,104 @@
+"""Sparse lexical top-k (armi_sparse_topk) and RRF fusion (armi_rrf_fuse) on the GPU against the
+CPU oracle. Integer / index work: ids and counts bit-identical; sparse scores are the exact fp32
+Qdrant-order sums (bitwise); RRF scores are fp64 sums (bitwise).
+Reference call sites: src/audio_rag/retrieval/qdrant.py:289-293, 299-312 (sparse), 295 (RRF)."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _sparse_index(csr, gpu, base=0):
+    from audio_rag_amd.retrieval.device import SparseIndex
+
+    indptr, indices, values = csr
+    return SparseIndex(_t(indptr, gpu), _t(indices, gpu), _t(values, gpu), 250002, base)
+
+
+def _run(idx, qcsr, k, gpu, mask=None):
+    qi, qx, qv = qcsr
+    m = None if mask is None else _t(mask.view(np.int64), gpu)
+    out = idx.topk(_t(qi, gpu), _t(qx, gpu), _t(qv, gpu), k, row_mask=m)
+    torch.cuda.synchronize()
+    return {f: getattr(out, f).cpu().numpy() for f in ("ids", "scores", "count", "flags")}
+
+
+def _same(got, ref):
+    np.testing.assert_array_equal(got["count"], ref.count)
+    for b in range(ref.count.shape[0]):
+        c = ref.count[b]
+        np.testing.assert_array_equal(got["ids"][b, :c], ref.ids[b, :c], err_msg=f"query {b}")
+        np.testing.assert_array_equal(got["scores"][b, :c], ref.scores[b, :c], err_msg=f"query {b}")
+        assert (got["ids"][b, c:] == -1).all()
+
+
+@pytest.mark.parametrize("n,b,k", [(3000, 8, 5), (20000, 64, 40), (777, 70, 12), (40, 5, 20)])
+def test_sparse_matches_oracle(gpu, oracle_mod, n, b, k):
+    csr = oracle_mod.sparse_corpus(n, seed=2 + n)
+    q = oracle_mod.sparse_queries(b, seed=3 + n)
+    idx = _sparse_index(csr, gpu, base=7)
+    got = _run(idx, q, k, gpu)
+    _same(got, oracle_mod.sparse_topk(*csr, *q, k, ordinal_base=7))
+
+
+def test_sparse_certifies_and_masks(gpu, oracle_mod):
+    n = 50000
+    csr = oracle_mod.sparse_corpus(n, seed=21)
+    q = oracle_mod.sparse_queries(64, seed=22)
+    idx = _sparse_index(csr, gpu)
+    got = _run(idx, q, 40, gpu)
+    assert (got["flags"] & 1).mean() > 0.9, got["flags"]
+    _same(got, oracle_mod.sparse_topk(*csr, *q, 40))
+    rng = np.random.default_rng(1)
+    mask = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in np.nonzero(rng.random(n) < 0.5)[0]:
+        mask[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    got = _run(idx, q, 10, gpu, mask=mask)
+    _same(got, oracle_mod.sparse_topk(*csr, *q, 10, row_mask=mask))
+
+
+def test_sparse_no_overlap_and_empty_query(gpu, oracle_mod):
+    csr = oracle_mod.sparse_corpus(500, seed=31)
+    qi = np.array([0, 0, 2], dtype=np.int32)           # query 0 empty, query 1 two unseen terms
+    qx = np.array([250000, 250001], dtype=np.int32)
+    qv = np.array([0.3, 0.2], dtype=np.float32)
+    idx = _sparse_index(csr, gpu)
+    got = _run(idx, (qi, qx, qv), 5, gpu)
+    assert (got["count"] == 0).all()
+    _same(got, oracle_mod.sparse_topk(*csr, qi, qx, qv, 5))
+
+
+def _rrf_case(rng, n_q, ka, kb, universe):
+    a_ids = np.full((n_q, ka), -1, dtype=np.int64)
+    b_ids = np.full((n_q, kb), -1, dtype=np.int64)
+    a_cnt = rng.integers(0, ka + 1, size=n_q).astype(np.int32)
+    b_cnt = rng.integers(0, kb + 1, size=n_q).astype(np.int32)
+    for q in range(n_q):
+        a_ids[q, :a_cnt[q]] = rng.choice(universe, size=a_cnt[q], replace=False)
+        b_ids[q, :b_cnt[q]] = rng.choice(universe, size=b_cnt[q], replace=False)
+    return a_ids, a_cnt, b_ids, b_cnt
+
+
+@pytest.mark.parametrize("ka,kb,limit,universe", [(40, 40, 20, 60), (10, 10, 5, 15), (200, 200, 100, 300), (3, 7, 20, 9)])
+def test_rrf_matches_qdrant_local_mode(gpu, oracle_mod, ka, kb, limit, universe):
+    from audio_rag_amd.retrieval.device import TopK, rrf_fuse
+
+    rng = np.random.default_rng(ka * 7 + kb)
+    a_ids, a_cnt, b_ids, b_cnt = _rrf_case(rng, 33, ka, kb, universe)
+    z = lambda x: _t(x, gpu)
+    a = TopK(scores=None, ids=z(a_ids), rank=None, count=z(a_cnt))
+    b = TopK(scores=None, ids=z(b_ids), rank=None, count=z(b_cnt))
+    out = rrf_fuse(a, b, limit, rrf_k=2)
+    torch.cuda.synchronize()
+    ids, rank, cnt = out.ids.cpu().numpy(), out.rank.cpu().numpy(), out.count.cpu().numpy()
+    for q in range(33):
+        ref = oracle_mod.rrf([list(a_ids[q, :a_cnt[q]]), list(b_ids[q, :b_cnt[q]])], limit)
+        assert cnt[q] == len(ref)
+        assert [int(x) for x in ids[q, :cnt[q]]] == [int(p) for p, _ in ref]
+        assert [float(x) for x in rank[q, :cnt[q]]] == [s for _, s in ref]
