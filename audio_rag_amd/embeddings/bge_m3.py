@@ -1,0 +1,179 @@
+"""BGE-M3 query / chunk encoder on the MI355X (PyTorch-ROCm forward, as north_star allows).
+
+Mirrors BGEM3Embedder (src/audio_rag/embeddings/bge.py:14-157) over FlagEmbedding's
+BGEM3FlagModel (flagembedding >= 1.3.5, not installed):
+  * model: XLM-RoBERTa-large (24 layers, d 1024, 16 heads, FFN 4096, vocab 250002, LN eps 1e-5)
+    run in fp16 on the GPU (bge.py:54 use_fp16 on cuda)
+  * dense  = L2-normalised hidden state of <s> (fp16 values, bge.py:149 .tolist())
+  * sparse = relu(Linear(1024 -> 1)(hidden)) per token, max per token id, special tokens and
+    weights <= 0 dropped, keys in first-occurrence order (_convert_sparse, bge.py:95-102)
+Weights: BAAI/bge-m3 is not on disk and cannot be downloaded here; the encoder and the sparse
+head are initialised from EmbeddingConfig.seed (documented in DESIGN.md). Token ids come from
+audio_rag_amd.text (stand-in tokenizer) or are passed directly (embed_query_ids).
+"""
+
+from __future__ import annotations
+
+import gc
+import logging
+
+import torch
+
+from audio_rag_amd.config.schema import EmbeddingConfig
+from audio_rag_amd.core.base import BaseEmbedder, EmbeddingResult, SparseVector
+from audio_rag_amd.core.exceptions import EmbeddingError
+from audio_rag_amd.embeddings.base import EmbeddingsRegistry
+from audio_rag_amd.text import SPECIAL_IDS, HashTokenizer, pad_batch
+from audio_rag_amd.utils.decorators import require_loaded, timed
+
+logger = logging.getLogger(__name__)
+
+VRAM_ESTIMATE = 2.5  # GB (bge.py:11)
+
+# XLM-RoBERTa-large as used by BAAI/bge-m3
+BGE_M3_ARCH = dict(vocab_size=250002, hidden_size=1024, num_hidden_layers=24,
+                   num_attention_heads=16, intermediate_size=4096, max_position_embeddings=8194,
+                   layer_norm_eps=1e-5, pad_token_id=1, bos_token_id=0, eos_token_id=2,
+                   type_vocab_size=1)
+
+
+def build_bge_m3(seed: int, arch: dict | None = None):
+    """Seeded random XLM-R encoder + sparse head (CPU, fp32)."""
+    from transformers import XLMRobertaConfig, XLMRobertaModel
+
+    cfg = XLMRobertaConfig(**{**BGE_M3_ARCH, **(arch or {})})
+    g = torch.random.fork_rng()
+    with g:
+        torch.manual_seed(seed)
+        model = XLMRobertaModel(cfg, add_pooling_layer=False)
+        sparse_linear = torch.nn.Linear(cfg.hidden_size, 1)
+    model.eval()
+    return model, sparse_linear
+
+
+def lexical_weights(token_weights: list[float], input_ids: list[int]) -> dict[int, float]:
+    """FlagEmbedding's _process_token_weights: per token id the max weight, ids of special
+    tokens and weights <= 0 skipped, first-occurrence key order."""
+    result: dict[int, float] = {}
+    for w, idx in zip(token_weights, input_ids):
+        if idx in SPECIAL_IDS or not w > 0:
+            continue
+        if w > result.get(idx, 0.0):
+            result[idx] = w
+    return result
+
+
+@EmbeddingsRegistry.register("bge-m3")
+class BGEM3Embedder(BaseEmbedder):
+    def __init__(self, config: EmbeddingConfig, device: torch.device | None = None,
+                 arch: dict | None = None):
+        self.config = config
+        self._device = device or torch.device("cuda", 0)
+        self._dimension = (arch or {}).get("hidden_size", BGE_M3_ARCH["hidden_size"])
+        self._use_sparse = config.use_sparse
+        self._arch = arch
+        self._model = None
+        self._sparse = None
+        self.tokenizer = HashTokenizer()
+        logger.info(f"BGEM3Embedder initialized: model={config.model}, device={self._device}, "
+                    f"sparse={self._use_sparse}")
+
+    def load(self) -> None:
+        if self._model is not None:
+            return
+        try:
+            model, sparse = build_bge_m3(self.config.seed, self._arch)
+            self._model = model.to(self._device, dtype=torch.float16)
+            self._sparse = sparse.to(self._device, dtype=torch.float16)
+        except Exception as e:
+            raise EmbeddingError(f"Failed to load embedding model: {e}")
+
+    def unload(self) -> None:
+        if self._model is None:
+            return
+        self._model = None
+        self._sparse = None
+        gc.collect()
+        torch.cuda.empty_cache()
+
+    @property
+    def is_loaded(self) -> bool:
+        return self._model is not None
+
+    @property
+    def vram_required(self) -> float:
+        return VRAM_ESTIMATE
+
+    @property
+    def dimension(self) -> int:
+        return self._dimension
+
+    @property
+    def supports_sparse(self) -> bool:
+        return self._use_sparse
+
+    # ---------------------------------------------------------------------------- device
+
+    @torch.inference_mode()
+    def encode_ids(self, seqs: list[list[int]]) -> tuple[torch.Tensor, list[dict[int, float]] | None]:
+        """Encodes token-id sequences; returns (dense fp16 [B, d] on the device, lexical
+        weights per sequence or None)."""
+        ids, mask = pad_batch(seqs)
+        ids_t = torch.tensor(ids, dtype=torch.long, device=self._device)
+        mask_t = torch.tensor(mask, dtype=torch.long, device=self._device)
+        hidden = self._model(input_ids=ids_t, attention_mask=mask_t).last_hidden_state
+        dense = torch.nn.functional.normalize(hidden[:, 0], dim=-1)
+        lex = None
+        if self._use_sparse:
+            tw = torch.relu(self._sparse(hidden)).squeeze(-1).float().cpu().tolist()
+            lex = [lexical_weights(tw[i][: len(s)], s) for i, s in enumerate(seqs)]
+        return dense.contiguous(), lex
+
+    def _results(self, dense: torch.Tensor, lex) -> list[EmbeddingResult]:
+        rows = dense.cpu().tolist()
+        out = []
+        for i, d in enumerate(rows):
+            sparse = None
+            if lex is not None:
+                sparse = self._convert_sparse(lex[i])
+            out.append(EmbeddingResult(dense=d, sparse=sparse))
+        return out
+
+    def _convert_sparse(self, sparse_dict: dict) -> SparseVector | None:
+        """bge.py:95-102."""
+        if not sparse_dict:
+            return None
+        return SparseVector(indices=[int(k) for k in sparse_dict.keys()],
+                            values=[float(v) for v in sparse_dict.values()])
+
+    # ----------------------------------------------------------------------------- API
+
+    @timed
+    @require_loaded
+    def embed(self, texts: list[str]) -> list[EmbeddingResult]:
+        if not texts:
+            return []
+        try:
+            out = []
+            bs = self.config.batch_size
+            for a in range(0, len(texts), bs):
+                seqs = [self.tokenizer.encode(t, self.config.max_length) for t in texts[a:a + bs]]
+                out.extend(self._results(*self.encode_ids(seqs)))
+            return out
+        except Exception as e:
+            raise EmbeddingError(f"Embedding generation failed: {e}")
+
+    @require_loaded
+    def embed_query(self, query: str) -> EmbeddingResult:
+        try:
+            seqs = [self.tokenizer.encode(query, self.config.max_length)]
+            return self._results(*self.encode_ids(seqs))[0]
+        except Exception as e:
+            raise EmbeddingError(f"Query embedding failed: {e}")
+
+    @require_loaded
+    def embed_queries(self, queries: list[str]):
+        """Batched query encode for the batched pipeline: (dense fp16 [B, d] device, lexical
+        weights per query or None)."""
+        seqs = [self.tokenizer.encode(q, self.config.max_length) for q in queries]
+        return self.encode_ids(seqs)

@@ -1,0 +1,105 @@
+"""XLM-RoBERTa sequence-classification forward (the bge-reranker-base cross-encoder) on the
+MI355X: the non-GEMM ops are libarmi kernels (armi_enc_*), the GEMMs go to hipBLASLt/rocBLAS
+through torch.
+
+Restates what sentence-transformers' CrossEncoder.predict runs for BGEReranker
+(src/audio_rag/reranking/bge.py:51-55, 119-123): XLMRobertaForSequenceClassification with
+num_labels = 1 (12 layers, d 768, 12 heads, FFN 3072, exact-erf GELU, LN eps 1e-5), head
+dense -> tanh -> out_proj on <s>, then sigmoid. Activations are fp32 (ST's default dtype).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from audio_rag_amd._armi import call, ptr, stream_handle
+
+# XLM-RoBERTa-base as used by BAAI/bge-reranker-base
+RERANKER_ARCH = dict(vocab_size=250002, hidden_size=768, num_hidden_layers=12,
+                     num_attention_heads=12, intermediate_size=3072, max_position_embeddings=514,
+                     layer_norm_eps=1e-5, pad_token_id=1, bos_token_id=0, eos_token_id=2,
+                     type_vocab_size=1, num_labels=1)
+
+
+def build_reranker(seed: int, arch: dict | None = None):
+    """Seeded random XLMRobertaForSequenceClassification (CPU, fp32, eager attention)."""
+    from transformers import XLMRobertaConfig, XLMRobertaForSequenceClassification
+
+    cfg = XLMRobertaConfig(**{**RERANKER_ARCH, **(arch or {})})
+    with torch.random.fork_rng():
+        torch.manual_seed(seed)
+        model = XLMRobertaForSequenceClassification(cfg)
+    model.eval()
+    return model
+
+
+class CrossEncoderXLMR:
+    def __init__(self, hf_model, device: torch.device):
+        cfg = hf_model.config
+        self.device = device
+        self.d = cfg.hidden_size
+        self.heads = cfg.num_attention_heads
+        self.dh = self.d // self.heads
+        self.eps = float(cfg.layer_norm_eps)
+        self.pad = cfg.pad_token_id
+        sd = {k: v.detach().to(device=device, dtype=torch.float32).contiguous()
+              for k, v in hf_model.state_dict().items()}
+        e = "roberta.embeddings."
+        self.word = sd[e + "word_embeddings.weight"]
+        self.pos = sd[e + "position_embeddings.weight"]
+        self.type0 = sd[e + "token_type_embeddings.weight"][0].contiguous()
+        self.emb_ln = (sd[e + "LayerNorm.weight"], sd[e + "LayerNorm.bias"])
+        self.layers = []
+        for i in range(cfg.num_hidden_layers):
+            p = f"roberta.encoder.layer.{i}."
+            a = p + "attention.self."
+            wqkv = torch.cat([sd[a + "query.weight"], sd[a + "key.weight"], sd[a + "value.weight"]])
+            bqkv = torch.cat([sd[a + "query.bias"], sd[a + "key.bias"], sd[a + "value.bias"]])
+            self.layers.append(dict(
+                wqkv_t=wqkv.t().contiguous(), bqkv=bqkv,
+                wo_t=sd[p + "attention.output.dense.weight"].t().contiguous(),
+                bo=sd[p + "attention.output.dense.bias"],
+                ln1=(sd[p + "attention.output.LayerNorm.weight"], sd[p + "attention.output.LayerNorm.bias"]),
+                wi_t=sd[p + "intermediate.dense.weight"].t().contiguous(),
+                bi=sd[p + "intermediate.dense.bias"],
+                wo2_t=sd[p + "output.dense.weight"].t().contiguous(),
+                bo2=sd[p + "output.dense.bias"],
+                ln2=(sd[p + "output.LayerNorm.weight"], sd[p + "output.LayerNorm.bias"]),
+            ))
+        self.head = (sd["classifier.dense.weight"], sd["classifier.dense.bias"],
+                     sd["classifier.out_proj.weight"].reshape(-1).contiguous(),
+                     sd["classifier.out_proj.bias"])
+
+    @torch.inference_mode()
+    def forward(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        """ids, mask: int32 [n, L] on the device -> sigmoid scores float32 [n]."""
+        n, L = ids.shape
+        d, H, dh = self.d, self.heads, self.dh
+        s = stream_handle()
+        h = torch.empty((n * L, d), dtype=torch.float32, device=self.device)
+        call("armi_enc_embed", ptr(ids), ptr(self.word), ptr(self.pos), ptr(self.type0),
+             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad, self.eps, s)
+        scale = 1.0 / math.sqrt(dh)
+        for ly in self.layers:
+            qkv = torch.addmm(ly["bqkv"], h, ly["wqkv_t"])                  # [n*L, 3d]
+            qkv = qkv.view(n, L, 3, H, dh).permute(2, 0, 3, 1, 4)          # [3, n, H, L, dh]
+            q, k, v = qkv[0], qkv[1], qkv[2]
+            scores = torch.matmul(q, k.transpose(-1, -2)).contiguous()    # [n, H, L, L]
+            call("armi_enc_masked_softmax", ptr(scores), ptr(mask), n, H, L, scale, s)
+            ctx = torch.matmul(scores, v).permute(0, 2, 1, 3).reshape(n * L, d)
+            attn = torch.addmm(ly["bo"], ctx, ly["wo_t"])
+            h1 = torch.empty_like(h)
+            call("armi_enc_layernorm_residual", ptr(attn), ptr(h), ptr(ly["ln1"][0]),
+                 ptr(ly["ln1"][1]), ptr(h1), n * L, d, self.eps, s)
+            inter = torch.mm(h1, ly["wi_t"])
+            call("armi_enc_bias_gelu", ptr(inter), ptr(ly["bi"]), n * L, inter.shape[1], s)
+            out = torch.addmm(ly["bo2"], inter, ly["wo2_t"])
+            h = torch.empty_like(h)
+            call("armi_enc_layernorm_residual", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
+                 ptr(ly["ln2"][1]), ptr(h), n * L, d, self.eps, s)
+        probs = torch.empty(n, dtype=torch.float32, device=self.device)
+        call("armi_enc_cls_head_sigmoid", ptr(h), ptr(self.head[0]), ptr(self.head[1]),
+             ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, L, d, s)
+        return probs

@@ -1,0 +1,145 @@
+"""A chunk collection: host staging of upserted points plus their device indexes.
+
+Replaces one Qdrant collection as QdrantRetriever creates and fills it
+(src/audio_rag/retrieval/qdrant.py:59-132 _ensure_collection, 140-225 add):
+  * named dense vector "dense" (size = embedding_dim, COSINE)      -> DenseIndex (fp16 rows)
+  * named sparse vector "sparse" (hybrid collections only)         -> SparseIndex (CSR)
+  * payload {text, start, end, speaker, metadata}                  -> host list
+Points get consecutive ordinals in upsert order (the reference's uuid4 ids are never surfaced:
+RetrievalResult carries no id, core/base.py:56-61). The device indexes are rebuilt lazily on the
+first search after an add; a built collection is read-only, so concurrent searches are safe.
+"""
+
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex
+
+BGE_M3_VOCAB = 250002
+
+
+def _match_value(field_value, wanted) -> bool:
+    """Qdrant MatchValue: equality on keyword / integer / bool payload values; an array field
+    matches when any element does."""
+    if isinstance(field_value, list):
+        return any(_match_value(v, wanted) for v in field_value)
+    if isinstance(field_value, bool) or isinstance(wanted, bool):
+        return isinstance(field_value, bool) and isinstance(wanted, bool) and field_value == wanted
+    if isinstance(field_value, float) and not field_value.is_integer():
+        return False
+    return field_value == wanted
+
+
+@dataclass
+class ChunkCollection:
+    name: str
+    dim: int
+    hybrid: bool
+    device: torch.device
+    # host staging
+    dense_rows: list[np.ndarray] = field(default_factory=list)        # fp16 [n_i, dim] blocks
+    sparse_rows: list[tuple[np.ndarray, np.ndarray] | None] = field(default_factory=list)
+    payloads: list[dict] = field(default_factory=list)
+    # device state
+    _dense: DenseIndex | None = None
+    _sparse: SparseIndex | None = None
+    _built_rows: int = -1
+    _mask_cache: dict = field(default_factory=dict)
+    _lock: threading.Lock = field(default_factory=threading.Lock)
+
+    @property
+    def count(self) -> int:
+        return len(self.payloads)
+
+    # ------------------------------------------------------------------------------ upsert
+
+    def upsert(self, dense: np.ndarray, sparse: list[tuple[np.ndarray, np.ndarray] | None],
+               payloads: list[dict]) -> None:
+        """dense: float16 [n, dim]; sparse[i]: (indices int32 ascending, values float32) or
+        None; payloads: one dict per point."""
+        if dense.dtype != np.float16 or dense.ndim != 2 or dense.shape[1] != self.dim:
+            raise ValueError(f"dense vectors must be float16 [n, {self.dim}]")
+        if not (len(sparse) == len(payloads) == dense.shape[0]):
+            raise ValueError("dense / sparse / payload counts differ")
+        bits = dense.view(np.uint16)
+        if ((bits >> 10) & 31).max(initial=0) > 15:
+            raise ValueError("dense components must be finite with |x| < 2 (unit embeddings)")
+        with self._lock:
+            self.dense_rows.append(np.ascontiguousarray(dense))
+            self.sparse_rows.extend(sparse)
+            self.payloads.extend(payloads)
+            self._mask_cache.clear()
+
+    # ------------------------------------------------------------------------------- build
+
+    def _ensure_built(self) -> None:
+        if self._built_rows == self.count:
+            return
+        with self._lock:
+            if self._built_rows == self.count:
+                return
+            rows = (np.concatenate(self.dense_rows) if self.dense_rows
+                    else np.zeros((0, self.dim), dtype=np.float16))
+            old_dense, old_sparse = self._dense, self._sparse
+            self._dense = DenseIndex(torch.from_numpy(rows).to(self.device))
+            if self.hybrid:
+                indptr = np.zeros(self.count + 1, dtype=np.int64)
+                lens = [0 if s is None else len(s[0]) for s in self.sparse_rows]
+                np.cumsum(lens, out=indptr[1:])
+                idx = np.concatenate([s[0] for s in self.sparse_rows if s is not None] or
+                                     [np.zeros(0, np.int32)]).astype(np.int32)
+                val = np.concatenate([s[1] for s in self.sparse_rows if s is not None] or
+                                     [np.zeros(0, np.float32)]).astype(np.float32)
+                vocab = max(BGE_M3_VOCAB, int(idx.max(initial=-1)) + 1)
+                t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+                self._sparse = SparseIndex(t(indptr), t(idx), t(val), vocab)
+            self._built_rows = self.count
+            for old in (old_dense, old_sparse):
+                if old is not None:
+                    old.close()
+
+    @property
+    def dense_index(self) -> DenseIndex:
+        self._ensure_built()
+        return self._dense
+
+    @property
+    def sparse_index(self) -> SparseIndex | None:
+        self._ensure_built()
+        return self._sparse
+
+    # ------------------------------------------------------------------------------ filter
+
+    def filter_mask(self, filter_metadata: dict | None) -> torch.Tensor | None:
+        """Bitmask (int64 words on the device) of points whose payload metadata matches every
+        condition: Filter(must=[FieldCondition(key=f"metadata.{k}", match=MatchValue(v))])
+        (qdrant.py:263-269)."""
+        if not filter_metadata:
+            return None
+        key = tuple(sorted((k, repr(v)) for k, v in filter_metadata.items()))
+        cached = self._mask_cache.get(key)
+        if cached is not None and cached[0] == self.count:
+            return cached[1]
+        n = self.count
+        ok = np.zeros(n, dtype=bool)
+        for i, p in enumerate(self.payloads):
+            md = p.get("metadata") or {}
+            ok[i] = all(k in md and _match_value(md[k], v) for k, v in filter_metadata.items())
+        words = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        idx = np.nonzero(ok)[0]
+        np.bitwise_or.at(words, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
+        mask = torch.from_numpy(words.view(np.int64)).to(self.device)
+        self._mask_cache[key] = (n, mask)
+        return mask
+
+    def close(self) -> None:
+        for ix in (self._dense, self._sparse):
+            if ix is not None:
+                ix.close()
+        self._dense = self._sparse = None
+        self._built_rows = -1

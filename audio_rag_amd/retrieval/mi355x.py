@@ -1,0 +1,247 @@
+"""MI355XRetriever: drop-in replacement of QdrantRetriever (src/audio_rag/retrieval/qdrant.py).
+
+Same constructor (config, embedding_dim), same methods and semantics:
+  add(chunks, embeddings, collection_name)                      qdrant.py:140-225
+  search(query_embedding, top_k, collection_name, filter_metadata, search_type)  qdrant.py:227-352
+  delete_collection / count / collection_exists / is_hybrid_collection         qdrant.py:134-138, 354-381
+The ranking arithmetic runs on the GPU through libarmi (dense cosine, sparse dot, RRF); nothing
+falls back to the CPU. search_batch() is the batched device API the pipeline and bench use.
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from audio_rag_amd.config.schema import RetrievalConfig
+from audio_rag_amd.core.base import (AudioChunk, BaseRetriever, EmbeddingResult, RetrievalResult,
+                                     SparseVector)
+from audio_rag_amd.core.exceptions import RetrievalError
+from audio_rag_amd.retrieval.base import RetrievalRegistry
+from audio_rag_amd.retrieval.collection import ChunkCollection
+from audio_rag_amd.retrieval.device import TopK, rrf_fuse
+from audio_rag_amd.utils.decorators import timed
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class QueryBatch:
+    """B queries on the device: dense fp16 [B, dim] and an optional sparse CSR."""
+
+    dense: torch.Tensor
+    sparse_indptr: torch.Tensor | None = None   # int32 [B+1]
+    sparse_indices: torch.Tensor | None = None  # int32
+    sparse_values: torch.Tensor | None = None   # float32
+
+    @property
+    def has_sparse(self) -> bool:
+        return self.sparse_indptr is not None
+
+
+def sparse_arrays(sv: SparseVector | None) -> tuple[np.ndarray, np.ndarray] | None:
+    """SparseVector -> (ascending int32 indices, float32 values). Qdrant stores sparse vectors
+    sorted by index; duplicate indices are rejected like Qdrant does."""
+    if sv is None:
+        return None
+    idx = np.asarray(sv.indices, dtype=np.int64)
+    val = np.asarray(sv.values, dtype=np.float32)
+    if idx.shape != val.shape:
+        raise ValueError("sparse vector indices and values differ in length")
+    order = np.argsort(idx, kind="stable")
+    idx, val = idx[order], val[order]
+    if idx.size and (np.any(idx[1:] == idx[:-1]) or idx[0] < 0 or idx[-1] >= 2**31):
+        raise ValueError("sparse vector indices must be unique non-negative int32")
+    return idx.astype(np.int32), val
+
+
+def fp16_rows(vectors: list[list[float]] | np.ndarray, dim: int) -> np.ndarray:
+    a = np.asarray(vectors, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] != dim:
+        raise ValueError(f"dense vectors must have dimension {dim}, got shape {a.shape}")
+    return a.astype(np.float16)
+
+
+@RetrievalRegistry.register("mi355x")
+class MI355XRetriever(BaseRetriever):
+    """Dense (cosine), sparse (lexical) and hybrid (RRF) search on an MI355X chunk store."""
+
+    def __init__(self, config: RetrievalConfig, embedding_dim: int = 1024):
+        self.config = config
+        self.embedding_dim = embedding_dim
+        self.device = torch.device("cuda", config.device)
+        self._collections: dict[str, ChunkCollection] = {}
+        logger.info(f"MI355XRetriever initialized: collection={config.collection_name}, "
+                    f"search_type={config.search_type}, device={self.device}")
+
+    # ---------------------------------------------------------------------- collections
+
+    def _resolve_collection(self, collection_name: str | None) -> str:
+        return collection_name or self.config.collection_name
+
+    def _ensure_collection(self, collection_name: str | None = None, hybrid: bool = False) -> str:
+        """Creates a missing collection (hybrid = dense + sparse named vectors, else dense-only
+        legacy schema), as qdrant.py:59-132 does."""
+        resolved = self._resolve_collection(collection_name)
+        coll = self._collections.get(resolved)
+        if coll is not None:
+            if hybrid and not coll.hybrid:
+                logger.warning(f"Collection {resolved} exists but is not hybrid-enabled. "
+                               "Re-index required for hybrid search.")
+            return resolved
+        try:
+            self._collections[resolved] = ChunkCollection(resolved, self.embedding_dim, hybrid,
+                                                          self.device)
+            logger.info(f"Creating {'hybrid' if hybrid else 'dense'} collection: {resolved}")
+            return resolved
+        except Exception as e:
+            raise RetrievalError(f"Failed to ensure collection '{resolved}': {e}")
+
+    def is_hybrid_collection(self, collection_name: str | None = None) -> bool:
+        resolved = self._ensure_collection(collection_name)
+        return self._collections[resolved].hybrid
+
+    def delete_collection(self, collection_name: str | None = None) -> None:
+        resolved = self._resolve_collection(collection_name)
+        try:
+            coll = self._collections.pop(resolved, None)
+            if coll is not None:
+                coll.close()
+            logger.info(f"Deleted collection: {resolved}")
+        except Exception as e:
+            raise RetrievalError(f"Failed to delete collection '{resolved}': {e}")
+
+    def count(self, collection_name: str | None = None) -> int:
+        resolved = self._ensure_collection(collection_name)
+        return self._collections[resolved].count
+
+    def collection_exists(self, collection_name: str | None = None) -> bool:
+        return self._resolve_collection(collection_name) in self._collections
+
+    def collection(self, collection_name: str | None = None) -> ChunkCollection:
+        return self._collections[self._ensure_collection(collection_name)]
+
+    # ------------------------------------------------------------------------------ add
+
+    @timed
+    def add(self, chunks: list[AudioChunk], embeddings: list[EmbeddingResult],
+            collection_name: str | None = None) -> None:
+        if not chunks:
+            return
+        if len(chunks) != len(embeddings):
+            raise RetrievalError(f"Chunks/embeddings mismatch: {len(chunks)} chunks, "
+                                 f"{len(embeddings)} embeddings")
+        has_sparse = any(e.sparse is not None for e in embeddings)
+        resolved = self._ensure_collection(collection_name, hybrid=has_sparse)
+        try:
+            coll = self._collections[resolved]
+            dense = fp16_rows([e.dense for e in embeddings], self.embedding_dim)
+            if coll.hybrid and not self.config.reproduce_sparse_drop:
+                sparse = [sparse_arrays(e.sparse) for e in embeddings]
+            else:
+                # legacy collections keep dense only; with reproduce_sparse_drop the reference's
+                # final dense-only batch upsert (qdrant.py:210-220) replaces every point, so the
+                # stored points have no sparse vector
+                sparse = [None] * len(embeddings)
+            payloads = [{"text": c.text, "start": c.start, "end": c.end, "speaker": c.speaker,
+                         "metadata": c.metadata or {}} for c in chunks]
+            coll.upsert(dense, sparse, payloads)
+            logger.info(f"Added {len(chunks)} chunks to {resolved} (hybrid={coll.hybrid})")
+        except Exception as e:
+            raise RetrievalError(f"Failed to add chunks to '{resolved}': {e}")
+
+    def add_arrays(self, dense: np.ndarray, payloads: list[dict],
+                   sparse: list[tuple[np.ndarray, np.ndarray] | None] | None = None,
+                   collection_name: str | None = None) -> None:
+        """Bulk upsert of pre-embedded chunks (fp16 [n, dim] + payload dicts), the fast ingest
+        path for large corpora."""
+        resolved = self._ensure_collection(collection_name, hybrid=sparse is not None)
+        coll = self._collections[resolved]
+        if sparse is None or not coll.hybrid:
+            sparse = [None] * len(payloads)
+        coll.upsert(np.ascontiguousarray(dense, dtype=np.float16), sparse, payloads)
+
+    # --------------------------------------------------------------------------- search
+
+    def _mode(self, coll: ChunkCollection, search_type: str, has_sparse: bool) -> str:
+        if search_type == "hybrid" and coll.hybrid and has_sparse:
+            return "hybrid"
+        if search_type == "sparse" and coll.hybrid and has_sparse:
+            return "sparse"
+        return "dense" if coll.hybrid else "legacy_dense"
+
+    def search_batch(self, queries: QueryBatch, top_k: int | None = None,
+                     collection_name: str | None = None, filter_metadata: dict | None = None,
+                     search_type: str | None = None) -> tuple[TopK, str]:
+        """Device top-k for B queries; returns (TopK, mode). Scores are cosine (dense),
+        sparse dot (sparse) or the RRF score (hybrid), as Qdrant's hit.score."""
+        resolved = self._ensure_collection(collection_name)
+        top_k = top_k or self.config.top_k
+        search_type = search_type or self.config.search_type
+        coll = self._collections[resolved]
+        mode = self._mode(coll, search_type, queries.has_sparse)
+        mask = coll.filter_mask(filter_metadata)
+        if mode == "hybrid":
+            dense = coll.dense_index.topk(queries.dense, 2 * top_k, row_mask=mask)
+            sparse = coll.sparse_index.topk(queries.sparse_indptr, queries.sparse_indices,
+                                            queries.sparse_values, 2 * top_k, row_mask=mask)
+            return rrf_fuse(dense, sparse, top_k, rrf_k=self.config.rrf_k), mode
+        if mode == "sparse":
+            return coll.sparse_index.topk(queries.sparse_indptr, queries.sparse_indices,
+                                          queries.sparse_values, top_k, row_mask=mask), mode
+        return coll.dense_index.topk(queries.dense, top_k, row_mask=mask), mode
+
+    def to_query_batch(self, query_embeddings: list[EmbeddingResult]) -> QueryBatch:
+        dense = torch.from_numpy(fp16_rows([q.dense for q in query_embeddings],
+                                           self.embedding_dim)).to(self.device)
+        if any(q.sparse is None for q in query_embeddings):
+            return QueryBatch(dense=dense)
+        parts = [sparse_arrays(q.sparse) for q in query_embeddings]
+        indptr = np.zeros(len(parts) + 1, dtype=np.int32)
+        np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
+        idx = np.concatenate([p[0] for p in parts]).astype(np.int32)
+        val = np.concatenate([p[1] for p in parts]).astype(np.float32)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        return QueryBatch(dense=dense, sparse_indptr=t(indptr), sparse_indices=t(idx),
+                          sparse_values=t(val))
+
+    def materialize(self, out: TopK, mode: str, resolved: str, b: int = 0,
+                    threshold: float | None = None) -> list[RetrievalResult]:
+        """Row b of a device TopK -> fresh RetrievalResult objects from the payload table
+        (qdrant.py:334-346)."""
+        coll = self._collections[resolved]
+        count = int(out.count[b].item())
+        ids = out.ids[b, :count].cpu().tolist()
+        scores = (out.rank if mode == "hybrid" else out.scores)[b, :count].cpu().tolist()
+        results = []
+        for pid, score in zip(ids, scores):
+            if threshold is not None and score < threshold:
+                continue
+            p = coll.payloads[pid]
+            chunk = AudioChunk(text=p.get("text", ""), start=p.get("start", 0.0),
+                               end=p.get("end", 0.0), speaker=p.get("speaker"),
+                               metadata=p.get("metadata"))
+            results.append(RetrievalResult(chunk=chunk, score=float(score), source=resolved))
+        return results
+
+    @timed
+    def search(self, query_embedding: EmbeddingResult, top_k: int | None = None,
+               collection_name: str | None = None, filter_metadata: dict | None = None,
+               search_type: str | None = None) -> list[RetrievalResult]:
+        resolved = self._ensure_collection(collection_name)
+        top_k = top_k or self.config.top_k
+        search_type = search_type or self.config.search_type
+        try:
+            batch = self.to_query_batch([query_embedding])
+            out, mode = self.search_batch(batch, top_k, resolved, filter_metadata, search_type)
+            thr = None
+            if mode == "legacy_dense" and self.config.score_threshold > 0:
+                thr = self.config.score_threshold
+            results = self.materialize(out, mode, resolved, 0, thr)
+            logger.debug(f"Search returned {len(results)} results")
+            return results
+        except Exception as e:
+            raise RetrievalError(f"Search failed in '{resolved}': {e}")

@@ -136,36 +136,24 @@ def main() -> None:
 
     from audio_rag_amd import _armi
     from audio_rag_amd.retrieval.device import DenseIndex, merge_shards
+    from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
 
     n, dim, batch, k = args.chunks, args.dim, args.batch, args.top_k
-    lo = n * rank // world
-    hi = n * (rank + 1) // world
+    lo, hi = shard_range(n, rank, world)
     rows = make_rows(lo, hi - lo, dim, dev)
     index = DenseIndex(rows, ordinal_base=lo)
     n_q_batches = 8
     queries = make_queries(n_q_batches, batch, dim, dev, seed=1 + rank)
-    all_q = torch.empty((world * batch, dim), dtype=torch.float16, device=dev)
     ws = torch.empty(index.workspace_bytes(world * batch, k), dtype=torch.uint8, device=dev)
-    g_a = torch.empty((world, world * batch, 2 * k), dtype=torch.int64, device=dev)
-    g_b = torch.empty((world, world * batch, k + 1), dtype=torch.int32, device=dev)
+    sharded = None
+    if distributed:
+        sharded = ShardedSearch(lambda q, kk: index.topk(q, kk, workspace=ws), merge_shards)
 
     def step(i: int, q_local: torch.Tensor | None = None):
         ql = q_local if q_local is not None else queries[i % n_q_batches]
-        if not distributed:
+        if sharded is None:
             return index.topk(ql, k, workspace=ws)
-        dist.all_gather_into_tensor(all_q[:world * ql.shape[0]], ql)
-        local = index.topk(all_q[:world * ql.shape[0]], k, workspace=ws)
-        nb = ql.shape[0]
-        pack_a = torch.cat([local.rank.view(torch.int64), local.ids], dim=1)
-        pack_b = torch.cat([local.scores.view(torch.int32), local.count[:, None]], dim=1)
-        ga = g_a[:, :world * nb]
-        gb = g_b[:, :world * nb]
-        dist.all_gather_into_tensor(ga, pack_a.contiguous())
-        dist.all_gather_into_tensor(gb, pack_b.contiguous())
-        mine_a = ga[:, rank * nb:(rank + 1) * nb]
-        mine_b = gb[:, rank * nb:(rank + 1) * nb]
-        return merge_shards(mine_a[..., :k].contiguous().view(torch.float64), mine_b[..., :k].contiguous().view(torch.float32),
-                            mine_a[..., k:].contiguous(), mine_b[..., k].contiguous(), k)
+        return sharded.dense(ql, k)
 
     def barrier():
         if distributed:
@@ -192,7 +180,9 @@ def main() -> None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    certified = float((last.flags == 1).float().mean().item()) if last.flags is not None else None
+    certified = None
+    if last is not None and last.flags is not None:
+        certified = float((last.flags == 1).float().mean().item())
 
     # p50 latency of one step (batch of 64 per GPU) and of a single query
     lat, lat1 = [], []

@@ -1,0 +1,136 @@
+"""Sharded search over a world_size-2 gloo process group on the CPU: the collective plumbing of
+audio_rag_amd/retrieval/shards.py (query all-gather, packed candidate all-gather, per-rank
+slicing, merge, hybrid RRF) must give every rank exactly the global answer for its queries.
+The per-shard search and the merge are CPU stand-ins built on the oracle (this test checks the
+exchange, the GPU kernels are checked by the -m gpu tests)."""
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+N, DIM, B, K = 1500, 256, 5, 7
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _topk_t(ids, scores, rank, count):
+    from audio_rag_amd.retrieval.device import TopK
+
+    return TopK(scores=torch.from_numpy(np.ascontiguousarray(scores, dtype=np.float32)),
+                ids=torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int64)),
+                rank=torch.from_numpy(np.ascontiguousarray(rank, dtype=np.float64)),
+                count=torch.from_numpy(np.ascontiguousarray(count, dtype=np.int32)))
+
+
+def cpu_merge(rank, scores, ids, count, k):
+    """Merge [S, B, k] lists by (key desc, ordinal asc) — CPU stand-in of armi_topk_merge_shards."""
+    s, b, _ = ids.shape
+    out_ids = np.full((b, k), -1, np.int64)
+    out_sc = np.full((b, k), -np.inf, np.float32)
+    out_rk = np.full((b, k), -np.inf, np.float64)
+    out_ct = np.zeros(b, np.int32)
+    for q in range(b):
+        pool = []
+        for sh in range(s):
+            for j in range(int(count[sh, q])):
+                pool.append((-float(rank[sh, q, j]), int(ids[sh, q, j]), float(scores[sh, q, j])))
+        pool.sort()
+        for j, (nk, oid, sc) in enumerate(pool[:k]):
+            out_ids[q, j], out_sc[q, j], out_rk[q, j] = oid, sc, -nk
+        out_ct[q] = min(k, len(pool))
+    return _topk_t(out_ids, out_sc, out_rk, out_ct)
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
+    from oracle import oracle as o
+
+    rows = o.unit_fp16(N, DIM, seed=3)
+    csr = o.sparse_corpus(N, seed=4)
+    lo, hi = shard_range(N, rank, world)
+    shard_csr = (csr[0][lo:hi + 1] - csr[0][lo], csr[1][csr[0][lo]:csr[0][hi]], csr[2][csr[0][lo]:csr[0][hi]])
+
+    def local_dense(q, k):
+        r = o.dense_topk(rows[lo:hi], q.numpy().view(np.uint16), k, ordinal_base=lo)
+        return _topk_t(r.ids, r.scores, r.rank, r.count)
+
+    def local_sparse(qcsr, k):
+        qi, qx, qv = (t.numpy() for t in qcsr)
+        r = o.sparse_topk(*shard_csr, qi, qx, qv, k, ordinal_base=lo)
+        return _topk_t(r.ids, r.scores, r.scores.astype(np.float64), r.count)
+
+    def merge(rank_, scores, ids, count, k):
+        return cpu_merge(rank_.numpy(), scores.numpy(), ids.numpy(), count.numpy(), k)
+
+    def rrf(d, s, k):
+        b = d.ids.shape[0]
+        ids = np.full((b, k), -1, np.int64)
+        sc = np.zeros((b, k), np.float64)
+        cnt = np.zeros(b, np.int32)
+        for q in range(b):
+            f = o.rrf([list(d.ids[q, :d.count[q]].tolist()), list(s.ids[q, :s.count[q]].tolist())], k)
+            cnt[q] = len(f)
+            for j, (p, v) in enumerate(f):
+                ids[q, j], sc[q, j] = p, v
+        return _topk_t(ids, sc.astype(np.float32), sc, cnt)
+
+    ss = ShardedSearch(local_dense, merge, local_sparse=local_sparse, rrf=rrf)
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    q_mine = torch.from_numpy(q_all[rank * B:(rank + 1) * B].view(np.float16).copy())
+    qi, qx, qv = o.sparse_queries(B * world, seed=6)
+    a, b = qi[rank * B], qi[(rank + 1) * B]
+    q_csr = (torch.from_numpy(qi[rank * B:(rank + 1) * B + 1] - a), torch.from_numpy(qx[a:b]),
+             torch.from_numpy(qv[a:b]))
+    d = ss.dense(q_mine, K)
+    s = ss.sparse(q_csr, K)
+    h = ss.hybrid(q_mine, q_csr, K)
+    np.savez(Path(out_dir) / f"rank{rank}.npz", d_ids=d.ids.numpy(), d_rank=d.rank.numpy(),
+             d_cnt=d.count.numpy(), s_ids=s.ids.numpy(), s_sc=s.scores.numpy(),
+             s_cnt=s.count.numpy(), h_ids=h.ids.numpy(), h_sc=h.rank.numpy(), h_cnt=h.count.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_search_equals_global(tmp_path, oracle_mod):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    o = oracle_mod
+    rows = o.unit_fp16(N, DIM, seed=3)
+    csr = o.sparse_corpus(N, seed=4)
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    qcsr = o.sparse_queries(B * world, seed=6)
+    gd = o.dense_topk(rows, q_all, K)
+    gs = o.sparse_topk(*csr, *qcsr, K)
+    gd2 = o.dense_topk(rows, q_all, 2 * K)
+    gs2 = o.sparse_topk(*csr, *qcsr, 2 * K)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        sl = slice(r * B, (r + 1) * B)
+        np.testing.assert_array_equal(z["d_ids"], gd.ids[sl])
+        np.testing.assert_array_equal(z["d_rank"][z["d_ids"] >= 0], gd.rank[sl][gd.ids[sl] >= 0])
+        np.testing.assert_array_equal(z["d_cnt"], gd.count[sl])
+        np.testing.assert_array_equal(z["s_cnt"], gs.count[sl])
+        for q in range(B):
+            c = gs.count[sl][q]
+            np.testing.assert_array_equal(z["s_ids"][q, :c], gs.ids[sl][q, :c])
+            np.testing.assert_array_equal(z["s_sc"][q, :c], gs.scores[sl][q, :c])
+            want = o.rrf([list(gd2.ids[r * B + q, :gd2.count[r * B + q]]),
+                          list(gs2.ids[r * B + q, :gs2.count[r * B + q]])], K)
+            assert z["h_cnt"][q] == len(want)
+            assert [int(x) for x in z["h_ids"][q, :len(want)]] == [p for p, _ in want]
+            assert [float(x) for x in z["h_sc"][q, :len(want)]] == [v for _, v in want]
