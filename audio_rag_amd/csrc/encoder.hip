@@ -132,7 +132,8 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta,
                                                     float* __restrict__ out, int n_seq, int L,
-                                                    int width, int pad_id, float eps) {
+                                                    int width, int pad_id, int vocab, int n_pos,
+                                                    float eps) {
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tok >= (int64_t)n_seq * L) return;
   const int lane = threadIdx.x & 63;
@@ -145,8 +146,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
     const bool nonpad = (c <= t) && (row_ids[c] != pad_id);
     count += __popcll(__ballot(nonpad));
   }
-  const int id = row_ids[t];
-  const int pid = (id != pad_id) ? pad_id + count : pad_id;
+  int id = row_ids[t];
+  int pid = (id != pad_id) ? pad_id + count : pad_id;
+  if (id < 0 || id >= vocab) id = 3;  // <unk>
+  pid = pid < n_pos ? pid : n_pos - 1;
   const float* w = word + (int64_t)id * width;
   const float* pp = pos + (int64_t)pid * width;
   float v[kMaxPerLane];
@@ -238,15 +241,16 @@ int armi_enc_bias_gelu(float* x, const float* bias, int64_t n_rows, int width,
 
 int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
-                   int width, int pad_id, float eps, hipStream_t stream) {
+                   int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream) {
   ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane, "embed: width must be in [1, 1024]");
+  ARMI_REQUIRE(vocab > 3 && n_pos > pad_id + 1 && pad_id >= 0, "embed: bad vocab / n_pos / pad_id");
   ARMI_REQUIRE(L >= 1, "embed: L must be >= 1");
   if (n_seq <= 0) return ARMI_OK;
   ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
                "embed: null pointer argument");
   const int64_t toks = (int64_t)n_seq * L;
   embed_kernel<<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
-      ids, word, pos, type0, gamma, beta, out, n_seq, L, width, pad_id, eps);
+      ids, word, pos, type0, gamma, beta, out, n_seq, L, width, pad_id, vocab, n_pos, eps);
   ARMI_LAUNCHED("embed_kernel");
   return ARMI_OK;
 }

@@ -91,65 +91,124 @@ __device__ __forceinline__ void topm_insert(float x, int32_t id, float (&s)[kLan
   disc = fmaxf(disc, x);
 }
 
-// Score one row for this lane's query. Returns false when the row shares no index with it.
-__device__ __forceinline__ bool score_row(int64_t a, int64_t e, int lane, int32_t vocab,
+constexpr int kSlots = kQB * kMaxTerms;
+constexpr int kHitBatch = 16;
+
+__device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ int64_t rl_64(int64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v & 0xffffffffu), lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float rl_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+constexpr uint32_t kAbsent = 0xffffffffu;  // weights[slot][q] bit pattern: q lacks the term
+
+// Walks rows [r0, r1) of the CSR as one flat entry stream [indptr[r0], indptr[r1]), lane l of
+// the wave accumulating query l. Per 64-entry block the hit entries (index present in the
+// batch's term table) are compacted into this wave's LDS scratch with one mbcnt-ranked write,
+// then walked with broadcast LDS reads: no per-hit ballot / readlane scalar work. Loads are
+// issued in the order they are consumed (vmcnt retires in issue order): block i's weight loads
+// first, then block i+1's term-slot lookups, then block i+2's index / value loads. Hits are added
+// in ascending entry order = ascending index order within a row (fp32, multiply and add rounded
+// separately, as Qdrant). on_row(row, score, any) runs once per row, in row order.
+template <typename OnRow>
+__device__ __forceinline__ void scan_rows(int64_t r0, int64_t r1, int lane, int32_t vocab,
+                                          const int64_t* __restrict__ indptr,
                                           const int32_t* __restrict__ indices,
                                           const float* __restrict__ values,
                                           const int32_t* __restrict__ slot_of_term,
-                                          const float* __restrict__ weights,
-                                          const unsigned long long* __restrict__ qmask,
-                                          float& score) {
+                                          const float* __restrict__ weights, int* lds_slot,
+                                          float* lds_val, int* lds_pos, OnRow&& on_row) {
+  if (r0 >= r1) return;
+  const int64_t p_begin = indptr[r0];
+  const int64_t p_end = indptr[r1];
+  int64_t r = r0;
+  int64_t win = r0;
+  int64_t ends = (win + lane < r1) ? indptr[win + lane + 1] : p_end;
+  int64_t e_cur = rl_64(ends, 0);
   float acc = 0.0f;
   bool any = false;
-  for (int64_t c0 = a; c0 < e; c0 += 64) {
-    const int64_t j = c0 + lane;
-    int s = kNoSlot;
-    float dv = 0.f;
-    if (j < e) {
-      const int32_t t = indices[j];
-      if (t >= 0 && t < vocab) s = slot_of_term[t];
-      dv = values[j];
+  auto next_row = [&]() {
+    on_row(r, acc, any);
+    acc = 0.0f;
+    any = false;
+    ++r;
+    if (r < r1) {
+      if (r - win >= 64) {
+        win = r;
+        ends = (win + lane < r1) ? indptr[win + lane + 1] : p_end;
+      }
+      e_cur = rl_64(ends, (int)(r - win));
     }
-    // a slot is a pair index of this pass: anything else (the memset pattern) is "absent"
-    const bool present = s >= 0 && s < kQB * kMaxTerms;
-    unsigned long long m = __ballot(present);
-    while (m) {
-      // up to 8 hits in flight, then accumulate them in ascending index order
-      int hs[8];
-      float hv[8], hw[8];
-      unsigned long long hq[8];
-      int nh = 0;
+  };
+  auto load_block = [&](int64_t p0, int32_t& t, float& v) {
+    const int64_t j = p0 + lane;
+    t = -1;
+    v = 0.f;
+    if (j < p_end) {
+      t = indices[j];
+      v = values[j];
+    }
+  };
+  auto lookup = [&](int32_t t) -> int {
+    int sl = -1;
+    if (t >= 0 && t < vocab) sl = slot_of_term[t];
+    return (sl >= 0 && sl < kSlots) ? sl : -1;
+  };
+  int32_t tb, tc;
+  float va, vb, vc;
+  load_block(p_begin, tb, va);
+  int sa = lookup(tb);
+  load_block(p_begin + 64, tb, vb);
+  for (int64_t p0 = p_begin; p0 < p_end; p0 += 64) {
+    const unsigned long long m = __ballot(sa >= 0);
+    const int nh = __popcll(m);
+    if (sa >= 0) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      lds_slot[rank] = sa;
+      lds_val[rank] = va;
+      lds_pos[rank] = lane;
+    }
+    int sb = -1;
+    bool prefetched = false;
+    for (int h0 = 0; h0 < nh; h0 += kHitBatch) {
+      float hw[kHitBatch];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (m) {
-          const int b = __ffsll((long long)m) - 1;
-          m &= m - 1;
-          hs[u] = __shfl(s, b);
-          hv[u] = __shfl(dv, b);
-          nh = u + 1;
-        } else {
-          hs[u] = 0;
-          hv[u] = 0.f;
-        }
+      for (int u = 0; u < kHitBatch; ++u) {
+        hw[u] = __uint_as_float(kAbsent);
+        if (h0 + u < nh) hw[u] = weights[lds_slot[h0 + u] * kQB + lane];
+      }
+      if (!prefetched) {
+        sb = lookup(tb);
+        load_block(p0 + 128, tc, vc);
+        prefetched = true;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (u < nh) {
-          hq[u] = qmask[hs[u]];
-          hw[u] = weights[(size_t)hs[u] * kQB + lane];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (u < nh && ((hq[u] >> lane) & 1ull)) {
-          acc = __fadd_rn(acc, __fmul_rn(hw[u], hv[u]));
-          any = true;
+      for (int u = 0; u < kHitBatch; ++u) {
+        if (h0 + u < nh) {
+          const int64_t pos = p0 + __builtin_amdgcn_readfirstlane(lds_pos[h0 + u]);
+          while (pos >= e_cur) next_row();
+          if (__float_as_uint(hw[u]) != kAbsent) {
+            acc = __fadd_rn(acc, __fmul_rn(hw[u], lds_val[h0 + u]));
+            any = true;
+          }
         }
       }
     }
+    if (!prefetched) {
+      sb = lookup(tb);
+      load_block(p0 + 128, tc, vc);
+    }
+    sa = sb;
+    va = vb;
+    tb = tc;
+    vb = vc;
   }
-  score = acc;
-  return any;
+  while (r < r1) next_row();
 }
 
 __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
@@ -161,10 +220,17 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   __shared__ float lkey[kQB][kWavesPerWG * kLaneList];
   __shared__ int32_t lrow[kQB][kWavesPerWG * kLaneList];
   __shared__ float ldisc[kQB][kWavesPerWG];
+  __shared__ int hslot[kWavesPerWG][64];
+  __shared__ float hval[kWavesPerWG][64];
+  __shared__ int hpos[kWavesPerWG][64];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t lo = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t hi = min(lo + rows_per_wg, n_rows);
+  // contiguous rows per wave keep each wave's CSR stream sequential
+  const int64_t span = hi > lo ? hi - lo : 0;
+  const int64_t r0 = lo + span * wave / kWavesPerWG;
+  const int64_t r1 = lo + span * (wave + 1) / kWavesPerWG;
   float s[kLaneList];
   int32_t ix[kLaneList];
 #pragma unroll
@@ -173,17 +239,15 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     ix[j] = 0x7fffffff;
   }
   float disc = kNegInf;
-  for (int64_t r = lo + wave; r < hi; r += kWavesPerWG) {
-    if (row_mask && !((row_mask[r >> 6] >> (r & 63)) & 1ull)) continue;
-    float sc;
-    const bool hit = score_row(indptr[r], indptr[r + 1], lane, vocab, indices, values,
-                               slot_of_term, weights, qmask, sc);
-    if (__any(hit && sc > s[kLaneList - 1]) ) {
-      if (hit) topm_insert(sc, (int32_t)r, s, ix, disc);
-    } else if (hit) {
-      disc = fmaxf(disc, sc);
-    }
-  }
+  scan_rows(r0, r1, lane, vocab, indptr, indices, values, slot_of_term, weights, hslot[wave],
+            hval[wave], hpos[wave], [&](int64_t row, float sc, bool hit) {
+              if (row_mask && !((row_mask[row >> 6] >> (row & 63)) & 1ull)) return;
+              if (__any(hit && sc > s[kLaneList - 1])) {
+                if (hit) topm_insert(sc, (int32_t)row, s, ix, disc);
+              } else if (hit) {
+                disc = fmaxf(disc, sc);
+              }
+            });
 #pragma unroll
   for (int j = 0; j < kLaneList; ++j) {
     lkey[lane][wave * kLaneList + j] = s[j];
@@ -317,25 +381,29 @@ __global__ __launch_bounds__(kScanThreads) void sparse_collect_kernel(
     const float* __restrict__ weights, const unsigned long long* __restrict__ qmask,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
     int32_t* __restrict__ coll_row) {
+  __shared__ int hslot[kWavesPerWG][64];
+  __shared__ float hval[kWavesPerWG][64];
+  __shared__ int hpos[kWavesPerWG][64];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const float t = lane < nq ? thr[lane] : std::numeric_limits<float>::infinity();
   if (__all(t == std::numeric_limits<float>::infinity())) return;
   const int64_t lo = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t hi = min(lo + rows_per_wg, n_rows);
-  for (int64_t r = lo + wave; r < hi; r += kWavesPerWG) {
-    if (row_mask && !((row_mask[r >> 6] >> (r & 63)) & 1ull)) continue;
-    float sc;
-    const bool hit = score_row(indptr[r], indptr[r + 1], lane, vocab, indices, values,
-                               slot_of_term, weights, qmask, sc);
-    if (hit && sc >= t) {
-      const int slot = atomicAdd(&coll_count[lane], 1);
-      if (slot < kCollectCap) {
-        coll_key[(size_t)lane * kCollectCap + slot] = sc;
-        coll_row[(size_t)lane * kCollectCap + slot] = (int32_t)r;
-      }
-    }
-  }
+  const int64_t span = hi > lo ? hi - lo : 0;
+  const int64_t r0 = lo + span * wave / kWavesPerWG;
+  const int64_t r1 = lo + span * (wave + 1) / kWavesPerWG;
+  scan_rows(r0, r1, lane, vocab, indptr, indices, values, slot_of_term, weights, hslot[wave],
+            hval[wave], hpos[wave], [&](int64_t row, float sc, bool hit) {
+              if (row_mask && !((row_mask[row >> 6] >> (row & 63)) & 1ull)) return;
+              if (hit && sc >= t) {
+                const int slot = atomicAdd(&coll_count[lane], 1);
+                if (slot < kCollectCap) {
+                  coll_key[(size_t)lane * kCollectCap + slot] = sc;
+                  coll_row[(size_t)lane * kCollectCap + slot] = (int32_t)row;
+                }
+              }
+            });
 }
 
 __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
@@ -491,6 +559,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     }
     ARMI_HIP(hipMemsetAsync(w.slot_of_term, 0x7f, sizeof(int32_t) * idx->vocab, stream));
     ARMI_HIP(hipMemsetAsync(w.qmask, 0, sizeof(unsigned long long) * kQB * kMaxTerms, stream));
+    ARMI_HIP(hipMemsetAsync(w.weights, 0xff, sizeof(float) * kQB * kMaxTerms * kQB, stream));
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
     term_slots_kernel<<<dim3(nqp), dim3(64), 0, stream>>>(q_indptr + q0, q_indices, idx->vocab,
                                                           w.slot_of_term);

@@ -68,9 +68,25 @@ class CrossEncoderXLMR:
                 bo2=sd[p + "output.dense.bias"],
                 ln2=(sd[p + "output.LayerNorm.weight"], sd[p + "output.LayerNorm.bias"]),
             ))
+        self.gemm_dtype = torch.float32
         self.head = (sd["classifier.dense.weight"], sd["classifier.dense.bias"],
                      sd["classifier.out_proj.weight"].reshape(-1).contiguous(),
                      sd["classifier.out_proj.bias"])
+
+    def to_dtype(self, dtype: torch.dtype) -> None:
+        """GEMM operand dtype (fp32 or bf16, fp32 accumulate); LayerNorm / softmax / GELU / head
+        stay fp32 in the armi kernels."""
+        self.gemm_dtype = dtype
+        for ly in self.layers:
+            for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
+                ly[name + "_g"] = ly[name].to(dtype)
+
+    def _mm(self, x: torch.Tensor, ly: dict, name: str, bias: torch.Tensor | None) -> torch.Tensor:
+        if self.gemm_dtype == torch.float32:
+            w = ly[name]
+            return torch.addmm(bias, x, w) if bias is not None else torch.mm(x, w)
+        y = torch.mm(x.to(self.gemm_dtype), ly[name + "_g"]).float()
+        return y.add_(bias) if bias is not None else y
 
     @torch.inference_mode()
     def forward(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
@@ -80,22 +96,31 @@ class CrossEncoderXLMR:
         s = stream_handle()
         h = torch.empty((n * L, d), dtype=torch.float32, device=self.device)
         call("armi_enc_embed", ptr(ids), ptr(self.word), ptr(self.pos), ptr(self.type0),
-             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad, self.eps, s)
+             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad,
+             self.word.shape[0], self.pos.shape[0], self.eps, s)
         scale = 1.0 / math.sqrt(dh)
         for ly in self.layers:
-            qkv = torch.addmm(ly["bqkv"], h, ly["wqkv_t"])                  # [n*L, 3d]
+            qkv = self._mm(h, ly, "wqkv_t", ly["bqkv"])                     # [n*L, 3d]
             qkv = qkv.view(n, L, 3, H, dh).permute(2, 0, 3, 1, 4)          # [3, n, H, L, dh]
             q, k, v = qkv[0], qkv[1], qkv[2]
-            scores = torch.matmul(q, k.transpose(-1, -2)).contiguous()    # [n, H, L, L]
+            if self.gemm_dtype == torch.float32:
+                scores = torch.matmul(q, k.transpose(-1, -2)).contiguous()  # [n, H, L, L]
+            else:
+                scores = torch.matmul(q.to(self.gemm_dtype),
+                                      k.to(self.gemm_dtype).transpose(-1, -2)).float().contiguous()
             call("armi_enc_masked_softmax", ptr(scores), ptr(mask), n, H, L, scale, s)
-            ctx = torch.matmul(scores, v).permute(0, 2, 1, 3).reshape(n * L, d)
-            attn = torch.addmm(ly["bo"], ctx, ly["wo_t"])
+            if self.gemm_dtype == torch.float32:
+                ctx = torch.matmul(scores, v)
+            else:
+                ctx = torch.matmul(scores.to(self.gemm_dtype), v.to(self.gemm_dtype)).float()
+            ctx = ctx.permute(0, 2, 1, 3).reshape(n * L, d)
+            attn = self._mm(ctx, ly, "wo_t", ly["bo"])
             h1 = torch.empty_like(h)
             call("armi_enc_layernorm_residual", ptr(attn), ptr(h), ptr(ly["ln1"][0]),
                  ptr(ly["ln1"][1]), ptr(h1), n * L, d, self.eps, s)
-            inter = torch.mm(h1, ly["wi_t"])
+            inter = self._mm(h1, ly, "wi_t", None)
             call("armi_enc_bias_gelu", ptr(inter), ptr(ly["bi"]), n * L, inter.shape[1], s)
-            out = torch.addmm(ly["bo2"], inter, ly["wo2_t"])
+            out = self._mm(inter, ly, "wo2_t", ly["bo2"])
             h = torch.empty_like(h)
             call("armi_enc_layernorm_residual", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
                  ptr(ly["ln2"][1]), ptr(h), n * L, d, self.eps, s)

@@ -205,9 +205,11 @@ def merge_shards(rank: torch.Tensor, scores: torch.Tensor, ids: torch.Tensor, co
                ids=torch.empty((b, k_out), dtype=torch.int64, device=dev),
                rank=torch.empty((b, k_out), dtype=torch.float64, device=dev),
                count=torch.empty(b, dtype=torch.int32, device=dev))
-    call("armi_topk_merge_shards", ptr(rank.contiguous()), ptr(scores.contiguous()),
-         ptr(ids.contiguous()), ptr(count.contiguous()), s, b, k_in, k_out, ptr(out.rank),
-         ptr(out.scores), ptr(out.ids), ptr(out.count), stream_handle())
+    # hold the contiguous copies until the launch is enqueued (a freed temporary's block can be
+    # handed to the next allocation before the kernel reads it)
+    rank, scores, ids, count = (t.contiguous() for t in (rank, scores, ids, count))
+    call("armi_topk_merge_shards", ptr(rank), ptr(scores), ptr(ids), ptr(count), s, b, k_in,
+         k_out, ptr(out.rank), ptr(out.scores), ptr(out.ids), ptr(out.count), stream_handle())
     return out
 
 
@@ -220,9 +222,10 @@ def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
     out_ids = torch.empty((n, limit), dtype=torch.int64, device=dev)
     out_score = torch.empty((n, limit), dtype=torch.float64, device=dev)
     out_count = torch.empty(n, dtype=torch.int32, device=dev)
-    call("armi_rrf_fuse", ptr(a.ids.contiguous()), ptr(a.count), ka, ptr(b.ids.contiguous()),
-         ptr(b.count), kb, n, rrf_k, limit, ptr(out_ids), ptr(out_score), ptr(out_count),
-         stream_handle())
+    a_ids, b_ids = a.ids.contiguous(), b.ids.contiguous()
+    a_cnt, b_cnt = a.count.to(torch.int32).contiguous(), b.count.to(torch.int32).contiguous()
+    call("armi_rrf_fuse", ptr(a_ids), ptr(a_cnt), ka, ptr(b_ids), ptr(b_cnt), kb, n, rrf_k, limit,
+         ptr(out_ids), ptr(out_score), ptr(out_count), stream_handle())
     return TopK(scores=out_score.float(), ids=out_ids, rank=out_score, count=out_count)
 
 

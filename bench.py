@@ -60,6 +60,74 @@ def make_queries(n_batches: int, batch: int, dim: int, device, seed: int) -> tor
     return (x / x.norm(dim=2, keepdim=True)).half().contiguous()
 
 
+VOCAB = 250002
+
+
+def _zipf_cdf(device, a: float = 1.1) -> torch.Tensor:
+    r = torch.arange(1, VOCAB - 4 + 1, dtype=torch.float64, device=device)
+    p = r.pow(-a)
+    return torch.cumsum(p / p.sum(), 0)
+
+
+def _sparse_rows(n: int, mean_nnz: float, lo: int, hi: int, wlo: float, whi: float,
+                 g: torch.Generator, cdf: torch.Tensor, cap: int):
+    """SURVEY §8(d) law on the device: nnz ~ clip(Poisson(mean), lo, hi), unique Zipf(1.1) token
+    ids in [4, VOCAB) (sorted per row), weights U(wlo, whi). Returns (counts, indices, values)."""
+    dev = cdf.device
+    nnz = torch.poisson(torch.full((n,), mean_nnz, device=dev), generator=g).clamp_(lo, hi)
+    u = torch.rand((n, cap), generator=g, device=dev, dtype=torch.float64)
+    ids = torch.searchsorted(cdf, u).clamp_(max=VOCAB - 5).to(torch.int32) + 4
+    ids, _ = torch.sort(ids, dim=1)
+    fresh = torch.ones_like(ids, dtype=torch.bool)
+    fresh[:, 1:] = ids[:, 1:] != ids[:, :-1]
+    rank = torch.cumsum(fresh.to(torch.int32), dim=1)
+    keep = fresh & (rank <= nnz[:, None].to(torch.int32))
+    counts = keep.sum(dim=1)
+    idx = ids[keep]
+    vals = torch.empty(idx.numel(), device=dev).uniform_(wlo, whi, generator=g)
+    return counts, idx.contiguous(), vals.contiguous()
+
+
+def make_sparse_rows(first: int, count: int, device, seed: int = 2):
+    """CSR rows [first, first+count) of the global synthetic sparse corpus (64k-row chunks with
+    their own seeds, as make_rows)."""
+    cdf = _zipf_cdf(device)
+    cnts, idxs, vals = [], [], []
+    c0 = first // CHUNK_ROWS
+    c1 = (first + count + CHUNK_ROWS - 1) // CHUNK_ROWS
+    for c in range(c0, c1):
+        a = c * CHUNK_ROWS
+        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
+        cnt, idx, val = _sparse_rows(CHUNK_ROWS, 96.0, 16, 256, 0.01, 0.40, g, cdf, cap=320)
+        off = torch.zeros(CHUNK_ROWS + 1, dtype=torch.int64, device=device)
+        off[1:] = torch.cumsum(cnt, 0)
+        lo, hi = max(a, first) - a, min(a + CHUNK_ROWS, first + count) - a
+        if lo < hi:
+            cnts.append(cnt[lo:hi])
+            idxs.append(idx[off[lo]:off[hi]])
+            vals.append(val[off[lo]:off[hi]])
+    counts = torch.cat(cnts)
+    indptr = torch.zeros(count + 1, dtype=torch.int64, device=device)
+    indptr[1:] = torch.cumsum(counts, 0)
+    return indptr, torch.cat(idxs).contiguous(), torch.cat(vals).contiguous()
+
+
+def make_sparse_queries(n: int, device, seed: int):
+    g = torch.Generator(device=device).manual_seed(seed)
+    cnt, idx, val = _sparse_rows(n, 12.0, 1, 32, 0.05, 0.35, g, _zipf_cdf(device), cap=48)
+    indptr = torch.zeros(n + 1, dtype=torch.int32, device=device)
+    indptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    return indptr, idx, val
+
+
+def doc_tokens(ordinals: torch.Tensor, length: int) -> torch.Tensor:
+    """Synthetic token ids of a chunk (240 tokens, ids in [4, VOCAB)), a pure
+    function of the chunk ordinal so every rank can build rerank pairs without a payload table."""
+    pos = torch.arange(length, device=ordinals.device, dtype=torch.int64)
+    h = ordinals[..., None].to(torch.int64) * 2654435761 + pos * 40503 + 12345
+    return (h % (VOCAB - 4) + 4).to(torch.int32)
+
+
 def cpu_baseline(n_full: int, dim: int, batch: int, k: int, budget_s: float = 12.0) -> dict:
     """The reference's CPU path for this search: qdrant-client local mode COSINE (fp32 rows
     normalised at insert, fp32 dot, arg-selection), restated in numpy (oracle.dense_fp32_local)
@@ -121,6 +189,12 @@ def main() -> None:
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=30)
+    ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank"], default="dense",
+                    help="dense: BASELINE metric (default); hybrid: dense+sparse prefetch 2k + RRF "
+                         "(configs[2] without rerank); hybrid_rerank: configs[2]: top-20 fused -> "
+                         "cross-encoder -> top-k")
+    ap.add_argument("--initial-k", type=int, default=20)
+    ap.add_argument("--rerank-dtype", choices=["fp32", "bf16"], default="fp32")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,25 +209,78 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=dev)
 
     from audio_rag_amd import _armi
-    from audio_rag_amd.retrieval.device import DenseIndex, merge_shards
+    from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex, TopK, merge_shards, rrf_fuse
     from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
 
     n, dim, batch, k = args.chunks, args.dim, args.batch, args.top_k
+    wl = args.workload
+    search_k = k if wl == "dense" else (args.initial_k if wl == "hybrid_rerank" else k)
+    pre_k = search_k if wl == "dense" else 2 * search_k
     lo, hi = shard_range(n, rank, world)
     rows = make_rows(lo, hi - lo, dim, dev)
     index = DenseIndex(rows, ordinal_base=lo)
     n_q_batches = 8
     queries = make_queries(n_q_batches, batch, dim, dev, seed=1 + rank)
-    ws = torch.empty(index.workspace_bytes(world * batch, k), dtype=torch.uint8, device=dev)
+    ws = torch.empty(index.workspace_bytes(world * batch, pre_k), dtype=torch.uint8, device=dev)
+    sindex = None
+    q_sparse = []
+    if wl != "dense":
+        sindex = SparseIndex(*make_sparse_rows(lo, hi - lo, dev), vocab=VOCAB, ordinal_base=lo)
+        sws = torch.empty(sindex.workspace_bytes(world * batch, pre_k), dtype=torch.uint8, device=dev)
+        q_sparse = [make_sparse_queries(batch, dev, seed=1000 * (1 + rank) + j) for j in range(n_q_batches)]
+    reranker = None
+    if wl == "hybrid_rerank":
+        from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
+        reranker = CrossEncoderXLMR(build_reranker(seed=5), dev)
+        if args.rerank_dtype == "bf16":
+            reranker.to_dtype(torch.bfloat16)
+        gq = torch.Generator(device=dev).manual_seed(4 + rank)
+        q_tokens = torch.randint(4, VOCAB, (n_q_batches, batch, 16), generator=gq, device=dev,
+                                 dtype=torch.int32)
     sharded = None
     if distributed:
-        sharded = ShardedSearch(lambda q, kk: index.topk(q, kk, workspace=ws), merge_shards)
+        sharded = ShardedSearch(lambda q, kk: index.topk(q, kk, workspace=ws), merge_shards,
+                                local_sparse=(lambda c, kk: sindex.topk(*c, kk, workspace=sws)) if sindex else None,
+                                rrf=lambda a, b, kk: rrf_fuse(a, b, kk))
+
+    def rerank(fused: TopK, qt: torch.Tensor) -> TopK:
+        """configs[2]: every query's fused candidates -> (query, chunk) pairs of L = 256 tokens
+        (<s> q16 </s></s> d236 </s>) -> cross-encoder -> stable sort -> top-k."""
+        nb, kc = fused.ids.shape
+        ids = fused.ids.clamp(min=0)
+        d = doc_tokens(ids, 236)
+        eos = torch.full((nb, kc, 1), 2, dtype=torch.int32, device=dev)
+        bos = torch.zeros((nb, kc, 1), dtype=torch.int32, device=dev)
+        qq = qt[:, None, :].expand(nb, kc, qt.shape[1])
+        pairs = torch.cat([bos, qq, eos, eos, d, eos], dim=2).reshape(nb * kc, -1).contiguous()
+        valid = (torch.arange(kc, device=dev)[None, :] < fused.count[:, None])
+        mask = torch.ones_like(pairs)
+        probs = reranker.forward(pairs, mask).view(nb, kc)
+        probs = torch.where(valid, probs, torch.full_like(probs, -1.0))
+        order = torch.sort(probs, dim=1, descending=True, stable=True).indices[:, :k]
+        return TopK(scores=torch.gather(probs, 1, order), ids=torch.gather(fused.ids, 1, order),
+                    rank=torch.gather(probs, 1, order).double(),
+                    count=torch.clamp(fused.count, max=k))
 
     def step(i: int, q_local: torch.Tensor | None = None):
-        ql = q_local if q_local is not None else queries[i % n_q_batches]
+        j = i % n_q_batches
+        ql = q_local if q_local is not None else queries[j]
+        if wl == "dense":
+            if sharded is None:
+                return index.topk(ql, k, workspace=ws)
+            return sharded.dense(ql, k)
+        qs = q_sparse[j]
+        if ql.shape[0] != batch:  # single-query latency probe
+            qs = (qs[0][:ql.shape[0] + 1], qs[1], qs[2])
         if sharded is None:
-            return index.topk(ql, k, workspace=ws)
-        return sharded.dense(ql, k)
+            d = index.topk(ql, pre_k, workspace=ws)
+            sp = sindex.topk(*qs, pre_k, workspace=sws)
+            fused = rrf_fuse(d, sp, search_k)
+        else:
+            fused = sharded.hybrid(ql, qs, search_k)
+        if reranker is None:
+            return fused
+        return rerank(fused, q_tokens[j][:ql.shape[0]])
 
     def barrier():
         if distributed:
@@ -181,7 +308,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     certified = None
-    if last is not None and last.flags is not None:
+    if wl == "dense" and last is not None and last.flags is not None:
         certified = float((last.flags == 1).float().mean().item())
 
     # p50 latency of one step (batch of 64 per GPU) and of a single query
@@ -225,9 +352,17 @@ def main() -> None:
         "dtype": "f16",
         "data": "synthetic: N(0,1) rows and queries L2-normalised then cast to fp16 (SURVEY.md §8(d)), resident in HBM",
         "config": {
-            "workload": (f"dense cosine top-{k} over {n} x {dim} fp16 chunks sharded by ordinal over "
-                         f"{world} GPU(s), {batch} queries per GPU per step (RCCL all-gather of "
-                         f"queries and per-shard top-{k} when N>1)"),
+            "workload": {
+                "dense": (f"dense cosine top-{k} over {n} x {dim} fp16 chunks sharded by ordinal over "
+                          f"{world} GPU(s), {batch} queries per GPU per step (RCCL all-gather of "
+                          f"queries and per-shard top-{k} when N>1)"),
+                "hybrid": (f"hybrid top-{k}: dense cosine + sparse lexical prefetch {pre_k} each, RRF "
+                           f"(1/(2+pos)), {n} chunks, {batch} queries per GPU per step"),
+                "hybrid_rerank": (f"hybrid top-{search_k} (prefetch {pre_k}+{pre_k}, RRF) -> "
+                                  f"cross-encoder (XLM-R base, 12 layers, L=256, "
+                                  f"{args.rerank_dtype} GEMMs) -> top-{k}, {n} chunks, {batch} "
+                                  f"queries per GPU per step"),
+            }[wl],
             "n_chunks": n, "dim": dim, "batch_per_gpu": batch, "top_k": k,
             "parallelism": f"corpus-shard{world}",
         },
@@ -247,7 +382,7 @@ def main() -> None:
             "launches_timed": launches.value,
         },
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and wl == "dense":
         result["cpu_baseline"] = cpu_baseline(n, dim, batch, k)
     else:
         result["cpu_baseline"] = None

@@ -180,10 +180,12 @@ int armi_enc_masked_softmax(float* scores, const int32_t* mask, int n_seq, int h
 int armi_enc_bias_gelu(float* x, const float* bias, int64_t n_rows, int width,
                        hipStream_t stream);
 /* XLM-R embeddings: word[ids] + pos[padding_idx + cumsum(ids != pad)] + type[0], then
- * LayerNorm. ids [n_seq][L] int32. */
+ * LayerNorm. ids [n_seq][L] int32; word [vocab][width], pos [n_pos][width]. Ids outside
+ * [0, vocab) embed as <unk> (id 3) and positions are clamped to n_pos - 1, so no input can read
+ * outside the tables. */
 int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
-                   int width, int pad_id, float eps, hipStream_t stream);
+                   int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
 /* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)
  * hidden [n_seq][L][width] -> out [n_seq]. */
 int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const float* dense_b,

@@ -52,7 +52,8 @@ def test_masked_softmax(gpu, L):
     add = (1 - mask.float())[:, None, None, :] * torch.finfo(torch.float32).min
     ref = torch.softmax(s * scale + add, dim=-1)
     S = s.to(gpu).contiguous()
-    _call("armi_enc_masked_softmax", S.data_ptr(), mask.to(gpu).data_ptr(), n, H, L, scale)
+    M = mask.to(gpu)
+    _call("armi_enc_masked_softmax", S.data_ptr(), M.data_ptr(), n, H, L, scale)
     torch.testing.assert_close(S.cpu(), ref, rtol=0, atol=1e-6)
 
 
@@ -62,7 +63,8 @@ def test_bias_gelu(gpu):
     b = torch.randn(3072, generator=g)
     ref = torch.nn.functional.gelu(x + b)
     X = x.to(gpu).contiguous()
-    _call("armi_enc_bias_gelu", X.data_ptr(), b.to(gpu).data_ptr(), 128, 3072)
+    Bd = b.to(gpu)
+    _call("armi_enc_bias_gelu", X.data_ptr(), Bd.data_ptr(), 128, 3072)
     torch.testing.assert_close(X.cpu(), ref, rtol=0, atol=1e-5)
 
 
@@ -81,9 +83,8 @@ def test_embed_positions_and_layernorm(gpu):
     pid = torch.cumsum(nonpad, dim=1) * nonpad + 1
     ref = torch.nn.functional.layer_norm(word[ids] + pos[pid] + typ, (d,), w, b, 1e-5)
     out = torch.empty(3 * 40, d, device=gpu)
-    _call("armi_enc_embed", ids.int().to(gpu).data_ptr(), word.to(gpu).data_ptr(),
-          pos.to(gpu).data_ptr(), typ.to(gpu).data_ptr(), w.to(gpu).data_ptr(),
-          b.to(gpu).data_ptr(), out.data_ptr(), 3, 40, d, 1, 1e-5)
+    dev = [t.to(gpu).contiguous() for t in (ids.int(), word, pos, typ, w, b)]  # keep alive
+    _call("armi_enc_embed", *(t.data_ptr() for t in dev), out.data_ptr(), 3, 40, d, 1, V, P, 1e-5)
     torch.testing.assert_close(out.cpu().view(3, 40, d), ref, rtol=0, atol=2e-5)
 
 
@@ -162,3 +163,25 @@ def test_bge_m3_embedder_outputs(gpu):
     # keys keep first-occurrence order (FlagEmbedding dict order, bge.py:100)
     first = [t for t in dict.fromkeys(ids) if t in got_lex]
     assert r.sparse.indices == first
+
+
+def test_cross_encoder_bf16_gemms_within_budget(gpu):
+    """bf16 GEMM operands (fp32 accumulate, fp32 LN/softmax/GELU): measured distance to the fp32
+    transformers forward at the full bge-reranker-base shape."""
+    from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
+
+    hf = build_reranker(seed=5, arch=dict(attn_implementation="eager"))
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(4, hf.config.vocab_size, (8, 256), generator=g)
+    ids[:, 0] = 0
+    ids[:, 17] = 2
+    ids[:, 18] = 2
+    ids[:, -1] = 2
+    mask = torch.ones_like(ids)
+    ref = _hf_scores(hf, ids, mask)
+    enc = CrossEncoderXLMR(hf, gpu)
+    enc.to_dtype(torch.bfloat16)
+    got = enc.forward(ids.int().to(gpu), mask.int().to(gpu)).cpu()
+    err = (got - ref).abs().max().item()
+    print(f"bf16 GEMM max |score error| = {err:.2e}")
+    assert err < 1e-2

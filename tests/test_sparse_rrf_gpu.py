@@ -102,3 +102,22 @@ def test_rrf_matches_qdrant_local_mode(gpu, oracle_mod, ka, kb, limit, universe)
         assert cnt[q] == len(ref)
         assert [int(x) for x in ids[q, :cnt[q]]] == [int(p) for p, _ in ref]
         assert [float(x) for x in rank[q, :cnt[q]]] == [s for _, s in ref]
+
+
+def test_sparse_empty_rows_and_long_rows(gpu, oracle_mod):
+    """Rows without sparse entries (e.g. points stored dense-only) and rows longer than a 64-entry
+    block, interleaved, so row boundaries fall anywhere inside the scan's entry blocks."""
+    indptr, indices, values = oracle_mod.sparse_corpus(5000, seed=41)
+    lens = np.diff(indptr)
+    keep = np.ones(len(lens), dtype=bool)
+    keep[::3] = False  # every third row empty
+    new_ptr = np.zeros_like(indptr)
+    np.cumsum(np.where(keep, lens, 0), out=new_ptr[1:])
+    sel = np.concatenate([np.arange(indptr[r], indptr[r + 1]) for r in range(len(lens)) if keep[r]])
+    csr = (new_ptr, indices[sel], values[sel])
+    q = oracle_mod.sparse_queries(20, seed=42)
+    idx = _sparse_index(csr, gpu)
+    for k in (3, 40):
+        got = _run(idx, q, k, gpu)
+        _same(got, oracle_mod.sparse_topk(*csr, *q, k))
+        assert not np.isin(got["ids"], np.nonzero(~keep)[0]).any()
