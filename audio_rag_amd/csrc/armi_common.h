@@ -133,6 +133,11 @@ __device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) 
   }
 }
 
+// Wave index within the workgroup as a wave-uniform (SGPR) value: the compiler cannot prove
+// threadIdx.x >> 6 uniform by itself, and everything derived from a "divergent" wave index
+// (list pointers, loop bounds, loaded metadata) would otherwise go to VGPRs and exec-masked flow.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __host__ __device__ inline int pow2_at_least(int x) {
   int p = 1;
   while (p < x) p <<= 1;

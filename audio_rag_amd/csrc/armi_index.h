@@ -19,7 +19,12 @@ struct armi_index {
   unsigned long long* invalid = nullptr;  // [1] count of rows outside the fp16 domain
 };
 
-// Sparse store: caller-owned CSR plus a device inverted index (postings) built at create time.
+// Sparse store: a device inverted index built at create time from the caller's CSR (which may
+// be freed afterwards). Term t's postings (row, value) sit in [term_ptr[t], term_ptr[t+1]),
+// ascending by row, the last slot a sentinel row (INT32_MAX); 64 sentinel slots pad the end.
+// The rows are split into n_ranges contiguous ranges of range_rows rows (a multiple of 64), one
+// scan workgroup each; terms with >= 256 postings carry start_tab[long_of[t]][range] = offset of
+// their first posting at or after the range start.
 struct armi_sparse_index {
   int device = 0;
   int64_t n_rows = 0;
@@ -27,9 +32,15 @@ struct armi_sparse_index {
   int32_t vocab = 0;
   int64_t ordinal_base = 0;
   int num_cus = 0;
-  const int64_t* indptr = nullptr;
-  const int32_t* indices = nullptr;
-  const float* values = nullptr;
+  int64_t range_rows = 0;
+  int n_ranges = 0;
+  int64_t n_postings = 0;        // valid postings + one sentinel per term
+  int64_t n_long = 0;
+  int32_t* term_ptr = nullptr;   // [vocab+1]
+  int32_t* prow = nullptr;       // [n_postings + 64]
+  float* pval = nullptr;         // [n_postings + 64]
+  int32_t* long_of = nullptr;    // [vocab] index into start_tab, -1 for short terms
+  int32_t* start_tab = nullptr;  // [n_long][n_ranges]
 };
 
 namespace armi {

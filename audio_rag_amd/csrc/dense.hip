@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   }
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6;
+  const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   const int qg = q_first + ql;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
 
   // maxima + bound of the scan workgroups
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(256) void dense_exact_scan_kernel(
   int64_t* ord = reinterpret_cast<int64_t*>(smem + 2 * cap * 8);  // [2*cap]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = armi::wave_id();
   for (int e = tid; e < 2 * cap; e += 256) {
     key[e] = kNegInfD;
     ord[e] = kNoOrd;

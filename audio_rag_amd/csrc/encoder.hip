@@ -52,7 +52,7 @@ __device__ __forceinline__ void layernorm_row(float (&v)[kMaxPerLane], int width
 __global__ __launch_bounds__(256) void layernorm_residual_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ out, int64_t n_rows, int width, float eps) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
   if (row >= n_rows) return;
   const int lane = threadIdx.x & 63;
   const float* xr = x + row * width;
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void masked_softmax_kernel(float* __restrict__
                                                              const int32_t* __restrict__ mask,
                                                              int n_seq, int heads, int L,
                                                              float scale) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
   const int64_t n_rows = (int64_t)n_seq * heads * L;
   if (row >= n_rows) return;
   const int lane = threadIdx.x & 63;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
                                                     float* __restrict__ out, int n_seq, int L,
                                                     int width, int pad_id, int vocab, int n_pos,
                                                     float eps) {
-  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t tok = (int64_t)blockIdx.x * 4 + armi::wave_id();
   if (tok >= (int64_t)n_seq * L) return;
   const int lane = threadIdx.x & 63;
   const int seq = (int)(tok / L);
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void cls_head_kernel(const float* __restrict__
   extern __shared__ __attribute__((aligned(16))) float sh[];  // [width] x0, [width] h, [4] red
   const int seq = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = armi::wave_id();
   const float* x0 = hidden + (int64_t)seq * L * width;
   float* xs = sh;
   float* hs = sh + width;

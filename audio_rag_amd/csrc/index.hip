@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void row_norms_kernel(const uint16_t* __restri
                                                         float* __restrict__ inv_norm32,
                                                         unsigned long long* __restrict__ invalid) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
   if (row >= n_padded) return;
   if (row >= n_rows) {  // tile padding: never a result
     if (lane == 0) {

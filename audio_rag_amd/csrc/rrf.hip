@@ -35,7 +35,9 @@ __global__ __launch_bounds__(64) void rrf_kernel(const int64_t* __restrict__ a_i
   const int64_t* a = a_ids + (size_t)q * ka;
   const int64_t* b = b_ids + (size_t)q * kb;
 
-  for (int i = lane; i < kPool; i += 64) {
+  // sort only the power of two covering both lists
+  const int n2 = armi::pow2_at_least(max(ca + cb, 2));
+  for (int i = lane; i < n2; i += 64) {
     score[i] = -std::numeric_limits<double>::infinity();
     id[i] = -1;
     seen[i] = 0x7fffffff;
@@ -77,9 +79,9 @@ __global__ __launch_bounds__(64) void rrf_kernel(const int64_t* __restrict__ a_i
   const int n = ca + appended;
   __syncthreads();
   // stable descending sort: key (score desc, seen asc)
-  for (int size = 2; size <= kPool; size <<= 1) {
+  for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = lane; t < kPool / 2; t += 64) {
+      for (int t = lane; t < n2 / 2; t += 64) {
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;

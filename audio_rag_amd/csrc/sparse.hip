@@ -1,4 +1,4 @@
-// Sparse lexical-weight top-k over a CSR chunk store (gfx950).
+// Sparse lexical-weight top-k over a device inverted index (gfx950).
 //
 // Restates Qdrant's sparse-vector search as called by QdrantRetriever.search
 // (src/audio_rag/retrieval/qdrant.py:289-293 sparse prefetch of hybrid search, 299-312 sparse
@@ -8,17 +8,29 @@
 //   accumulated in fp32 (multiply and add rounded separately; no FMA), only rows that share at
 //   least one index are results, ranking (score desc, ordinal asc).
 //
-// Design (one batch of up to 64 queries per scan; lane l of every wave = query l):
-//   prep:   a per-batch term table: slot_of_term[t] = the first (query, term) pair naming t,
-//           weights[slot][64] = each query's weight for that term, qmask[slot] = which queries.
-//   scan:   row-major walk of the CSR (each byte read once); for every row the wave loads 64
-//           (index, value) pairs at a time, looks each index up in slot_of_term, ballots the
-//           hits and adds the hits in ascending index order, lane-parallel over queries. Each
-//           lane keeps a 4-deep top list of rows for its query plus the best score it dropped.
-//   merge:  per query, pool the workgroup lists, keep the k best, certify against the dropped
+// Layout (built on the device at create time): postings per term, ascending row, each list
+// closed by a sentinel row; rows cut into one contiguous range per CU.
+//
+// Search, one pass per 64 queries:
+//   wave_terms: the 64 queries are dealt to 16 waves, 4 each (wave w owns queries w, w+16, ...).
+//           Per wave: the ascending union of its queries' terms with a 4-bit query mask and the
+//           4 weights.
+//   scan:   workgroup = one row range, wave = 4 queries, lane = one row of a 64-row tile. For each
+//           tile the wave walks its terms in ascending term order; a term whose next posting is
+//           inside the tile loads 64 postings (lane-reversed), keeps the prefix inside the tile
+//           and ds_permutes each value to the lane of its row, where every owning query adds
+//           fl32(w * v) into its fp32 accumulator. Ascending term order per (row, query) is the
+//           Qdrant summation order; nothing else is reordered. Per-term cursors carry over to
+//           the next tile. Each wave keeps a sorted 16-entry list per query (16 lanes each) plus
+//           the best score it dropped.
+//   merge:  per query, pool the range lists, keep the k best, certify against the dropped
 //           bound (scores are exact, so the bound test is strict: k-th > bound).
-//   fallback for uncertified queries: a second scan collects every row scoring >= the k-th
-//           candidate (a lower bound of the true k-th), then sorts them.
+//   fallback for uncertified queries: the scan rerun in collect mode gathers every row scoring
+//           >= the k-th candidate (a lower bound of the true k-th), then sorts them.
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -26,252 +38,616 @@
 
 namespace {
 
-constexpr int kQB = 64;
-constexpr int kLaneList = 4;
-constexpr int kScanThreads = 1024;  // 16 waves: one workgroup per CU
-constexpr int kWavesPerWG = kScanThreads / 64;
-constexpr int kKW = 16;             // candidates per workgroup and query (of 64 lane entries)
-constexpr int kSelCap = 1024;       // kept entries per query in the merge
+constexpr int kQB = 64;                 // queries per pass
+constexpr int kQW = 4;                  // queries per wave
+constexpr int kWaves = kQB / kQW;       // 16 waves per workgroup
+constexpr int kScanThreads = kWaves * 64;
+constexpr int kKW = 16;                 // candidates per range and query (16 lanes per query)
+constexpr int kSelCap = 1024;           // kept entries per query in the merge
 constexpr int kMaxK = 240;
-constexpr int kCollectCap = 4096;             // rows per query collected by the fallback
-constexpr int kNoSlot = 0x7f7f7f7f;  // byte pattern of the per-pass memset
+constexpr int kCollectCap = 4096;       // rows per query collected by the fallback
+constexpr int kMaxTerms = 256;          // query terms per query (BGE-M3 queries are short)
+constexpr int kWaveTerms = kQW * kMaxTerms;
+constexpr int kLongTerm = 256;          // postings from which a term gets a range-start table
+constexpr int kPad = 64;
+constexpr int kBatch = 4;               // terms whose LDS reads are in flight together
+constexpr int kMaxRanges = 256;
+constexpr int kMaxU = kQB * kMaxTerms;  // distinct terms of one pass, at most
+constexpr int kU = 128;                 // terms per staging segment
+constexpr int kHold = kU / kWaves;      // terms of a segment staged by one wave
+constexpr int kRegSegs = 64 / kHold;    // segments whose cursors stay in registers
+constexpr size_t kScanLds = (size_t)2 * kU * 64 * 4;   // double-buffered staging, 128 KB
+constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + weights, 128 KB
+constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
-constexpr int64_t kNoOrd = std::numeric_limits<int64_t>::max();
 constexpr uint32_t kFlagOverflow = 4u;
+static_assert(kQW * kKW == 64, "one 16-lane list segment per query of the wave");
 
-constexpr int kMaxTerms = 256;  // query terms per query (BGE-M3 queries are short)
+// ------------------------------------------------------------------------- index build
 
-// block per query of the pass: slot_of_term[t] = min pair index (relative to the pass) naming t
-__global__ void term_slots_kernel(const int32_t* __restrict__ q_indptr,
-                                  const int32_t* __restrict__ q_indices, int32_t vocab,
-                                  int32_t* __restrict__ slot_of_term) {
-  const int q = blockIdx.x;
-  const int32_t base = q_indptr[0];
-  const int32_t a = q_indptr[q], e = min(q_indptr[q + 1], a + kMaxTerms);
-  for (int32_t p = a + threadIdx.x; p < e; p += blockDim.x) {
-    const int32_t t = q_indices[p];
-    if (t >= 0 && t < vocab) atomicMin(&slot_of_term[t], p - base);
+__global__ void entry_rows_kernel(const int64_t* __restrict__ indptr, int64_t n_rows,
+                                  int32_t* __restrict__ row_of) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + armi::wave_id();
+  if (r >= n_rows) return;
+  for (int64_t e = indptr[r] + (threadIdx.x & 63); e < indptr[r + 1]; e += 64)
+    row_of[e] = (int32_t)r;
+}
+
+__global__ void count_nonfinite_kernel(const float* __restrict__ values, int64_t nnz,
+                                       unsigned long long* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool b = i < nnz && !isfinite(values[i]);
+  const unsigned long long m = __ballot(b);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
+__global__ void term_keys_kernel(const int32_t* __restrict__ indices, int64_t nnz, int32_t vocab,
+                                 uint32_t* __restrict__ keys, int32_t* __restrict__ ent) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const int32_t t = indices[i];
+  keys[i] = (t >= 0 && t < vocab) ? (uint32_t)t : (uint32_t)vocab;  // invalid ids sort last
+  ent[i] = (int32_t)i;
+}
+
+// term_ptr[t] = (#entries with term < t) + t: one sentinel slot per preceding term.
+__global__ void term_ptr_kernel(const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
+                                int32_t* __restrict__ term_ptr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nnz) return;
+  const int64_t prev = i == 0 ? -1 : (int64_t)skeys[i - 1];
+  const int64_t cur = i == nnz ? (int64_t)vocab : (int64_t)skeys[i];
+  for (int64_t t = prev + 1; t <= cur && t <= vocab; ++t) term_ptr[t] = (int32_t)(i + t);
+}
+
+__global__ void postings_kernel(const uint32_t* __restrict__ skeys, const int32_t* __restrict__ sent,
+                                const int32_t* __restrict__ row_of,
+                                const float* __restrict__ values, int64_t nnz, int32_t vocab,
+                                int32_t* __restrict__ prow, float* __restrict__ pval) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const uint32_t t = skeys[i];
+  if (t >= (uint32_t)vocab) return;
+  const int64_t pos = i + t;
+  const int32_t e = sent[i];
+  prow[pos] = row_of[e];
+  pval[pos] = values[e];
+}
+
+__global__ void sentinels_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
+                                 int64_t n_postings, int32_t* __restrict__ prow,
+                                 float* __restrict__ pval, int32_t* __restrict__ is_long) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < vocab) {
+    const int32_t s = term_ptr[t + 1] - 1;
+    prow[s] = kEndRow;
+    pval[s] = 0.f;
+    is_long[t] = (s - term_ptr[t]) >= kLongTerm ? 1 : 0;
+  } else if (t == vocab) {
+    is_long[t] = 0;
+  }
+  if (t < kPad) {
+    prow[n_postings + t] = kEndRow;
+    pval[n_postings + t] = 0.f;
   }
 }
 
-__global__ void term_weights_kernel(const int32_t* __restrict__ q_indptr,
-                                    const int32_t* __restrict__ q_indices,
-                                    const float* __restrict__ q_values, int32_t vocab,
-                                    const int32_t* __restrict__ slot_of_term,
-                                    float* __restrict__ weights,
-                                    unsigned long long* __restrict__ qmask,
-                                    uint32_t* __restrict__ flags) {
-  const int q = blockIdx.x;
-  const int32_t a = q_indptr[q], b = q_indptr[q + 1];
-  const int32_t e = min(b, a + kMaxTerms);
-  if (threadIdx.x == 0) flags[q] = (b - a > kMaxTerms) ? 8u : 0u;  // 8 = terms dropped
-  for (int32_t p = a + threadIdx.x; p < e; p += blockDim.x) {
-    const int32_t t = q_indices[p];
-    if (t < 0 || t >= vocab) continue;
-    const int s = slot_of_term[t];
-    weights[(size_t)s * kQB + q] = q_values[p];
-    atomicOr(&qmask[s], 1ull << q);
+__global__ void long_of_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
+                               const int32_t* __restrict__ scan, int32_t* __restrict__ long_of) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= vocab) return;
+  long_of[t] = (term_ptr[t + 1] - 1 - term_ptr[t]) >= kLongTerm ? scan[t] : -1;
+}
+
+// start_tab[l][g] = rank (within term t) of t's first posting with row >= g*R: the posting whose
+// (previous row, row] interval holds g*R; the ranges after t's last posting get P_t.
+__global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
+                                 const int32_t* __restrict__ term_ptr,
+                                 const int32_t* __restrict__ long_of,
+                                 const int32_t* __restrict__ prow, int64_t range_rows,
+                                 int n_ranges, int32_t* __restrict__ start_tab) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const uint32_t t = skeys[i];
+  if (t >= (uint32_t)vocab) return;
+  const int32_t l = long_of[t];
+  if (l < 0) return;
+  const int64_t pos = i + t;
+  const int32_t first = term_ptr[t];
+  const int32_t last = term_ptr[t + 1] - 2;
+  const int32_t rel = (int32_t)(pos - first);
+  const int64_t r = prow[pos];
+  const int64_t prev = pos == first ? -1 : (int64_t)prow[pos - 1];
+  int32_t* tab = start_tab + (size_t)l * n_ranges;
+  const int64_t g_lo = (prev + range_rows) / range_rows;  // ceil((prev + 1) / R)
+  const int64_t g_hi = min(r / range_rows, (int64_t)n_ranges - 1);
+  for (int64_t g = g_lo; g <= g_hi; ++g) tab[g] = rel;
+  if (pos == last)
+    for (int64_t g = r / range_rows + 1; g < n_ranges; ++g) tab[g] = rel + 1;
+}
+
+// ------------------------------------------------------------------------- per-pass prep
+
+// One term of a wave's list: pass term index u, owning-query mask, the 4 query weights (0 where
+// the query lacks the term). 32 B: one scalar load.
+struct alignas(32) TermMeta {
+  int32_t u;
+  int32_t m;
+  float w[kQW];
+  int32_t pad[2];
+};
+
+// One block for the pass. Sorts the pass's (term, query) pairs by (term, wave, i) with query
+// q = wave + 16 i, numbers the distinct terms u = 0..nU-1 ascending (uterm[u] = term), and builds
+// per wave the ascending list of its terms: (u, 4-bit query mask, 4 weights).
+// flags[q] = 8 when a query has more than 256 terms (the first 256 are used).
+__global__ __launch_bounds__(1024) void pass_terms_kernel(
+    const int32_t* __restrict__ q_indptr, const int32_t* __restrict__ q_indices,
+    const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
+    int32_t* __restrict__ n_terms, TermMeta* __restrict__ wl, int32_t* __restrict__ wl_count,
+    uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
+  float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
+  __shared__ int32_t off[kQB + 1];
+  __shared__ int32_t part[1024];
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  if (tid < kQB) {
+    int n = 0;
+    if (tid < nq) {
+      const int32_t len = q_indptr[tid + 1] - q_indptr[tid];
+      n = min(len, kMaxTerms);
+      flags[tid] = len > kMaxTerms ? 8u : 0u;
+    }
+    // inclusive scan of the per-query counts within wave 0
+    int x = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    off[tid + 1] = x;
+    if (tid == 0) off[0] = 0;
   }
-}
-
-__device__ __forceinline__ void topm_insert(float x, int32_t id, float (&s)[kLaneList],
-                                            int32_t (&ix)[kLaneList], float& disc) {
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    // (score desc, row asc): rows arrive in ascending order per lane, so strict > keeps ties
-    // in row order
-    const bool c = x > s[j];
-    const float ts = c ? x : s[j];
-    const int32_t ti = c ? id : ix[j];
-    x = c ? s[j] : x;
-    id = c ? ix[j] : id;
-    s[j] = ts;
-    ix[j] = ti;
+  __syncthreads();
+  const int total = off[kQB];
+  const int n2 = armi::pow2_at_least(max(total, 2));
+  for (int e = tid; e < n2; e += 1024) {
+    uint32_t k = 0xffffffffu;
+    float v = 0.f;
+    if (e < total) {
+      int a = 0, n = kQB;  // q = last index with off[q] <= e
+      while (n > 1) {
+        const int h = n >> 1;
+        if (off[a + h] <= e) a += h;
+        n -= h;
+      }
+      const int q = a;
+      const int32_t p = q_indptr[q] + (e - off[q]);
+      const int32_t t = q_indices[p];
+      if (t >= 0 && t < vocab) {
+        k = ((uint32_t)t << 6) | ((uint32_t)(q & 15) << 2) | (uint32_t)(q >> 4);
+        v = q_values[p];
+      }
+    }
+    key[e] = k;
+    val[e] = v;
   }
-  disc = fmaxf(disc, x);
-}
-
-constexpr int kSlots = kQB * kMaxTerms;
-constexpr int kHitBatch = 16;
-
-__device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
-__device__ __forceinline__ int64_t rl_64(int64_t v, int lane) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v & 0xffffffffu), lane);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ float rl_f(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-
-constexpr uint32_t kAbsent = 0xffffffffu;  // weights[slot][q] bit pattern: q lacks the term
-
-// Walks rows [r0, r1) of the CSR as one flat entry stream [indptr[r0], indptr[r1]), lane l of
-// the wave accumulating query l. Per 64-entry block the hit entries (index present in the
-// batch's term table) are compacted into this wave's LDS scratch with one mbcnt-ranked write,
-// then walked with broadcast LDS reads: no per-hit ballot / readlane scalar work. Loads are
-// issued in the order they are consumed (vmcnt retires in issue order): block i's weight loads
-// first, then block i+1's term-slot lookups, then block i+2's index / value loads. Hits are added
-// in ascending entry order = ascending index order within a row (fp32, multiply and add rounded
-// separately, as Qdrant). on_row(row, score, any) runs once per row, in row order.
-template <typename OnRow>
-__device__ __forceinline__ void scan_rows(int64_t r0, int64_t r1, int lane, int32_t vocab,
-                                          const int64_t* __restrict__ indptr,
-                                          const int32_t* __restrict__ indices,
-                                          const float* __restrict__ values,
-                                          const int32_t* __restrict__ slot_of_term,
-                                          const float* __restrict__ weights, int* lds_slot,
-                                          float* lds_val, int* lds_pos, OnRow&& on_row) {
-  if (r0 >= r1) return;
-  const int64_t p_begin = indptr[r0];
-  const int64_t p_end = indptr[r1];
-  int64_t r = r0;
-  int64_t win = r0;
-  int64_t ends = (win + lane < r1) ? indptr[win + lane + 1] : p_end;
-  int64_t e_cur = rl_64(ends, 0);
-  float acc = 0.0f;
-  bool any = false;
-  auto next_row = [&]() {
-    on_row(r, acc, any);
-    acc = 0.0f;
-    any = false;
-    ++r;
-    if (r < r1) {
-      if (r - win >= 64) {
-        win = r;
-        ends = (win + lane < r1) ? indptr[win + lane + 1] : p_end;
-      }
-      e_cur = rl_64(ends, (int)(r - win));
-    }
-  };
-  auto load_block = [&](int64_t p0, int32_t& t, float& v) {
-    const int64_t j = p0 + lane;
-    t = -1;
-    v = 0.f;
-    if (j < p_end) {
-      t = indices[j];
-      v = values[j];
-    }
-  };
-  auto lookup = [&](int32_t t) -> int {
-    int sl = -1;
-    if (t >= 0 && t < vocab) sl = slot_of_term[t];
-    return (sl >= 0 && sl < kSlots) ? sl : -1;
-  };
-  int32_t tb, tc;
-  float va, vb, vc;
-  load_block(p_begin, tb, va);
-  int sa = lookup(tb);
-  load_block(p_begin + 64, tb, vb);
-  for (int64_t p0 = p_begin; p0 < p_end; p0 += 64) {
-    const unsigned long long m = __ballot(sa >= 0);
-    const int nh = __popcll(m);
-    if (sa >= 0) {
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      lds_slot[rank] = sa;
-      lds_val[rank] = va;
-      lds_pos[rank] = lane;
-    }
-    int sb = -1;
-    bool prefetched = false;
-    for (int h0 = 0; h0 < nh; h0 += kHitBatch) {
-      float hw[kHitBatch];
-#pragma unroll
-      for (int u = 0; u < kHitBatch; ++u) {
-        hw[u] = __uint_as_float(kAbsent);
-        if (h0 + u < nh) hw[u] = weights[lds_slot[h0 + u] * kQB + lane];
-      }
-      if (!prefetched) {
-        sb = lookup(tb);
-        load_block(p0 + 128, tc, vc);
-        prefetched = true;
-      }
-#pragma unroll
-      for (int u = 0; u < kHitBatch; ++u) {
-        if (h0 + u < nh) {
-          const int64_t pos = p0 + __builtin_amdgcn_readfirstlane(lds_pos[h0 + u]);
-          while (pos >= e_cur) next_row();
-          if (__float_as_uint(hw[u]) != kAbsent) {
-            acc = __fadd_rn(acc, __fmul_rn(hw[u], lds_val[h0 + u]));
-            any = true;
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int e = tid; e < n2; e += 1024) {
+        const int o = e ^ stride;
+        if (o > e) {
+          const bool up = (e & size) == 0;
+          const uint32_t x = key[e], y = key[o];
+          if ((x > y) == up) {
+            key[e] = y;
+            key[o] = x;
+            const float tv = val[e];
+            val[e] = val[o];
+            val[o] = tv;
           }
         }
       }
     }
-    if (!prefetched) {
-      sb = lookup(tb);
-      load_block(p0 + 128, tc, vc);
-    }
-    sa = sb;
-    va = vb;
-    tb = tc;
-    vb = vc;
   }
-  while (r < r1) next_row();
+  __syncthreads();
+  // u = rank of the distinct term: per-thread head counts over consecutive slots, then a scan
+  const int per = (n2 + 1023) / 1024;
+  const int e0 = tid * per, e1 = min(n2, e0 + per);
+  int heads = 0;
+  for (int e = e0; e < e1; ++e)
+    heads += (key[e] != 0xffffffffu && (e == 0 || (key[e] >> 6) != (key[e - 1] >> 6))) ? 1 : 0;
+  part[tid] = heads;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int x = tid >= d ? part[tid - d] : 0;
+    __syncthreads();
+    part[tid] += x;
+    __syncthreads();
+  }
+  int u = part[tid] - heads - 1;
+  uint32_t rek[16];  // per <= 16 (n2 <= 16384)
+  for (int e = e0; e < e1; ++e) {
+    const uint32_t k = key[e];
+    if (k != 0xffffffffu && (e == 0 || (k >> 6) != (key[e - 1] >> 6))) {
+      ++u;
+      uterm[u] = (int32_t)(k >> 6);
+    }
+    rek[e - e0] = k == 0xffffffffu ? k : (((uint32_t)u << 6) | (k & 63u));
+  }
+  if (tid == 1023) *n_terms = part[1023];
+  __syncthreads();
+  for (int e = e0; e < e1; ++e) key[e] = rek[e - e0];  // term id -> u (same order)
+  __syncthreads();
+  // wave w of this block writes list w: one entry per (u, w) group (at most 4 queries each)
+  int run = 0;
+  for (int c0 = 0; c0 < n2; c0 += 64) {
+    const int e = c0 + lane;
+    const uint32_t k = key[e];
+    const bool mine = k != 0xffffffffu && (int)((k >> 2) & 15u) == wave;
+    const bool head = mine && (e == 0 || (key[e - 1] >> 2) != (k >> 2));
+    const unsigned long long hb = __ballot(head);
+    if (head) {
+      const int idx = run + __popcll(hb & ((1ull << lane) - 1ull));
+      int m = 0;
+      float w4[kQW] = {0.f, 0.f, 0.f, 0.f};
+      for (int x = e; x < n2 && x < e + kQW; ++x) {
+        const uint32_t kx = key[x];
+        if (kx == 0xffffffffu || (kx >> 2) != (k >> 2)) break;
+        m |= 1 << (kx & 3u);
+        w4[kx & 3u] = val[x];
+      }
+      TermMeta tm;
+      tm.u = (int32_t)(k >> 6);
+      tm.m = m;
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) tm.w[i] = w4[i];
+      tm.pad[0] = tm.pad[1] = 0;
+      wl[wave * kWaveTerms + idx] = tm;
+    }
+    run += __popcll(hb);
+  }
+  if (lane == 0) wl_count[wave] = run;
 }
 
-__global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, const uint64_t* __restrict__ row_mask, int64_t n_rows,
-    int64_t rows_per_wg, int nq, int32_t vocab, const int32_t* __restrict__ slot_of_term,
-    const float* __restrict__ weights, const unsigned long long* __restrict__ qmask,
-    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
-  __shared__ float lkey[kQB][kWavesPerWG * kLaneList];
-  __shared__ int32_t lrow[kQB][kWavesPerWG * kLaneList];
-  __shared__ float ldisc[kQB][kWavesPerWG];
-  __shared__ int hslot[kWavesPerWG][64];
-  __shared__ float hval[kWavesPerWG][64];
-  __shared__ int hpos[kWavesPerWG][64];
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int64_t lo = (int64_t)blockIdx.x * rows_per_wg;
-  const int64_t hi = min(lo + rows_per_wg, n_rows);
-  // contiguous rows per wave keep each wave's CSR stream sequential
-  const int64_t span = hi > lo ? hi - lo : 0;
-  const int64_t r0 = lo + span * wave / kWavesPerWG;
-  const int64_t r1 = lo + span * (wave + 1) / kWavesPerWG;
-  float s[kLaneList];
-  int32_t ix[kLaneList];
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    s[j] = kNegInf;
-    ix[j] = 0x7fffffff;
-  }
-  float disc = kNegInf;
-  scan_rows(r0, r1, lane, vocab, indptr, indices, values, slot_of_term, weights, hslot[wave],
-            hval[wave], hpos[wave], [&](int64_t row, float sc, bool hit) {
-              if (row_mask && !((row_mask[row >> 6] >> (row & 63)) & 1ull)) return;
-              if (__any(hit && sc > s[kLaneList - 1])) {
-                if (hit) topm_insert(sc, (int32_t)row, s, ix, disc);
-              } else if (hit) {
-                disc = fmaxf(disc, sc);
-              }
-            });
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    lkey[lane][wave * kLaneList + j] = s[j];
-    lrow[lane][wave * kLaneList + j] = ix[j];
-  }
-  ldisc[lane][wave] = disc;
-  __syncthreads();
-  // each wave merges 4 queries: 64 lane entries -> the best kKW, plus the bound
-  for (int qq = 0; qq < kQB / kWavesPerWG; ++qq) {
-    const int q = wave * (kQB / kWavesPerWG) + qq;
-    if (q >= nq) break;
-    float key = lkey[q][lane];
-    int32_t row = lrow[q][lane];
-    armi::wave_sort_approx_desc(key, row);
-    const size_t base = (size_t)blockIdx.x * kQB + q;
-    if (lane < kKW) {
-      cand_key[base * kKW + lane] = key;
-      cand_row[base * kKW + lane] = row;
+// ------------------------------------------------------------------------- scan
+
+__device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 8];  // debug phase timers
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float rl_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// first posting of term t at or after row `lo` (range g), with its row
+__device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n_ranges,
+                                             const int32_t* __restrict__ term_ptr,
+                                             const int32_t* __restrict__ long_of,
+                                             const int32_t* __restrict__ start_tab,
+                                             const int32_t* __restrict__ prow) {
+  const int32_t b = term_ptr[t];
+  const int32_t l = long_of[t];
+  int32_t c;
+  if (l >= 0) {
+    c = b + start_tab[(size_t)l * n_ranges + g];
+  } else {
+    int32_t a = b, n = term_ptr[t + 1] - 1 - b;
+    while (n > 0) {
+      const int32_t h = n >> 1;
+      if (prow[a + h] < lo) {
+        a += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
     }
-    float b = (lane < kWavesPerWG) ? ldisc[q][lane] : kNegInf;
-    if (lane == kKW) b = fmaxf(b, key);
+    c = a;
+  }
+  return make_int2(c, prow[c]);
+}
+
+// Workgroup = one row range; steps = (64-row tile, segment of 256 pass terms). Staging: term
+// u_local of the segment is held by wave u_local & 15 (lane slot u_local >> 4), which keeps its
+// cursor, loads the term's next 64 postings (lane-reversed: posting c+p in lane 63-p), keeps the
+// prefix inside the tile and scatters ~bits(value) to buf[u_local][row - tile start] in LDS
+// (0 = no posting). Compute: wave w walks its own queries' terms of the segment in ascending u,
+// reads buf[u_local][lane] and adds fl32(w * v) into the fp32 accumulator of each owning query
+// (lane = row). Staging of step s+1 is issued before, and written after, the compute of step s
+// (double-buffered LDS, one barrier per step). kCollect = false: per-range candidate lists;
+// kCollect = true: every row scoring >= thr.
+template <bool kCollect>
+__global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
+    const int32_t* __restrict__ term_ptr, const int32_t* __restrict__ prow,
+    const float* __restrict__ pval, const int32_t* __restrict__ long_of,
+    const int32_t* __restrict__ start_tab, int64_t n_rows, int64_t range_rows, int n_ranges,
+    const uint64_t* __restrict__ row_mask, int nq, const int32_t* __restrict__ uterm,
+    const int32_t* __restrict__ n_terms, const TermMeta* __restrict__ wl,
+    const int32_t* __restrict__ wl_count, int2* __restrict__ cursors,
+    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
+    const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
+    int32_t* __restrict__ coll_row, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][64]
+  const int g = blockIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = threadIdx.x & 63;
+  const bool has_q = wave < nq;
+  float tq[kQW];
+  if constexpr (kCollect) {
+    bool any = false;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
-    if (lane == 0) cand_bound[base] = b;
+    for (int i = 0; i < kQW; ++i) {
+      const int q = wave + kWaves * i;
+      tq[i] = q < nq ? thr[q] : std::numeric_limits<float>::infinity();
+      any |= tq[i] != std::numeric_limits<float>::infinity();
+    }
+    if (!__syncthreads_or(any)) return;  // workgroup-uniform
+  }
+  const int nU = *n_terms;
+  const int nSeg = (nU + kU - 1) / kU;
+  const int64_t lo = (int64_t)g * range_rows;
+  const int64_t hi = min(lo + range_rows, n_rows);
+  const int n_tiles = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+  const int n_w = has_q ? wl_count[wave] : 0;
+  const TermMeta* my = wl + wave * kWaveTerms;
+  int2* gcur = cursors + (size_t)g * kMaxU;
+
+  // cursors of the held terms: segments < kRegSegs in lane 16*seg + slot, the rest in memory
+  int2 creg = make_int2(0, kEndRow);
+  {
+    const int s = lane / kHold, u = s * kU + (lane % kHold) * kWaves + wave;
+    if (s < nSeg && u < nU)
+      creg = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, prow);
+  }
+  for (int s = kRegSegs; s < nSeg; ++s) {
+    const int u = s * kU + lane * kWaves + wave;
+    if (lane < kHold && u < nU)
+      gcur[u] = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, prow);
+  }
+
+  // per lane (= row within the tile) and query: the two best rows seen in this lane, plus the
+  // best score dropped from the lane
+  float l1s[kQW], l2s[kQW], disc[kQW];
+  int32_t l1r[kQW], l2r[kQW];
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    l1s[i] = kNegInf;
+    l2s[i] = kNegInf;
+    disc[i] = kNegInf;
+    l1r[i] = kEndRow;
+    l2r[i] = kEndRow;
+  }
+  f2 acc01 = f2{0.f, 0.f}, acc23 = f2{0.f, 0.f};
+
+  int32_t srow[kHold];
+  float sval[kHold];
+  uint32_t amask = 0, hmask = 0;
+  int2 scv = make_int2(0, kEndRow);
+  auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * 64, hi); };
+  auto issue = [&](int s) {
+    const int tile = s / nSeg, seg = s - tile * nSeg;
+    const int32_t thi = tile_hi(tile);
+    const int base = seg < kRegSegs ? seg * kHold : 0;
+    int2 cv = creg;
+    const int l = lane - base;
+    const int u = seg * kU + l * kWaves + wave;
+    const bool mine = l >= 0 && l < kHold && u < nU;
+    if (seg >= kRegSegs) cv = mine ? gcur[u] : make_int2(0, kEndRow);
+    hmask = (uint32_t)(__ballot(mine) >> base) & ((1u << kHold) - 1u);
+    amask = (uint32_t)(__ballot(mine && cv.y < thi) >> base) & ((1u << kHold) - 1u);
+    if (dbg & 2) amask = 0;
+    scv = cv;
+#pragma unroll
+    for (int k = 0; k < kHold; ++k) {
+      if ((amask >> k) & 1u) {
+        const int c = rl_i(cv.x, base + k);
+        srow[k] = prow[c + 63 - lane];
+        sval[k] = pval[c + 63 - lane];
+      }
+    }
+  };
+  auto finish = [&](int s) {
+    const int tile = s / nSeg, seg = s - tile * nSeg;
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * 64);
+    const int32_t thi = tile_hi(tile);
+    const int base = seg < kRegSegs ? seg * kHold : 0;
+    uint32_t* buf = sbuf + (size_t)(s & 1) * kU * 64;
+#pragma unroll
+    for (int k = 0; k < kHold; ++k) {
+      if ((amask >> k) & 1u) {
+        const unsigned long long outb = ~__ballot(srow[k] < thi);
+        const int n_in = outb == 0 ? 64 : __builtin_clzll(outb);  // postings inside the tile
+        const int32_t nr = n_in < 64 ? rl_i(srow[k], 63 - n_in) : thi;
+        if (lane == base + k) {
+          scv.x += n_in;
+          scv.y = nr;
+        }
+        uint32_t* row = buf + (k * kWaves + wave) * 64;
+        row[lane] = 0u;
+        const uint32_t vb = __float_as_uint(sval[k]);
+        if (lane >= 64 - n_in) row[srow[k] - tlo] = vb == 0u ? 0x80000000u : vb;
+      } else if ((hmask >> k) & 1u) {
+        buf[(k * kWaves + wave) * 64 + lane] = 0u;  // held but idle this step: an all-miss row
+      }
+    }
+    if (seg < kRegSegs) {
+      creg = scv;
+    } else {
+      const int u = seg * kU + lane * kWaves + wave;
+      if (lane < kHold && u < nU) gcur[u] = scv;
+    }
+  };
+  // seg_first (lane s): first list index whose term lies in segment s or later
+  int seg_first = n_w;
+  if (lane <= nSeg) {
+    int a0 = 0, n = n_w;
+    while (n > 0) {
+      const int h = n >> 1;
+      if (my[a0 + h].u < lane * kU) {
+        a0 += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
+    }
+    seg_first = a0;
+  }
+  // per query: 64-bit mask of tile rows hit by at least one of its terms
+  unsigned long long hbm[kQW] = {0ull, 0ull, 0ull, 0ull};
+  auto compute = [&](int s) {
+    const int tile = s / nSeg, seg = s - tile * nSeg;
+    (void)tile;
+    const uint32_t* buf = sbuf + (size_t)(s & 1) * kU * 64 + lane;
+    const int ubase = seg * kU;
+    const int j0 = rl_i(seg_first, seg);
+    const int j1 = seg + 1 < 64 ? rl_i(seg_first, seg + 1) : n_w;
+    for (int j = j0; j < j1; j += kBatch) {
+      TermMeta tm[kBatch];
+      uint32_t rv[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k)
+        if (j + k < j1) tm[k] = my[j + k];  // uniform: scalar loads
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k)
+        if (j + k < j1) rv[k] = buf[(tm[k].u - ubase) * 64];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        if (j + k < j1) {
+          // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting;
+          // adding fl32(w * +-0) leaves an fp32 sum unchanged, so a miss is a no-op
+          const unsigned long long hit = __ballot(rv[k] != 0u);
+          const float v = __uint_as_float(rv[k]);
+          const int m = tm[k].m;
+          if (m & 1) hbm[0] |= hit;
+          if (m & 2) hbm[1] |= hit;
+          if (m & 4) hbm[2] |= hit;
+          if (m & 8) hbm[3] |= hit;
+          const f2 vv = f2{v, v};
+          if (m & 3) acc01 = acc01 + f2{tm[k].w[0], tm[k].w[1]} * vv;
+          if (m & 12) acc23 = acc23 + f2{tm[k].w[2], tm[k].w[3]} * vv;
+        }
+      }
+    }
+  };
+  auto candidates = [&](int tile, uint64_t mrow) {
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * 64);
+    const int32_t thi = tile_hi(tile);
+    const bool ok = ((mrow >> lane) & 1ull) && (tlo + lane < thi);
+#pragma unroll
+    for (int i = 0; i < kQW; ++i) {
+      const bool cand = ok && ((hbm[i] >> lane) & 1ull);
+      const float sc = i == 0 ? acc01.x : i == 1 ? acc01.y : i == 2 ? acc23.x : acc23.y;
+      if constexpr (kCollect) {
+        const int q = wave + kWaves * i;
+        if (cand && sc >= tq[i]) {
+          const int slot = atomicAdd(&coll_count[q], 1);
+          if (slot < kCollectCap) {
+            coll_key[(size_t)q * kCollectCap + slot] = sc;
+            coll_row[(size_t)q * kCollectCap + slot] = tlo + lane;
+          }
+        }
+      } else {
+        // rows reach a lane in ascending order, so strict > keeps equal keys in row order
+        const float x = cand ? sc : kNegInf;
+        const int32_t r = tlo + lane;
+        const bool c1 = x > l1s[i];
+        const bool c2 = x > l2s[i];
+        disc[i] = fmaxf(disc[i], c2 ? l2s[i] : x);
+        l2s[i] = c1 ? l1s[i] : (c2 ? x : l2s[i]);
+        l2r[i] = c1 ? l1r[i] : (c2 ? r : l2r[i]);
+        l1s[i] = c1 ? x : l1s[i];
+        l1r[i] = c1 ? r : l1r[i];
+      }
+    }
+  };
+
+  const int S = n_tiles * nSeg;
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t_a = wall_clock64();
+  if (S > 0) {
+    issue(0);
+    finish(0);
+  }
+  __syncthreads();
+  unsigned long long t_b = wall_clock64();
+  tp[5] += t_b - t_a;
+  for (int s = 0; s < S; ++s) {
+    const int tile = s / nSeg, seg = s - tile * nSeg;
+    // loaded now, used after this step's compute
+    const uint64_t mrow = (row_mask && seg == nSeg - 1) ? row_mask[(lo >> 6) + tile] : ~0ull;
+    t_a = wall_clock64();
+    if (s + 1 < S) issue(s + 1);
+    t_b = wall_clock64();
+    tp[0] += t_b - t_a;
+    if (has_q) {
+      if (seg == 0) {
+        acc01 = f2{0.f, 0.f};
+        acc23 = f2{0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < kQW; ++i) hbm[i] = 0ull;
+      }
+      if (!(dbg & 1)) compute(s);
+      t_a = wall_clock64();
+      tp[1] += t_a - t_b;
+      if (seg == nSeg - 1) candidates(tile, mrow);
+      t_b = wall_clock64();
+      tp[2] += t_b - t_a;
+    }
+    if (s + 1 < S) finish(s + 1);
+    t_a = wall_clock64();
+    tp[3] += t_a - t_b;
+    if (!(dbg & 4)) __syncthreads();
+    t_b = wall_clock64();
+    tp[4] += t_b - t_a;
+  }
+  if ((dbg & 8) && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) g_sparse_prof[((size_t)g * kWaves + wave) * 8 + i] = tp[i];
+    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 6] = n_w;
+    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 7] = S;
+  }
+  if constexpr (!kCollect) {
+    if (has_q) {
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) {
+        const int q = wave + kWaves * i;
+        // top 16 of the 128 lane entries: sort both list levels, bitonic split of their heads
+        float ka = l1s[i], kb = l2s[i];
+        int32_t ra = l1r[i], rb = l2r[i];
+        armi::wave_sort_approx_desc(ka, ra);
+        armi::wave_sort_approx_desc(kb, rb);
+        const float kbr = __shfl(kb, (15 - lane) & 63);
+        const int32_t rbr = __shfl(rb, (15 - lane) & 63);
+        const float kb16 = __shfl(kb, 16);
+        float ck = kNegInf, lose = kNegInf;
+        int32_t cr = kEndRow;
+        if (lane < 16) {
+          const bool take_a = armi::approx_better(ka, ra, kbr, rbr);
+          ck = take_a ? ka : kbr;
+          cr = take_a ? ra : rbr;
+          lose = take_a ? kbr : ka;
+        } else if (lane == 16) {
+          lose = fmaxf(ka, kb16);
+        }
+        float b = fmaxf(disc[i], lose);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) b = fmaxf(b, __shfl_xor(b, o));
+        armi::wave_sort_approx_desc(ck, cr);
+        if (q < nq) {
+          const size_t base = (size_t)g * kQB + q;
+          if (lane < kKW) {
+            cand_key[base * kKW + lane] = ck;
+            cand_row[base * kKW + lane] = cr;
+          }
+          if (lane == 0) cand_bound[base] = b;
+        }
+      }
+    }
   }
 }
 
@@ -293,7 +669,7 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   const int qg = q_first + ql;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
   float b = kNegInf;
   for (int g = tid; g < 256; g += 256) {
@@ -373,39 +749,6 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   }
 }
 
-// Fallback scan: every row scoring >= thr[q] (and sharing an index) is appended to q's buffer.
-__global__ __launch_bounds__(kScanThreads) void sparse_collect_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, const uint64_t* __restrict__ row_mask, int64_t n_rows,
-    int64_t rows_per_wg, int nq, int32_t vocab, const int32_t* __restrict__ slot_of_term,
-    const float* __restrict__ weights, const unsigned long long* __restrict__ qmask,
-    const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
-    int32_t* __restrict__ coll_row) {
-  __shared__ int hslot[kWavesPerWG][64];
-  __shared__ float hval[kWavesPerWG][64];
-  __shared__ int hpos[kWavesPerWG][64];
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const float t = lane < nq ? thr[lane] : std::numeric_limits<float>::infinity();
-  if (__all(t == std::numeric_limits<float>::infinity())) return;
-  const int64_t lo = (int64_t)blockIdx.x * rows_per_wg;
-  const int64_t hi = min(lo + rows_per_wg, n_rows);
-  const int64_t span = hi > lo ? hi - lo : 0;
-  const int64_t r0 = lo + span * wave / kWavesPerWG;
-  const int64_t r1 = lo + span * (wave + 1) / kWavesPerWG;
-  scan_rows(r0, r1, lane, vocab, indptr, indices, values, slot_of_term, weights, hslot[wave],
-            hval[wave], hpos[wave], [&](int64_t row, float sc, bool hit) {
-              if (row_mask && !((row_mask[row >> 6] >> (row & 63)) & 1ull)) return;
-              if (hit && sc >= t) {
-                const int slot = atomicAdd(&coll_count[lane], 1);
-                if (slot < kCollectCap) {
-                  coll_key[(size_t)lane * kCollectCap + slot] = sc;
-                  coll_row[(size_t)lane * kCollectCap + slot] = (int32_t)row;
-                }
-              }
-            });
-}
-
 __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
     const int* __restrict__ coll_count, const float* __restrict__ coll_key,
     const int32_t* __restrict__ coll_row, int q_first, int k, int64_t ordinal_base,
@@ -437,28 +780,12 @@ __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
   }
 }
 
-struct Plan {
-  int n_wg;
-  int64_t rows_per_wg;
-  int pool2;
-};
-
-Plan plan(const armi_sparse_index* idx) {
-  Plan p;
-  const int64_t want = std::max<int64_t>(1, std::min<int64_t>(std::min(idx->num_cus, 256),
-                                                              (idx->n_rows + 63) / 64));
-  p.rows_per_wg = (idx->n_rows + want - 1) / want;
-  if (p.rows_per_wg == 0) p.rows_per_wg = 1;
-  p.n_wg = (int)((idx->n_rows + p.rows_per_wg - 1) / p.rows_per_wg);
-  if (p.n_wg == 0) p.n_wg = 1;
-  p.pool2 = 0;
-  return p;
-}
-
 struct Workspace {
-  int32_t* slot_of_term;
-  float* weights;
-  unsigned long long* qmask;
+  int32_t* uterm;
+  int32_t* n_terms;
+  TermMeta* wl;
+  int32_t* wl_count;
+  int2* cursors;
   float* cand_key;
   int32_t* cand_row;
   float* cand_bound;
@@ -472,19 +799,128 @@ struct Workspace {
 Workspace carve(void* base, const armi_sparse_index* idx) {
   armi::Carver cv(base);
   Workspace w{};
-  const Plan p = plan(idx);
-  w.slot_of_term = cv.take<int32_t>((size_t)idx->vocab);
-  w.weights = cv.take<float>((size_t)kQB * kMaxTerms * kQB);
-  w.qmask = cv.take<unsigned long long>((size_t)kQB * kMaxTerms);
-  w.cand_key = cv.take<float>((size_t)p.n_wg * kQB * kKW);
-  w.cand_row = cv.take<int32_t>((size_t)p.n_wg * kQB * kKW);
-  w.cand_bound = cv.take<float>((size_t)p.n_wg * kQB);
+  const size_t nr = (size_t)std::max(idx->n_ranges, 1);
+  w.uterm = cv.take<int32_t>(kMaxU);
+  w.n_terms = cv.take<int32_t>(1);
+  w.wl = cv.take<TermMeta>((size_t)kWaves * kWaveTerms);
+  w.wl_count = cv.take<int32_t>(kWaves);
+  w.cursors = cv.take<int2>(nr * kMaxU);
+  w.cand_key = cv.take<float>(nr * kQB * kKW);
+  w.cand_row = cv.take<int32_t>(nr * kQB * kKW);
+  w.cand_bound = cv.take<float>(nr * kQB);
   w.kth = cv.take<float>(kQB);
   w.coll_count = cv.take<int>(kQB);
   w.coll_key = cv.take<float>((size_t)kQB * kCollectCap);
   w.coll_row = cv.take<int32_t>((size_t)kQB * kCollectCap);
   w.bytes = cv.off + 256;
   return w;
+}
+
+// Device temporaries of the index build, released on every exit path.
+struct Scratch {
+  std::vector<void*> ptrs;
+  template <typename T>
+  hipError_t alloc(T** p, size_t count) {
+    *p = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+  ~Scratch() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+unsigned grid_for(int64_t n, int block) { return (unsigned)std::max<int64_t>(1, (n + block - 1) / block); }
+
+int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t* indices,
+                   const float* values, hipStream_t stream) {
+  const int64_t nnz = idx->nnz;
+  const int32_t vocab = idx->vocab;
+  Scratch tmp;
+  int32_t *row_of, *ent, *sent, *is_long, *scan;
+  uint32_t *keys, *skeys;
+  ARMI_HIP(tmp.alloc(&row_of, nnz));
+  ARMI_HIP(tmp.alloc(&ent, nnz));
+  ARMI_HIP(tmp.alloc(&sent, nnz));
+  ARMI_HIP(tmp.alloc(&keys, nnz));
+  ARMI_HIP(tmp.alloc(&skeys, nnz));
+  ARMI_HIP(tmp.alloc(&is_long, (size_t)vocab + 1));
+  ARMI_HIP(tmp.alloc(&scan, (size_t)vocab + 1));
+  if (nnz > 0) {
+    unsigned long long* bad;
+    ARMI_HIP(tmp.alloc(&bad, 1));
+    ARMI_HIP(hipMemsetAsync(bad, 0, 8, stream));
+    count_nonfinite_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(values, nnz, bad);
+    ARMI_LAUNCHED("count_nonfinite_kernel");
+    unsigned long long n_bad = 0;
+    ARMI_HIP(hipMemcpyAsync(&n_bad, bad, 8, hipMemcpyDeviceToHost, stream));
+    ARMI_HIP(hipStreamSynchronize(stream));
+    ARMI_REQUIRE(n_bad == 0, "armi_sparse_index_create: values must be finite");
+    entry_rows_kernel<<<grid_for(idx->n_rows, 4), 256, 0, stream>>>(indptr, idx->n_rows, row_of);
+    ARMI_LAUNCHED("entry_rows_kernel");
+    term_keys_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(indices, nnz, vocab, keys, ent);
+    ARMI_LAUNCHED("term_keys_kernel");
+    int end_bit = 1;
+    while (end_bit < 32 && (uint64_t(1) << end_bit) <= (uint64_t)vocab) ++end_bit;
+    size_t sort_bytes = 0;
+    ARMI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, keys, skeys, ent, sent,
+                                                (int)nnz, 0, end_bit, stream));
+    unsigned char* sort_tmp;
+    ARMI_HIP(tmp.alloc(&sort_tmp, sort_bytes));
+    ARMI_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp, sort_bytes, keys, skeys, ent, sent,
+                                                (int)nnz, 0, end_bit, stream));
+  }
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->term_ptr), ((size_t)vocab + 1) * 4));
+  term_ptr_kernel<<<grid_for(nnz + 1, 256), 256, 0, stream>>>(skeys, nnz, vocab, idx->term_ptr);
+  ARMI_LAUNCHED("term_ptr_kernel");
+  int32_t n_post = 0;
+  ARMI_HIP(hipMemcpyAsync(&n_post, idx->term_ptr + vocab, 4, hipMemcpyDeviceToHost, stream));
+  ARMI_HIP(hipStreamSynchronize(stream));
+  idx->n_postings = n_post;
+  const size_t cap = (size_t)n_post + kPad;
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->prow), cap * 4));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->pval), cap * 4));
+  if (nnz > 0) {
+    postings_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(skeys, sent, row_of, values, nnz, vocab,
+                                                            idx->prow, idx->pval);
+    ARMI_LAUNCHED("postings_kernel");
+  }
+  sentinels_kernel<<<grid_for(std::max<int64_t>((int64_t)vocab + 1, kPad), 256), 256, 0, stream>>>(
+      idx->term_ptr, vocab, idx->n_postings, idx->prow, idx->pval, is_long);
+  ARMI_LAUNCHED("sentinels_kernel");
+  size_t scan_bytes = 0;
+  ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, is_long, scan, vocab + 1, stream));
+  unsigned char* scan_tmp;
+  ARMI_HIP(tmp.alloc(&scan_tmp, scan_bytes));
+  ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, is_long, scan, vocab + 1, stream));
+  int32_t n_long = 0;
+  ARMI_HIP(hipMemcpyAsync(&n_long, scan + vocab, 4, hipMemcpyDeviceToHost, stream));
+  ARMI_HIP(hipStreamSynchronize(stream));
+  idx->n_long = n_long;
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->long_of), std::max<size_t>(vocab, 1) * 4));
+  long_of_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(idx->term_ptr, vocab, scan, idx->long_of);
+  ARMI_LAUNCHED("long_of_kernel");
+  const size_t tab = std::max<size_t>((size_t)n_long * std::max(idx->n_ranges, 1), 1);
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->start_tab), tab * 4));
+  if (nnz > 0 && n_long > 0 && idx->n_ranges > 0) {
+    start_tab_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(skeys, nnz, vocab, idx->term_ptr,
+                                                             idx->long_of, idx->prow,
+                                                             idx->range_rows, idx->n_ranges,
+                                                             idx->start_tab);
+    ARMI_LAUNCHED("start_tab_kernel");
+  }
+  ARMI_HIP(hipStreamSynchronize(stream));
+  return ARMI_OK;
+}
+
+void free_index(armi_sparse_index* idx) {
+  (void)hipFree(idx->term_ptr);
+  (void)hipFree(idx->prow);
+  (void)hipFree(idx->pval);
+  (void)hipFree(idx->long_of);
+  (void)hipFree(idx->start_tab);
+  delete idx;
 }
 
 }  // namespace
@@ -494,11 +930,13 @@ extern "C" {
 int armi_sparse_index_create(int device, const int64_t* indptr, const int32_t* indices,
                              const float* values, int64_t n_rows, int64_t nnz, int32_t vocab,
                              int64_t ordinal_base, armi_sparse_index** out, hipStream_t stream) {
-  (void)stream;
   ARMI_REQUIRE(out != nullptr, "armi_sparse_index_create: out is null");
   *out = nullptr;
-  ARMI_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31), "armi_sparse_index_create: bad n_rows");
-  ARMI_REQUIRE(vocab >= 1, "armi_sparse_index_create: vocab must be >= 1");
+  ARMI_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31) - 64,
+               "armi_sparse_index_create: bad n_rows");
+  ARMI_REQUIRE(vocab >= 1 && vocab < (1 << 26), "armi_sparse_index_create: vocab must be in [1, 2^26)");
+  ARMI_REQUIRE(nnz >= 0 && nnz + (int64_t)vocab + kPad < (int64_t(1) << 31),
+               "armi_sparse_index_create: nnz + vocab must stay below 2^31");
   ARMI_REQUIRE(indptr != nullptr || n_rows == 0, "armi_sparse_index_create: indptr is null");
   ARMI_REQUIRE((indices && values) || nnz == 0, "armi_sparse_index_create: null CSR arrays");
   ARMI_HIP(hipSetDevice(device));
@@ -511,15 +949,29 @@ int armi_sparse_index_create(int device, const int64_t* indptr, const int32_t* i
   idx->vocab = vocab;
   idx->ordinal_base = ordinal_base;
   idx->num_cus = prop.multiProcessorCount;
-  idx->indptr = indptr;
-  idx->indices = indices;
-  idx->values = values;
+  if (n_rows > 0) {
+    const int64_t want = std::max<int64_t>(
+        1, std::min<int64_t>(std::min(idx->num_cus, kMaxRanges), (n_rows + 63) / 64));
+    idx->range_rows = ((n_rows + want - 1) / want + 63) / 64 * 64;
+    idx->n_ranges = (int)((n_rows + idx->range_rows - 1) / idx->range_rows);
+  } else {
+    idx->range_rows = 64;
+    idx->n_ranges = 0;
+  }
+  const int rc = build_inverted(idx, indptr, indices, values, stream);
+  if (rc != ARMI_OK) {
+    free_index(idx);
+    return rc;
+  }
   *out = idx;
   return ARMI_OK;
 }
 
 int armi_sparse_index_destroy(armi_sparse_index* index) {
-  delete index;
+  if (index) {
+    (void)hipSetDevice(index->device);
+    free_index(index);
+  }
   return ARMI_OK;
 }
 
@@ -544,10 +996,16 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
                "armi_sparse_topk: workspace too small");
   ARMI_HIP(hipSetDevice(idx->device));
   const Workspace w = carve(workspace, idx);
-  const Plan p = plan(idx);
+  static const int dbg = getenv("ARMI_SPARSE_DBG") ? atoi(getenv("ARMI_SPARSE_DBG")) : 0;
   const size_t lds_collect = (size_t)kCollectCap * 8;
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect));
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepLds));
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds));
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds));
   for (int q0 = 0; q0 < n_queries; q0 += kQB) {
     const int nqp = std::min(kQB, n_queries - q0);
     uint32_t* pflags = out_flags + q0;
@@ -557,29 +1015,44 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       ARMI_HIP(hipMemsetAsync(out_ids + (size_t)q0 * k, 0xff, sizeof(int64_t) * nqp * k, stream));
       continue;
     }
-    ARMI_HIP(hipMemsetAsync(w.slot_of_term, 0x7f, sizeof(int32_t) * idx->vocab, stream));
-    ARMI_HIP(hipMemsetAsync(w.qmask, 0, sizeof(unsigned long long) * kQB * kMaxTerms, stream));
-    ARMI_HIP(hipMemsetAsync(w.weights, 0xff, sizeof(float) * kQB * kMaxTerms * kQB, stream));
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
-    term_slots_kernel<<<dim3(nqp), dim3(64), 0, stream>>>(q_indptr + q0, q_indices, idx->vocab,
-                                                          w.slot_of_term);
-    ARMI_LAUNCHED("term_slots_kernel");
-    term_weights_kernel<<<dim3(nqp), dim3(64), 0, stream>>>(q_indptr + q0, q_indices, q_values,
-                                                            idx->vocab, w.slot_of_term,
-                                                            w.weights, w.qmask, pflags);
-    ARMI_LAUNCHED("term_weights_kernel");
-    sparse_scan_kernel<<<dim3(p.n_wg), dim3(kScanThreads), 0, stream>>>(
-        idx->indptr, idx->indices, idx->values, row_mask, idx->n_rows, p.rows_per_wg, nqp,
-        idx->vocab, w.slot_of_term, w.weights, w.qmask, w.cand_key, w.cand_row, w.cand_bound);
+    pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
+        q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.wl,
+        w.wl_count, pflags);
+    ARMI_LAUNCHED("pass_terms_kernel");
+    sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
+        idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count,
+        w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
+    if (dbg & 8) {
+      std::vector<unsigned long long> h((size_t)kMaxRanges * kWaves * 8);
+      ARMI_HIP(hipStreamSynchronize(stream));
+      ARMI_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_sparse_prof), h.size() * 8));
+      double sum[8] = {0}, mx[8] = {0};
+      int cnt = 0;
+      for (int g = 0; g < idx->n_ranges; ++g)
+        for (int wv = 0; wv < kWaves; ++wv) {
+          ++cnt;
+          for (int i = 0; i < 8; ++i) {
+            sum[i] += (double)h[((size_t)g * kWaves + wv) * 8 + i];
+            mx[i] = std::max(mx[i], (double)h[((size_t)g * kWaves + wv) * 8 + i]);
+          }
+        }
+      fprintf(stderr, "sparse prof (us, 100MHz clock) avg/max: issue %.1f/%.1f compute %.1f/%.1f "
+              "cand %.1f/%.1f finish %.1f/%.1f barrier %.1f/%.1f prologue %.1f/%.1f n_w %.1f/%.0f S %.0f\n",
+              sum[0] / cnt / 100, mx[0] / 100, sum[1] / cnt / 100, mx[1] / 100, sum[2] / cnt / 100,
+              mx[2] / 100, sum[3] / cnt / 100, mx[3] / 100, sum[4] / cnt / 100, mx[4] / 100,
+              sum[5] / cnt / 100, mx[5] / 100, sum[6] / cnt, mx[6], mx[7]);
+    }
     sparse_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
-        w.cand_key, w.cand_row, w.cand_bound, p.n_wg, q0, k, idx->ordinal_base, out_scores,
-        out_ids, out_count, pflags, w.kth);
+        w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, idx->ordinal_base,
+        out_scores, out_ids, out_count, pflags, w.kth);
     ARMI_LAUNCHED("sparse_merge_kernel");
-    sparse_collect_kernel<<<dim3(p.n_wg), dim3(kScanThreads), 0, stream>>>(
-        idx->indptr, idx->indices, idx->values, row_mask, idx->n_rows, p.rows_per_wg, nqp,
-        idx->vocab, w.slot_of_term, w.weights, w.qmask, w.kth, w.coll_count, w.coll_key,
-        w.coll_row);
+    sparse_scan_kernel<true><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
+        idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count,
+        w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp), dim3(256), lds_collect, stream>>>(
         w.coll_count, w.coll_key, w.coll_row, q0, k, idx->ordinal_base, out_scores, out_ids,

@@ -229,6 +229,30 @@ def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
     return TopK(scores=out_score.float(), ids=out_ids, rank=out_score, count=out_count)
 
 
+class ConcurrentHybrid:
+    """The two prefetches of one hybrid search (qdrant.py:281-298) on two HIP streams: the
+    sparse top-k on a side stream overlaps the dense scan and merge on the caller's stream (the
+    two share nothing until the fusion), then RRF runs on the caller's stream."""
+
+    def __init__(self, device: torch.device):
+        self.side = torch.cuda.Stream(device=device)
+
+    def __call__(self, dense_fn, sparse_fn, sparse_inputs, limit: int, rrf_k: int = 2) -> TopK:
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        for t in sparse_inputs:
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            s = sparse_fn()
+        d = dense_fn()
+        main.wait_stream(self.side)
+        for t in (s.scores, s.ids, s.rank, s.count, s.flags):
+            if t is not None:
+                t.record_stream(main)
+        return rrf_fuse(d, s, limit, rrf_k=rrf_k)
+
+
 _hip = None
 
 

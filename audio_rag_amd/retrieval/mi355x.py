@@ -22,7 +22,7 @@ from audio_rag_amd.core.base import (AudioChunk, BaseRetriever, EmbeddingResult,
 from audio_rag_amd.core.exceptions import RetrievalError
 from audio_rag_amd.retrieval.base import RetrievalRegistry
 from audio_rag_amd.retrieval.collection import ChunkCollection
-from audio_rag_amd.retrieval.device import TopK, rrf_fuse
+from audio_rag_amd.retrieval.device import ConcurrentHybrid, TopK
 from audio_rag_amd.utils.decorators import timed
 
 logger = logging.getLogger(__name__)
@@ -74,6 +74,7 @@ class MI355XRetriever(BaseRetriever):
         self.embedding_dim = embedding_dim
         self.device = torch.device("cuda", config.device)
         self._collections: dict[str, ChunkCollection] = {}
+        self._hybrid: ConcurrentHybrid | None = None
         logger.info(f"MI355XRetriever initialized: collection={config.collection_name}, "
                     f"search_type={config.search_type}, device={self.device}")
 
@@ -185,10 +186,14 @@ class MI355XRetriever(BaseRetriever):
         mode = self._mode(coll, search_type, queries.has_sparse)
         mask = coll.filter_mask(filter_metadata)
         if mode == "hybrid":
-            dense = coll.dense_index.topk(queries.dense, 2 * top_k, row_mask=mask)
-            sparse = coll.sparse_index.topk(queries.sparse_indptr, queries.sparse_indices,
-                                            queries.sparse_values, 2 * top_k, row_mask=mask)
-            return rrf_fuse(dense, sparse, top_k, rrf_k=self.config.rrf_k), mode
+            if self._hybrid is None:
+                self._hybrid = ConcurrentHybrid(self.device)
+            sq = (queries.sparse_indptr, queries.sparse_indices, queries.sparse_values)
+            fused = self._hybrid(
+                lambda: coll.dense_index.topk(queries.dense, 2 * top_k, row_mask=mask),
+                lambda: coll.sparse_index.topk(*sq, 2 * top_k, row_mask=mask),
+                sq + ((mask,) if mask is not None else ()), top_k, rrf_k=self.config.rrf_k)
+            return fused, mode
         if mode == "sparse":
             return coll.sparse_index.topk(queries.sparse_indptr, queries.sparse_indices,
                                           queries.sparse_values, top_k, row_mask=mask), mode

@@ -209,7 +209,8 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=dev)
 
     from audio_rag_amd import _armi
-    from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex, TopK, merge_shards, rrf_fuse
+    from audio_rag_amd.retrieval.device import (ConcurrentHybrid, DenseIndex, SparseIndex, TopK,
+                                                merge_shards, rrf_fuse)
     from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
 
     n, dim, batch, k = args.chunks, args.dim, args.batch, args.top_k
@@ -228,6 +229,7 @@ def main() -> None:
         sindex = SparseIndex(*make_sparse_rows(lo, hi - lo, dev), vocab=VOCAB, ordinal_base=lo)
         sws = torch.empty(sindex.workspace_bytes(world * batch, pre_k), dtype=torch.uint8, device=dev)
         q_sparse = [make_sparse_queries(batch, dev, seed=1000 * (1 + rank) + j) for j in range(n_q_batches)]
+        hybrid = ConcurrentHybrid(dev)
     reranker = None
     if wl == "hybrid_rerank":
         from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
@@ -273,9 +275,8 @@ def main() -> None:
         if ql.shape[0] != batch:  # single-query latency probe
             qs = (qs[0][:ql.shape[0] + 1], qs[1], qs[2])
         if sharded is None:
-            d = index.topk(ql, pre_k, workspace=ws)
-            sp = sindex.topk(*qs, pre_k, workspace=sws)
-            fused = rrf_fuse(d, sp, search_k)
+            fused = hybrid(lambda: index.topk(ql, pre_k, workspace=ws),
+                           lambda: sindex.topk(*qs, pre_k, workspace=sws), qs, search_k)
         else:
             fused = sharded.hybrid(ql, qs, search_k)
         if reranker is None:
