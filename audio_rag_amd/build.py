@@ -66,6 +66,10 @@ def build(verbose: bool = False) -> Path:
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, LIB)
+    keep = {o.name for o in objs}
+    for stale in OBJ_DIR.glob("*.o"):  # objects of superseded sources
+        if stale.name not in keep:
+            stale.unlink()
     if verbose:
         print(f"built {LIB}")
     return LIB

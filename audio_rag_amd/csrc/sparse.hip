@@ -168,13 +168,15 @@ __global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz
 
 // ------------------------------------------------------------------------- per-pass prep
 
-// One term of a wave's list: pass term index u, owning-query mask, the 4 query weights (0 where
-// the query lacks the term). 32 B: one scalar load.
+// One term of a wave's list: byte offset of its staging row within a segment buffer
+// ((u % kU) * 256), owning-query mask, the 4 query weights (0 where the query lacks the term),
+// pass term index u. 32 B: one scalar load.
 struct alignas(32) TermMeta {
-  int32_t u;
+  int32_t off;
   int32_t m;
   float w[kQW];
-  int32_t pad[2];
+  int32_t u;
+  int32_t pad;
 };
 
 // One block for the pass. Sorts the pass's (term, query) pairs by (term, wave, i) with query
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
   int run = 0;
   for (int c0 = 0; c0 < n2; c0 += 64) {
     const int e = c0 + lane;
-    const uint32_t k = key[e];
+    const uint32_t k = e < n2 ? key[e] : 0xffffffffu;  // LDS past n2 was never written
     const bool mine = k != 0xffffffffu && (int)((k >> 2) & 15u) == wave;
     const bool head = mine && (e == 0 || (key[e - 1] >> 2) != (k >> 2));
     const unsigned long long hb = __ballot(head);
@@ -303,10 +305,11 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
       }
       TermMeta tm;
       tm.u = (int32_t)(k >> 6);
+      tm.off = (tm.u % kU) * 64 * 4;
       tm.m = m;
 #pragma unroll
       for (int i = 0; i < kQW; ++i) tm.w[i] = w4[i];
-      tm.pad[0] = tm.pad[1] = 0;
+      tm.pad = 0;
       wl[wave * kWaveTerms + idx] = tm;
     }
     run += __popcll(hb);
@@ -497,41 +500,38 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     }
     seg_first = a0;
   }
-  // per query: 64-bit mask of tile rows hit by at least one of its terms
-  unsigned long long hbm[kQW] = {0ull, 0ull, 0ull, 0ull};
+  // bit i: this lane's row got a posting of one of query i's terms in the current tile
+  uint32_t hb = 0;
   auto compute = [&](int s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
     (void)tile;
-    const uint32_t* buf = sbuf + (size_t)(s & 1) * kU * 64 + lane;
-    const int ubase = seg * kU;
+    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)(s & 1) * kU * 64 + lane);
     const int j0 = rl_i(seg_first, seg);
     const int j1 = seg + 1 < 64 ? rl_i(seg_first, seg + 1) : n_w;
-    for (int j = j0; j < j1; j += kBatch) {
+    // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; an
+    // absent query weight is 0 and adding fl32(0 * v) = +-0 leaves an fp32 sum unchanged, so
+    // every term updates all four accumulators without branches
+    auto term = [&](const TermMeta& tm, uint32_t rv) {
+      const float v = __uint_as_float(rv);
+      hb |= rv != 0u ? (uint32_t)tm.m : 0u;
+      const f2 vv = f2{v, v};
+      acc01 = acc01 + f2{tm.w[0], tm.w[1]} * vv;
+      acc23 = acc23 + f2{tm.w[2], tm.w[3]} * vv;
+    };
+    int j = j0;
+    for (; j + kBatch <= j1; j += kBatch) {
       TermMeta tm[kBatch];
       uint32_t rv[kBatch];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k)
-        if (j + k < j1) tm[k] = my[j + k];  // uniform: scalar loads
+      for (int k = 0; k < kBatch; ++k) tm[k] = my[j + k];  // uniform: scalar loads
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k)
-        if (j + k < j1) rv[k] = buf[(tm[k].u - ubase) * 64];
+      for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint32_t*>(buf + tm[k].off);
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        if (j + k < j1) {
-          // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting;
-          // adding fl32(w * +-0) leaves an fp32 sum unchanged, so a miss is a no-op
-          const unsigned long long hit = __ballot(rv[k] != 0u);
-          const float v = __uint_as_float(rv[k]);
-          const int m = tm[k].m;
-          if (m & 1) hbm[0] |= hit;
-          if (m & 2) hbm[1] |= hit;
-          if (m & 4) hbm[2] |= hit;
-          if (m & 8) hbm[3] |= hit;
-          const f2 vv = f2{v, v};
-          if (m & 3) acc01 = acc01 + f2{tm[k].w[0], tm[k].w[1]} * vv;
-          if (m & 12) acc23 = acc23 + f2{tm[k].w[2], tm[k].w[3]} * vv;
-        }
-      }
+      for (int k = 0; k < kBatch; ++k) term(tm[k], rv[k]);
+    }
+    for (; j < j1; ++j) {
+      const TermMeta tm = my[j];
+      term(tm, *reinterpret_cast<const uint32_t*>(buf + tm.off));
     }
   };
   auto candidates = [&](int tile, uint64_t mrow) {
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const bool ok = ((mrow >> lane) & 1ull) && (tlo + lane < thi);
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
-      const bool cand = ok && ((hbm[i] >> lane) & 1ull);
+      const bool cand = ok && ((hb >> i) & 1u);
       const float sc = i == 0 ? acc01.x : i == 1 ? acc01.y : i == 2 ? acc23.x : acc23.y;
       if constexpr (kCollect) {
         const int q = wave + kWaves * i;
@@ -588,8 +588,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       if (seg == 0) {
         acc01 = f2{0.f, 0.f};
         acc23 = f2{0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < kQW; ++i) hbm[i] = 0ull;
+        hb = 0;
       }
       if (!(dbg & 1)) compute(s);
       t_a = wall_clock64();

@@ -7,6 +7,7 @@ memory and the stream. Results stay on the device until the caller materialises 
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -238,6 +239,8 @@ class ConcurrentHybrid:
         self.side = torch.cuda.Stream(device=device)
 
     def __call__(self, dense_fn, sparse_fn, sparse_inputs, limit: int, rrf_k: int = 2) -> TopK:
+        if os.environ.get("ARMI_HYBRID_SERIAL"):
+            return rrf_fuse(dense_fn(), sparse_fn(), limit, rrf_k=rrf_k)
         main = torch.cuda.current_stream()
         self.side.wait_stream(main)
         for t in sparse_inputs:

@@ -121,3 +121,35 @@ def test_sparse_empty_rows_and_long_rows(gpu, oracle_mod):
         got = _run(idx, q, k, gpu)
         _same(got, oracle_mod.sparse_topk(*csr, *q, k))
         assert not np.isin(got["ids"], np.nonzero(~keep)[0]).any()
+
+
+def test_sparse_golden_corpus_repeatable(gpu, oracle_mod):
+    """The golden scenario's lexical corpus (300 chunks over a 600-id vocabulary slice: every
+    posting list is short, so every cursor comes from the in-list search), single queries and
+    batches, with and without metadata filters, each search run three times."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+    import replay
+    import scenario
+
+    s = scenario.build()
+    csr = replay.corpus_csr(s, True)
+    idx = _sparse_index(csr, gpu)
+    nq = len(s["qlex"])
+    parts = [replay.query_csr(s, q) for q in range(nq)]
+    qi = np.zeros(nq + 1, np.int32)
+    np.cumsum([len(p[1]) for p in parts], out=qi[1:])
+    batch = (qi, np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]))
+    masks = [None] + [replay.filter_mask(s, {"lecture": v}) for v in range(3)]
+    for mask in masks:
+        for k in (10, 20, 40):
+            want = oracle_mod.sparse_topk(*csr, *batch, k, row_mask=mask)
+            for _ in range(3):
+                _same(_run(idx, batch, k, gpu, mask=mask), want)
+            for q in range(0, nq, 7):
+                one = parts[q]
+                want1 = oracle_mod.sparse_topk(*csr, *one, k, row_mask=mask)
+                for _ in range(3):
+                    _same(_run(idx, one, k, gpu, mask=mask), want1)
