@@ -111,7 +111,10 @@ __global__ void postings_kernel(const uint32_t* __restrict__ skeys, const int32_
   const int64_t pos = i + t;
   const int32_t e = sent[i];
   prow[pos] = row_of[e];
-  pval[pos] = values[e];
+  // a zero value is kept as -0.0: the scan's staging rows use bit pattern 0 for "no posting",
+  // and fl32(w * -0.0) added to an fp32 sum changes it exactly as fl32(w * +0.0) does (not at all)
+  const float v = values[e];
+  pval[pos] = __float_as_uint(v) == 0u ? __uint_as_float(0x80000000u) : v;
 }
 
 __global__ void sentinels_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
@@ -187,11 +190,12 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const int32_t* __restrict__ q_indptr, const int32_t* __restrict__ q_indices,
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, TermMeta* __restrict__ wl, int32_t* __restrict__ wl_count,
-    uint32_t* __restrict__ flags) {
+    int32_t* __restrict__ qof, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
   float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
   __shared__ int32_t off[kQB + 1];
+  __shared__ int32_t qslot[kQB];
   __shared__ int32_t part[1024];
   const int tid = threadIdx.x;
   const int wave = armi::wave_id();
@@ -212,6 +216,25 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     }
     off[tid + 1] = x;
     if (tid == 0) off[0] = 0;
+    // balance the waves: queries sorted by term count (desc, then index) are dealt to the waves
+    // in snake order, so each wave's union of terms (its per-tile work) is about the same
+    int sk = (tid < nq ? n : -1) * 64 + (63 - tid);
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const int o = __shfl_xor(sk, stride);
+        const bool lower = (lane & stride) == 0;
+        const bool desc = (lane & size) == 0;
+        if ((lower == desc) ? (o > sk) : (o < sk)) sk = o;
+      }
+    }
+    const int r = lane;  // rank
+    const int q = 63 - (sk & 63);
+    const int w = ((r >> 4) & 1) ? 15 - (r & 15) : (r & 15);
+    const int slot = (w << 2) | (r >> 4);
+    qslot[q] = slot;
+    qof[slot] = r < nq ? q : -1;
   }
   __syncthreads();
   const int total = off[kQB];
@@ -230,27 +253,62 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
       const int32_t p = q_indptr[q] + (e - off[q]);
       const int32_t t = q_indices[p];
       if (t >= 0 && t < vocab) {
-        k = ((uint32_t)t << 6) | ((uint32_t)(q & 15) << 2) | (uint32_t)(q >> 4);
+        k = ((uint32_t)t << 6) | (uint32_t)qslot[q];
         v = q_values[p];
       }
     }
     key[e] = k;
     val[e] = v;
   }
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (int e = tid; e < n2; e += 1024) {
-        const int o = e ^ stride;
-        if (o > e) {
-          const bool up = (e & size) == 0;
-          const uint32_t x = key[e], y = key[o];
-          if ((x > y) == up) {
-            key[e] = y;
-            key[o] = x;
-            const float tv = val[e];
-            val[e] = val[o];
-            val[o] = tv;
+  if (n2 <= 1024) {
+    // one element per thread: in-wave stages by shuffles, cross-wave stages through LDS
+    __syncthreads();
+    uint32_t kk = tid < n2 ? key[tid] : 0xffffffffu;
+    float vv = tid < n2 ? val[tid] : 0.f;
+    for (int size = 2; size <= n2; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        uint32_t ok;
+        float ov;
+        if (stride >= 64) {
+          __syncthreads();
+          key[tid] = kk;
+          val[tid] = vv;
+          __syncthreads();
+          ok = key[tid ^ stride];
+          ov = val[tid ^ stride];
+        } else {
+          ok = (uint32_t)__shfl_xor((int)kk, stride);
+          ov = __shfl_xor(vv, stride);
+        }
+        const bool lower = (tid & stride) == 0;
+        const bool up = (tid & size) == 0;
+        if ((lower == up) ? (ok < kk) : (ok > kk)) {
+          kk = ok;
+          vv = ov;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < n2) {
+      key[tid] = kk;
+      val[tid] = vv;
+    }
+  } else {
+    for (int size = 2; size <= n2; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        __syncthreads();
+        for (int e = tid; e < n2; e += 1024) {
+          const int o = e ^ stride;
+          if (o > e) {
+            const bool up = (e & size) == 0;
+            const uint32_t x = key[e], y = key[o];
+            if ((x > y) == up) {
+              key[e] = y;
+              key[o] = x;
+              const float tv = val[e];
+              val[e] = val[o];
+              val[o] = tv;
+            }
           }
         }
       }
@@ -371,7 +429,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const int32_t* __restrict__ start_tab, int64_t n_rows, int64_t range_rows, int n_ranges,
     const uint64_t* __restrict__ row_mask, int nq, const int32_t* __restrict__ uterm,
     const int32_t* __restrict__ n_terms, const TermMeta* __restrict__ wl,
-    const int32_t* __restrict__ wl_count, int2* __restrict__ cursors,
+    const int32_t* __restrict__ wl_count, const int32_t* __restrict__ qof,
+    int2* __restrict__ cursors,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
     int32_t* __restrict__ coll_row, int dbg) {
@@ -379,14 +438,17 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   const int g = blockIdx.x;
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
-  const bool has_q = wave < nq;
+  int qw[kQW];  // this wave's queries (-1: none)
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) qw[i] = qof[wave * kQW + i];
+  const bool has_q = qw[0] >= 0;
   float tq[kQW];
   if constexpr (kCollect) {
     bool any = false;
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
-      const int q = wave + kWaves * i;
-      tq[i] = q < nq ? thr[q] : std::numeric_limits<float>::infinity();
+      const int q = qw[i];
+      tq[i] = q >= 0 ? thr[q] : std::numeric_limits<float>::infinity();
       any |= tq[i] != std::numeric_limits<float>::infinity();
     }
     if (!__syncthreads_or(any)) return;  // workgroup-uniform
@@ -449,7 +511,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     for (int k = 0; k < kHold; ++k) {
       if ((amask >> k) & 1u) {
         const int c = rl_i(cv.x, base + k);
-        srow[k] = prow[c + 63 - lane];
+        srow[k] = prow[c + 63 - lane];  // posting c + p sits in lane 63 - p
         sval[k] = pval[c + 63 - lane];
       }
     }
@@ -462,6 +524,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     uint32_t* buf = sbuf + (size_t)(s & 1) * kU * 64;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
+      uint32_t* row = buf + (k * kWaves + wave) * 64;
       if ((amask >> k) & 1u) {
         const unsigned long long outb = ~__ballot(srow[k] < thi);
         const int n_in = outb == 0 ? 64 : __builtin_clzll(outb);  // postings inside the tile
@@ -470,12 +533,11 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
           scv.x += n_in;
           scv.y = nr;
         }
-        uint32_t* row = buf + (k * kWaves + wave) * 64;
         row[lane] = 0u;
-        const uint32_t vb = __float_as_uint(sval[k]);
-        if (lane >= 64 - n_in) row[srow[k] - tlo] = vb == 0u ? 0x80000000u : vb;
+        // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
+        if (lane >= 64 - n_in) row[srow[k] - tlo] = __float_as_uint(sval[k]);
       } else if ((hmask >> k) & 1u) {
-        buf[(k * kWaves + wave) * 64 + lane] = 0u;  // held but idle this step: an all-miss row
+        row[lane] = 0u;  // held but idle this step: an all-miss row
       }
     }
     if (seg < kRegSegs) {
@@ -543,7 +605,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       const bool cand = ok && ((hb >> i) & 1u);
       const float sc = i == 0 ? acc01.x : i == 1 ? acc01.y : i == 2 ? acc23.x : acc23.y;
       if constexpr (kCollect) {
-        const int q = wave + kWaves * i;
+        const int q = qw[i];
         if (cand && sc >= tq[i]) {
           const int slot = atomicAdd(&coll_count[q], 1);
           if (slot < kCollectCap) {
@@ -614,7 +676,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     if (has_q) {
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
-        const int q = wave + kWaves * i;
+        const int q = qw[i];
         // top 16 of the 128 lane entries: sort both list levels, bitonic split of their heads
         float ka = l1s[i], kb = l2s[i];
         int32_t ra = l1r[i], rb = l2r[i];
@@ -637,7 +699,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) b = fmaxf(b, __shfl_xor(b, o));
         armi::wave_sort_approx_desc(ck, cr);
-        if (q < nq) {
+        if (q >= 0) {
           const size_t base = (size_t)g * kQB + q;
           if (lane < kKW) {
             cand_key[base * kKW + lane] = ck;
@@ -784,6 +846,7 @@ struct Workspace {
   int32_t* n_terms;
   TermMeta* wl;
   int32_t* wl_count;
+  int32_t* qof;
   int2* cursors;
   float* cand_key;
   int32_t* cand_row;
@@ -803,6 +866,7 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   w.n_terms = cv.take<int32_t>(1);
   w.wl = cv.take<TermMeta>((size_t)kWaves * kWaveTerms);
   w.wl_count = cv.take<int32_t>(kWaves);
+  w.qof = cv.take<int32_t>(kQB);
   w.cursors = cv.take<int2>(nr * kMaxU);
   w.cand_key = cv.take<float>(nr * kQB * kKW);
   w.cand_row = cv.take<int32_t>(nr * kQB * kKW);
@@ -1017,11 +1081,11 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
     pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
         q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.wl,
-        w.wl_count, pflags);
+        w.wl_count, w.qof, pflags);
     ARMI_LAUNCHED("pass_terms_kernel");
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
-        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
     if (dbg & 8) {
@@ -1050,7 +1114,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     ARMI_LAUNCHED("sparse_merge_kernel");
     sparse_scan_kernel<true><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
-        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp), dim3(256), lds_collect, stream>>>(
