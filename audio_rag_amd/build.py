@@ -27,6 +27,8 @@ ARCH = os.environ.get("ARMI_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-ffp-contract=off",
          f"-I{ROOT / 'include'}"]
+# extra flags for diagnostic builds, e.g. ARMI_BUILD_FLAGS=-DARMI_SPARSE_PROFILE
+FLAGS += os.environ.get("ARMI_BUILD_FLAGS", "").split()
 
 
 def _digest(path: Path, headers: list[Path]) -> str:

@@ -133,6 +133,34 @@ __device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) 
   }
 }
 
+// N independent wave sorts at once: every stage issues all N lists' shuffles before using any,
+// so the N dependent shuffle chains overlap instead of running back to back.
+template <int N>
+__device__ __forceinline__ void wave_sort_approx_desc_n(float (&key)[N], int32_t (&row)[N]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      float ok[N];
+      int32_t orow[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        ok[n] = __shfl_xor(key[n], stride);
+        orow[n] = __shfl_xor(row[n], stride);
+      }
+      const bool lower = (lane & stride) == 0;
+      const bool desc = (lane & size) == 0;
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        const bool other_better = approx_better(ok[n], orow[n], key[n], row[n]);
+        const bool take_other = (lower == desc) ? other_better : !other_better;
+        if (take_other) { key[n] = ok[n]; row[n] = orow[n]; }
+      }
+    }
+  }
+}
+
 // Wave index within the workgroup as a wave-uniform (SGPR) value: the compiler cannot prove
 // threadIdx.x >> 6 uniform by itself, and everything derived from a "divergent" wave index
 // (list pointers, loop bounds, loaded metadata) would otherwise go to VGPRs and exec-masked flow.

@@ -235,22 +235,35 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   ldisc[r * 16 + slot] = d0;
   ldisc[(32 + r) * 16 + slot] = d1;
   __syncthreads();
-  for (int qq = 0; qq < kQB / kWaves; ++qq) {
-    const int q = wave * (kQB / kWaves) + qq;
+  // each wave merges its kQB / kWaves queries together (interleaved shuffle chains)
+  constexpr int QW = kQB / kWaves;
+  float key[QW], b[QW];
+  int32_t row[QW];
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq) {
+    const int q = wave * QW + qq;
+    key[qq] = lkey[q * 64 + lane];
+    row[qq] = lrow[q * 64 + lane];
+    b[qq] = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
+  }
+  armi::wave_sort_approx_desc_n<QW>(key, row);
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq)
+    if (lane == kKW) b[qq] = fmaxf(b[qq], key[qq]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int qq = 0; qq < QW; ++qq) b[qq] = fmaxf(b[qq], __shfl_xor(b[qq], off));
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq) {
+    const int q = wave * QW + qq;
     if (q >= nq) break;
-    float key = lkey[q * 64 + lane];
-    int32_t row = lrow[q * 64 + lane];
-    armi::wave_sort_approx_desc(key, row);
     const size_t base = (size_t)blockIdx.x * kQB + q;
     if (lane < kKW) {
-      cand_key[base * kKW + lane] = key;
-      cand_row[base * kKW + lane] = row;
+      cand_key[base * kKW + lane] = key[qq];
+      cand_row[base * kKW + lane] = row[qq];
     }
-    float b = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
-    if (lane == kKW) b = fmaxf(b, key);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
-    if (lane == 0) cand_bound[base] = b;
+    if (lane == 0) cand_bound[base] = b[qq];
   }
 }
 

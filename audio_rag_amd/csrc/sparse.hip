@@ -377,7 +377,16 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
 
 // ------------------------------------------------------------------------- scan
 
-__device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 8];  // debug phase timers
+#ifdef ARMI_SPARSE_PROFILE
+// Profiling build only (ARMI_BUILD_FLAGS=-DARMI_SPARSE_PROFILE): per-wave phase timers and the
+// ARMI_SPARSE_DBG knobs (1 = skip compute, 2 = stage nothing, 4 = no step barrier, 8 = report).
+__device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 8];
+#define ARMI_PROF_T(x) x = wall_clock64()
+#define ARMI_PROF_ADD(i, a, b) tp[i] += (b) - (a)
+#else
+#define ARMI_PROF_T(x) (void)0
+#define ARMI_PROF_ADD(i, a, b) (void)0
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -630,22 +639,26 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 
   const int S = n_tiles * nSeg;
   unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long t_a = wall_clock64();
+  unsigned long long t_a = 0, t_b = 0;
+  (void)tp;
+  (void)t_a;
+  (void)t_b;
+  ARMI_PROF_T(t_a);
   if (S > 0) {
     issue(0);
     finish(0);
   }
   __syncthreads();
-  unsigned long long t_b = wall_clock64();
-  tp[5] += t_b - t_a;
+  ARMI_PROF_T(t_b);
+  ARMI_PROF_ADD(5, t_a, t_b);
   for (int s = 0; s < S; ++s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
     // loaded now, used after this step's compute
     const uint64_t mrow = (row_mask && seg == nSeg - 1) ? row_mask[(lo >> 6) + tile] : ~0ull;
-    t_a = wall_clock64();
+    ARMI_PROF_T(t_a);
     if (s + 1 < S) issue(s + 1);
-    t_b = wall_clock64();
-    tp[0] += t_b - t_a;
+    ARMI_PROF_T(t_b);
+    ARMI_PROF_ADD(0, t_a, t_b);
     if (has_q) {
       if (seg == 0) {
         acc01 = f2{0.f, 0.f};
@@ -653,59 +666,75 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
         hb = 0;
       }
       if (!(dbg & 1)) compute(s);
-      t_a = wall_clock64();
-      tp[1] += t_a - t_b;
+      ARMI_PROF_T(t_a);
+      ARMI_PROF_ADD(1, t_b, t_a);
       if (seg == nSeg - 1) candidates(tile, mrow);
-      t_b = wall_clock64();
-      tp[2] += t_b - t_a;
+      ARMI_PROF_T(t_b);
+      ARMI_PROF_ADD(2, t_a, t_b);
     }
     if (s + 1 < S) finish(s + 1);
-    t_a = wall_clock64();
-    tp[3] += t_a - t_b;
+    ARMI_PROF_T(t_a);
+    ARMI_PROF_ADD(3, t_b, t_a);
     if (!(dbg & 4)) __syncthreads();
-    t_b = wall_clock64();
-    tp[4] += t_b - t_a;
+    ARMI_PROF_T(t_b);
+    ARMI_PROF_ADD(4, t_a, t_b);
   }
+#ifdef ARMI_SPARSE_PROFILE
   if ((dbg & 8) && lane == 0) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) g_sparse_prof[((size_t)g * kWaves + wave) * 8 + i] = tp[i];
     g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 6] = n_w;
     g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 7] = S;
   }
+#endif
   if constexpr (!kCollect) {
     if (has_q) {
+      // per query: top 16 of the 128 lane entries (sort both list levels, bitonic split of their
+      // heads); the kQW queries' sorts run together so their shuffle chains overlap
+      float ka[kQW], kb[kQW], ck[kQW], bq[kQW];
+      int32_t ra[kQW], rb[kQW], cr[kQW];
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) {
+        ka[i] = l1s[i];
+        ra[i] = l1r[i];
+        kb[i] = l2s[i];
+        rb[i] = l2r[i];
+      }
+      armi::wave_sort_approx_desc_n<kQW>(ka, ra);
+      armi::wave_sort_approx_desc_n<kQW>(kb, rb);
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) {
+        const float kbr = __shfl(kb[i], (15 - lane) & 63);
+        const int32_t rbr = __shfl(rb[i], (15 - lane) & 63);
+        const float kb16 = __shfl(kb[i], 16);
+        float lose = kNegInf;
+        ck[i] = kNegInf;
+        cr[i] = kEndRow;
+        if (lane < 16) {
+          const bool take_a = armi::approx_better(ka[i], ra[i], kbr, rbr);
+          ck[i] = take_a ? ka[i] : kbr;
+          cr[i] = take_a ? ra[i] : rbr;
+          lose = take_a ? kbr : ka[i];
+        } else if (lane == 16) {
+          lose = fmaxf(ka[i], kb16);
+        }
+        bq[i] = fmaxf(disc[i], lose);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int i = 0; i < kQW; ++i) bq[i] = fmaxf(bq[i], __shfl_xor(bq[i], o));
+      armi::wave_sort_approx_desc_n<kQW>(ck, cr);
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
         const int q = qw[i];
-        // top 16 of the 128 lane entries: sort both list levels, bitonic split of their heads
-        float ka = l1s[i], kb = l2s[i];
-        int32_t ra = l1r[i], rb = l2r[i];
-        armi::wave_sort_approx_desc(ka, ra);
-        armi::wave_sort_approx_desc(kb, rb);
-        const float kbr = __shfl(kb, (15 - lane) & 63);
-        const int32_t rbr = __shfl(rb, (15 - lane) & 63);
-        const float kb16 = __shfl(kb, 16);
-        float ck = kNegInf, lose = kNegInf;
-        int32_t cr = kEndRow;
-        if (lane < 16) {
-          const bool take_a = armi::approx_better(ka, ra, kbr, rbr);
-          ck = take_a ? ka : kbr;
-          cr = take_a ? ra : rbr;
-          lose = take_a ? kbr : ka;
-        } else if (lane == 16) {
-          lose = fmaxf(ka, kb16);
-        }
-        float b = fmaxf(disc[i], lose);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) b = fmaxf(b, __shfl_xor(b, o));
-        armi::wave_sort_approx_desc(ck, cr);
         if (q >= 0) {
           const size_t base = (size_t)g * kQB + q;
           if (lane < kKW) {
-            cand_key[base * kKW + lane] = ck;
-            cand_row[base * kKW + lane] = cr;
+            cand_key[base * kKW + lane] = ck[i];
+            cand_row[base * kKW + lane] = cr[i];
           }
-          if (lane == 0) cand_bound[base] = b;
+          if (lane == 0) cand_bound[base] = bq[i];
         }
       }
     }
@@ -1059,7 +1088,11 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
                "armi_sparse_topk: workspace too small");
   ARMI_HIP(hipSetDevice(idx->device));
   const Workspace w = carve(workspace, idx);
+#ifdef ARMI_SPARSE_PROFILE
   static const int dbg = getenv("ARMI_SPARSE_DBG") ? atoi(getenv("ARMI_SPARSE_DBG")) : 0;
+#else
+  constexpr int dbg = 0;
+#endif
   const size_t lds_collect = (size_t)kCollectCap * 8;
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect));
@@ -1088,6 +1121,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
+#ifdef ARMI_SPARSE_PROFILE
     if (dbg & 8) {
       std::vector<unsigned long long> h((size_t)kMaxRanges * kWaves * 8);
       ARMI_HIP(hipStreamSynchronize(stream));
@@ -1108,6 +1142,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
               mx[2] / 100, sum[3] / cnt / 100, mx[3] / 100, sum[4] / cnt / 100, mx[4] / 100,
               sum[5] / cnt / 100, mx[5] / 100, sum[6] / cnt, mx[6], mx[7]);
     }
+#endif
     sparse_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
         w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, idx->ordinal_base,
         out_scores, out_ids, out_count, pflags, w.kth);
