@@ -1,0 +1,315 @@
+// Fused masked self-attention + fp16 glue kernels of the XLM-RoBERTa cross-encoder that
+// BGEReranker runs through sentence-transformers' CrossEncoder.predict
+// (src/audio_rag/reranking/bge.py:119-123; BAAI/bge-reranker-base: 12 heads x 64, L <= 512 at
+// bge.py:53). Replaces the eager QK^T -> masked softmax -> PV of XLMRobertaSelfAttention, which
+// materialises an fp32 [n, H, L, L] score tensor per layer (4 GB at 1280 pairs x L 256), with
+// one pass that keeps K and V^T of a (sequence, head) in LDS and the scores in registers.
+//
+// Layout (row-major, fp16 bit patterns):
+//   qkv  [n_seq][L][3][H][64]   the fused QKV projection output ([n*L][3*H*64])
+//   mask [n_seq][L] int32       key mask (0 = padding key)
+//   ctx  [n_seq][L][H][64]      attention output, already in the layout the output projection
+//                               consumes ([n*L][H*64]); no permute/copy
+//
+// Per workgroup: one (sequence, head, block of 128 queries); 4 waves x 32 queries.
+//   S^T = K . Q^T with v_mfma_f32_32x32x16_f16 puts one query on each lane (16 of a 32-key block
+//   per lane half), so row max / row sum are in-lane plus one cross-half shuffle.
+//   Pass 1 sweeps all key blocks for the exact row max m and sum l (online rescale of l only).
+//   Pass 2 recomputes S^T, forms P = exp(s - m) / l in fp16 straight from the accumulator
+//   registers (the accumulator of S^T is the A operand of P.V without any lane movement) and
+//   accumulates O = P . V against V^T in LDS. O needs no rescale, so it is final when the sweep
+//   ends. Recomputing QK^T costs 1/3 more attention MFMAs, ~2% of the encoder's FLOPs at L=256.
+#include <cmath>
+#include <limits>
+
+#include "armi_common.h"
+
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kDh = 64;           // head dim (XLM-R base and large)
+constexpr int kQPerWave = 32;
+constexpr int kWaves = 4;
+constexpr int kQPerWg = kQPerWave * kWaves;
+constexpr int kKStride = kDh + 8;  // K row stride in halves (144 B: conflict-free b128 reads)
+constexpr int kMaxL = 512;
+
+__device__ __forceinline__ int vt_stride(int lp) { return lp + 4; }  // V^T row stride (halves)
+
+__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a),
+                                                __builtin_bit_cast(half8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+  half2v v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// S^T block (32 keys x 32 queries) of key block kb: lane (r, h) gets keys (i&3)+8(i>>2)+4h of
+// the block for query r in register i.
+__device__ __forceinline__ f32x16 score_block(const uint16_t* __restrict__ ks, int kb, int r,
+                                              int h, const u32x4 (&qf)[kDh / 16]) {
+  f32x16 acc = {};
+  const uint16_t* krow = ks + (kb * 32 + r) * kKStride + 8 * h;
+#pragma unroll
+  for (int t = 0; t < kDh / 16; ++t) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(krow + 16 * t);
+    acc = mfma16(a, qf[t], acc);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void attention_f16_kernel(
+    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
+    int L, int heads, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lp = (L + 31) & ~31;
+  const int vts = vt_stride(lp);
+  uint16_t* ks = reinterpret_cast<uint16_t*>(smem);               // [lp][kKStride]
+  uint16_t* vt = ks + lp * kKStride;                               // [kDh][vts]
+  float* kbias = reinterpret_cast<float*>(vt + kDh * vts);         // [lp] 0 or -inf
+
+  const int qblk = blockIdx.x;
+  const int head = blockIdx.y;
+  const int seq = blockIdx.z;
+  const int tid = threadIdx.x;
+  const int row_stride = 3 * heads * kDh;  // halves between consecutive tokens
+  const uint16_t* base = qkv + (size_t)seq * L * row_stride + head * kDh;
+
+  // stage K (row-major) and V^T (two keys per 32-bit LDS word) of this (seq, head)
+  for (int e = tid; e < lp * (kDh / 8); e += 256) {
+    const int j = e >> 3, c = e & 7;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (j < L) v = *reinterpret_cast<const u32x4*>(base + (size_t)j * row_stride + heads * kDh + 8 * c);
+    *reinterpret_cast<u32x4*>(ks + j * kKStride + 8 * c) = v;
+  }
+  for (int e = tid; e < (lp / 2) * (kDh / 8); e += 256) {
+    const int jp = e >> 3, c = e & 7;
+    const int j = 2 * jp;
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+    const uint16_t* vbase = base + 2 * heads * kDh + 8 * c;
+    if (j < L) a = *reinterpret_cast<const u32x4*>(vbase + (size_t)j * row_stride);
+    if (j + 1 < L) b = *reinterpret_cast<const u32x4*>(vbase + (size_t)(j + 1) * row_stride);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
+      const uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
+      *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i) * vts + j) = lo;
+      *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i + 1) * vts + j) = hi;
+    }
+  }
+  for (int j = tid; j < lp; j += 256)
+    kbias[j] = (j < L && mask[(size_t)seq * L + j] != 0) ? 0.f : -INFINITY;
+
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int q = qblk * kQPerWg + wave * kQPerWave + r;
+  u32x4 qf[kDh / 16];
+#pragma unroll
+  for (int t = 0; t < kDh / 16; ++t) {
+    qf[t] = u32x4{0u, 0u, 0u, 0u};
+    if (q < L) qf[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
+  }
+  __syncthreads();
+  const int nkb = lp / 32;
+
+  // pass 1: row max and row sum (exp2 domain: s' = s * scale * log2 e)
+  float m = -INFINITY, l = 0.f;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const f32x16 acc = score_block(ks, kb, r, h, qf);
+    float s[16];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s[i] = acc[i] * scale_log2 + kbias[kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
+      bm = fmaxf(bm, s[i]);
+    }
+    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float mn = fmaxf(m, bm);
+    if (mn != -INFINITY) {
+      float add = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) add += exp2f(s[i] - mn);
+      l = l * exp2f(m - mn) + add;  // m == -inf -> l == 0 and exp2f(-inf) == 0
+      m = mn;
+    }
+  }
+  l += __shfl_xor(l, 32);
+  const float inv_l = l > 0.f ? 1.0f / l : 0.f;
+
+  // pass 2: O = softmax(S) . V
+  f32x16 o0 = {}, o1 = {};
+  const uint16_t* v0 = vt + r * vts + 4 * h;
+  const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const f32x16 acc = score_block(ks, kb, r, h, qf);
+    float p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float s = acc[i] * scale_log2 + kbias[kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
+      p[i] = (m == -INFINITY) ? 0.f : exp2f(s - m) * inv_l;
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      // A fragment of k-step st: registers 8st..8st+7 = keys 16st + 8(j>>2) + 4h + (j&3)
+      u32x4 pa;
+      pa[0] = pack_h2(p[8 * st + 0], p[8 * st + 1]);
+      pa[1] = pack_h2(p[8 * st + 2], p[8 * st + 3]);
+      pa[2] = pack_h2(p[8 * st + 4], p[8 * st + 5]);
+      pa[3] = pack_h2(p[8 * st + 6], p[8 * st + 7]);
+      const int key0 = kb * 32 + 16 * st;
+      const u32x2 a0 = *reinterpret_cast<const u32x2*>(v0 + key0);
+      const u32x2 a1 = *reinterpret_cast<const u32x2*>(v0 + key0 + 8);
+      const u32x2 b0 = *reinterpret_cast<const u32x2*>(v1 + key0);
+      const u32x2 b1 = *reinterpret_cast<const u32x2*>(v1 + key0 + 8);
+      o0 = mfma16(pa, u32x4{a0[0], a0[1], a1[0], a1[1]}, o0);
+      o1 = mfma16(pa, u32x4{b0[0], b0[1], b1[0], b1[1]}, o1);
+    }
+  }
+
+  // O tile: register i holds query (i&3)+8(i>>2)+4h of the wave's 32, dims r and 32 + r
+  const int qw0 = qblk * kQPerWg + wave * kQPerWave;
+  uint16_t* out = ctx + ((size_t)seq * L) * (heads * kDh) + head * kDh;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int qq = qw0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (qq < L) {
+      uint16_t* dst = out + (size_t)qq * (heads * kDh);
+      dst[r] = __builtin_bit_cast(uint16_t, (_Float16)o0[i]);
+      dst[32 + r] = __builtin_bit_cast(uint16_t, (_Float16)o1[i]);
+    }
+  }
+}
+
+// out = LayerNorm(x + res) (x fp16, res fp32 nullable) -> fp32 out and fp16 out16 (nullable).
+constexpr int kMaxPerLane = 16;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void layernorm_residual_f16_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ res, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ out, uint16_t* __restrict__ out16,
+    int64_t n_rows, int width, float eps) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const uint16_t* xr = x + row * width;
+  const float* rr = res ? res + row * width : nullptr;
+  float v[kMaxPerLane];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = 0.f;
+    if (c < width) {
+      v[i] = (float)__builtin_bit_cast(_Float16, xr[c]) + (rr ? rr[c] : 0.f);
+      s += v[i];
+    }
+  }
+  const float mean = wave_sum(s) / (float)width;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i)
+    if (lane + 64 * i < width) {
+      const float d = v[i] - mean;
+      ss += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)width + eps);
+#pragma unroll
+  for (int i = 0; i < kMaxPerLane; ++i) {
+    const int c = lane + 64 * i;
+    if (c < width) {
+      const float y = (v[i] - mean) * rstd * gamma[c] + beta[c];
+      out[row * width + c] = y;
+      if (out16) out16[row * width + c] = __builtin_bit_cast(uint16_t, (_Float16)y);
+    }
+  }
+}
+
+// in-place exact-erf GELU of fp16 x (+ fp32 bias[col], nullable), computed in fp32
+__global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
+                                                       const float* __restrict__ bias, int64_t n,
+                                                       int width) {
+  const int64_t i8 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i8 >= n) return;
+  u32x4 v = *reinterpret_cast<const u32x4*>(x + i8);
+  const int c0 = (int)(i8 % width);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t word = v[w];  // (bit_cast of a vector-element lvalue miscompiles)
+    const half2v hv = __builtin_bit_cast(half2v, word);
+    float t0 = (float)hv[0] + (bias ? bias[c0 + 2 * w] : 0.f);
+    float t1 = (float)hv[1] + (bias ? bias[c0 + 2 * w + 1] : 0.f);
+    t0 = 0.5f * t0 * (1.0f + erff(t0 * 0.70710678118654752440f));
+    t1 = 0.5f * t1 * (1.0f + erff(t1 * 0.70710678118654752440f));
+    v[w] = pack_h2(t0, t1);
+  }
+  *reinterpret_cast<u32x4*>(x + i8) = v;
+}
+
+size_t attention_lds_bytes(int L) {
+  const int lp = (L + 31) & ~31;
+  return (size_t)lp * kKStride * 2 + (size_t)kDh * (lp + 4) * 2 + (size_t)lp * 4;
+}
+
+}  // namespace
+
+extern "C" {
+
+int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* ctx, int n_seq,
+                           int L, int heads, int head_dim, float scale, hipStream_t stream) {
+  ARMI_REQUIRE(head_dim == kDh, "attention_f16: head_dim must be 64");
+  ARMI_REQUIRE(L >= 1 && L <= kMaxL, "attention_f16: L must be in [1, 512]");
+  ARMI_REQUIRE(heads >= 1 && heads <= 65535, "attention_f16: bad head count");
+  if (n_seq <= 0) return ARMI_OK;
+  ARMI_REQUIRE(n_seq <= 65535, "attention_f16: n_seq must be <= 65535 per call");
+  ARMI_REQUIRE(qkv && mask && ctx, "attention_f16: null pointer argument");
+  const size_t lds = attention_lds_bytes(L);
+  if (lds > 65536)
+    ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_f16_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const float scale_log2 = scale * 1.4426950408889634f;
+  attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(256), lds,
+                         stream>>>(qkv, mask, ctx, L, heads, scale_log2);
+  ARMI_LAUNCHED("attention_f16_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_layernorm_residual_f16(const uint16_t* x, const float* res, const float* gamma,
+                                    const float* beta, float* out, uint16_t* out16,
+                                    int64_t n_rows, int width, float eps, hipStream_t stream) {
+  ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane,
+               "layernorm_f16: width must be in [1, 1024]");
+  if (n_rows <= 0) return ARMI_OK;
+  ARMI_REQUIRE(x && gamma && beta && out, "layernorm_f16: null pointer argument");
+  layernorm_residual_f16_kernel<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, stream>>>(
+      x, res, gamma, beta, out, out16, n_rows, width, eps);
+  ARMI_LAUNCHED("layernorm_residual_f16_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
+                      hipStream_t stream) {
+  ARMI_REQUIRE(width >= 8 && width % 8 == 0, "gelu_f16: width must be a multiple of 8");
+  if (n_rows <= 0) return ARMI_OK;
+  ARMI_REQUIRE(x != nullptr, "gelu_f16: x is null");
+  const int64_t n = n_rows * width;
+  gelu_f16_kernel<<<dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream>>>(x, bias, n,
+                                                                                   width);
+  ARMI_LAUNCHED("gelu_f16_kernel");
+  return ARMI_OK;
+}
+
+}  // extern "C"

@@ -74,12 +74,61 @@ class CrossEncoderXLMR:
                      sd["classifier.out_proj.bias"])
 
     def to_dtype(self, dtype: torch.dtype) -> None:
-        """GEMM operand dtype (fp32 or bf16, fp32 accumulate); LayerNorm / softmax / GELU / head
-        stay fp32 in the armi kernels."""
+        """GEMM operand dtype, fp32 accumulate.
+        fp32 / bf16: LayerNorm / softmax / GELU / head stay fp32 in the armi kernels.
+        fp16: the fp16 forward (_forward_f16): fp16 GEMM outputs, fused fp16 attention
+        (armi_enc_attention_f16), fp32 residual stream and LayerNorm statistics."""
         self.gemm_dtype = dtype
         for ly in self.layers:
             for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
                 ly[name + "_g"] = ly[name].to(dtype)
+            if dtype == torch.float16:
+                # nn.Linear layout [out, in] for F.linear (the TN GEMM hipBLASLt tunes best)
+                for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
+                    ly[name[:-2] + "_h"] = ly[name].t().contiguous().half()
+                for name in ("bqkv", "bo", "bi", "bo2"):
+                    ly[name + "_h"] = ly[name].half()
+
+    def _forward_f16(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        n, L = ids.shape
+        d, H, dh = self.d, self.heads, self.dh
+        s = stream_handle()
+        rows = n * L
+        lin = torch.nn.functional.linear
+        h = torch.empty((rows, d), dtype=torch.float32, device=self.device)
+        call("armi_enc_embed", ptr(ids), ptr(self.word), ptr(self.pos), ptr(self.type0),
+             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad,
+             self.word.shape[0], self.pos.shape[0], self.eps, s)
+        h16 = h.half()
+        scale = 1.0 / math.sqrt(dh)
+        for ly in self.layers:
+            qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])                     # [n*L, 3d] fp16
+            ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
+            call("armi_enc_attention_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh, scale, s)
+            attn = lin(ctx, ly["wo_h"], ly["bo_h"])
+            h1 = torch.empty_like(h)
+            h1_16 = torch.empty_like(h16)
+            call("armi_enc_layernorm_residual_f16", ptr(attn), ptr(h), ptr(ly["ln1"][0]),
+                 ptr(ly["ln1"][1]), ptr(h1), ptr(h1_16), rows, d, self.eps, s)
+            inter = lin(h1_16, ly["wi_h"], ly["bi_h"])                      # [n*L, 4d] fp16
+            call("armi_enc_gelu_f16", ptr(inter), None, rows, inter.shape[1], s)
+            out = lin(inter, ly["wo2_h"], ly["bo2_h"])
+            h = torch.empty_like(h1)
+            h16 = torch.empty_like(h1_16)
+            call("armi_enc_layernorm_residual_f16", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
+                 ptr(ly["ln2"][1]), ptr(h), ptr(h16), rows, d, self.eps, s)
+        probs = torch.empty(n, dtype=torch.float32, device=self.device)
+        call("armi_enc_cls_head_sigmoid", ptr(h), ptr(self.head[0]), ptr(self.head[1]),
+             ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, L, d, s)
+        return probs
+
+    def flops(self, n: int, L: int) -> float:
+        """Matmul FLOPs of one forward over n sequences of length L (projections, FFN,
+        QK^T and PV; the fused attention recomputes QK^T once more, not counted)."""
+        d, ff, layers = self.d, self.layers[0]["wi_t"].shape[1], len(self.layers)
+        per_tok = 2 * (4 * d * d + 2 * d * ff)
+        attn = 2 * 2 * L * L * d
+        return float(layers * (n * L * per_tok + n * attn))
 
     def _mm(self, x: torch.Tensor, ly: dict, name: str, bias: torch.Tensor | None) -> torch.Tensor:
         if self.gemm_dtype == torch.float32:
@@ -91,6 +140,8 @@ class CrossEncoderXLMR:
     @torch.inference_mode()
     def forward(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
         """ids, mask: int32 [n, L] on the device -> sigmoid scores float32 [n]."""
+        if self.gemm_dtype == torch.float16:
+            return self._forward_f16(ids, mask)
         n, L = ids.shape
         d, H, dh = self.d, self.heads, self.dh
         s = stream_handle()

@@ -34,6 +34,9 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# dense (non-sparse) matrix peaks, MI355X_MICROARCH.md: bf16/f16 ~2.5 PF; fp32-input MFMA runs at
+# 1/16 of the bf16 rate (cdna_hip_programming.md §3 'FP32-input MFMA')
+MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.0}
 CHUNK_ROWS = 65536
 
 
@@ -194,7 +197,9 @@ def main() -> None:
                          "(configs[2] without rerank); hybrid_rerank: configs[2]: top-20 fused -> "
                          "cross-encoder -> top-k")
     ap.add_argument("--initial-k", type=int, default=20)
-    ap.add_argument("--rerank-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--rerank-dtype", choices=["fp32", "bf16", "fp16"], default="fp16",
+                    help="cross-encoder GEMM dtype (fp16: fp16 GEMMs + fused fp16 attention, "
+                         "within the 1e-3 score budget; fp32: the reference's dtype)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,8 +239,8 @@ def main() -> None:
     if wl == "hybrid_rerank":
         from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
         reranker = CrossEncoderXLMR(build_reranker(seed=5), dev)
-        if args.rerank_dtype == "bf16":
-            reranker.to_dtype(torch.bfloat16)
+        if args.rerank_dtype != "fp32":
+            reranker.to_dtype({"bf16": torch.bfloat16, "fp16": torch.float16}[args.rerank_dtype])
         gq = torch.Generator(device=dev).manual_seed(4 + rank)
         q_tokens = torch.randint(4, VOCAB, (n_q_batches, batch, 16), generator=gq, device=dev,
                                  dtype=torch.int32)
@@ -244,6 +249,9 @@ def main() -> None:
         sharded = ShardedSearch(lambda q, kk: index.topk(q, kk, workspace=ws), merge_shards,
                                 local_sparse=(lambda c, kk: sindex.topk(*c, kk, workspace=sws)) if sindex else None,
                                 rrf=lambda a, b, kk: rrf_fuse(a, b, kk))
+
+    # live timing of the cross-encoder forward (runs on torch's current stream)
+    rr_timing = {"on": False, "events": [], "flops": 0.0}
 
     def rerank(fused: TopK, qt: torch.Tensor) -> TopK:
         """configs[2]: every query's fused candidates -> (query, chunk) pairs of L = 256 tokens
@@ -257,7 +265,14 @@ def main() -> None:
         pairs = torch.cat([bos, qq, eos, eos, d, eos], dim=2).reshape(nb * kc, -1).contiguous()
         valid = (torch.arange(kc, device=dev)[None, :] < fused.count[:, None])
         mask = torch.ones_like(pairs)
+        if rr_timing["on"]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         probs = reranker.forward(pairs, mask).view(nb, kc)
+        if rr_timing["on"]:
+            ev[1].record()
+            rr_timing["events"].append(ev)
+            rr_timing["flops"] += reranker.flops(pairs.shape[0], pairs.shape[1])
         probs = torch.where(valid, probs, torch.full_like(probs, -1.0))
         order = torch.sort(probs, dim=1, descending=True, stable=True).indices[:, :k]
         return TopK(scores=torch.gather(probs, 1, order), ids=torch.gather(fused.ids, 1, order),
@@ -295,12 +310,15 @@ def main() -> None:
     _armi.call("armi_scan_timing_read", _armi.ctypes.byref(_armi.ctypes.c_double()),
                _armi.ctypes.byref(_armi.ctypes.c_int64()))
     barrier()
+    rr_timing["on"] = reranker is not None
     t0 = time.perf_counter()
     last = None
     for i in range(args.steps):
         last = step(i)
     barrier()
     elapsed = time.perf_counter() - t0
+    rr_timing["on"] = False
+    rr_ms = sum(a.elapsed_time(b) for a, b in rr_timing["events"])
     tot_ms, launches = _armi.ctypes.c_double(), _armi.ctypes.c_int64()
     _armi.call("armi_scan_timing_read", _armi.ctypes.byref(tot_ms), _armi.ctypes.byref(launches))
     _armi.call("armi_scan_timing_enable", 0)
@@ -383,6 +401,25 @@ def main() -> None:
             "launches_timed": launches.value,
         },
     }
+    if reranker is not None and rr_timing["events"]:
+        # configs[2]: the cross-encoder is the dominant (MFMA-bound) stage; the scan roofline
+        # moves to roofline_scan
+        rr_tflops = rr_timing["flops"] / (rr_ms * 1e-3) / 1e12
+        peak = MFMA_PEAK_TFLOPS[args.rerank_dtype]
+        result["roofline_scan"] = result["roofline"]
+        result["roofline"] = {
+            "bound": "mfma",
+            "kernel": f"cross-encoder forward ({args.rerank_dtype} GEMMs, fused attention)",
+            "achieved": rr_tflops,
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": rr_tflops / peak,
+            "traffic": None,
+            "algorithmic_flops_per_step": rr_timing["flops"] / max(len(rr_timing["events"]), 1),
+            "avg_forward_ms": rr_ms / max(len(rr_timing["events"]), 1),
+            "forwards_timed": len(rr_timing["events"]),
+        }
+        result["rerank_share_of_step"] = (rr_ms * 1e-3) / elapsed
     if world == 1 and not args.no_cpu_baseline and wl == "dense":
         result["cpu_baseline"] = cpu_baseline(n, dim, batch, k)
     else:

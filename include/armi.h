@@ -192,6 +192,26 @@ int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const f
                               const float* out_w, const float* out_b, float* out, int n_seq,
                               int L, int width, hipStream_t stream);
 
+/* fp16 forward pieces (fp16 GEMM operands, fp32 residual stream / statistics).
+ * Fused masked self-attention of XLMRobertaSelfAttention (eager QK^T -> softmax -> PV of
+ * transformers, as CrossEncoder.predict runs it for BGEReranker, reranking/bge.py:119-123):
+ *   qkv  [n_seq][L][3][heads][head_dim] fp16 (the fused Q|K|V projection output)
+ *   mask [n_seq][L] int32 key mask (0 = padding key)
+ *   ctx  [n_seq][L][heads][head_dim] fp16 = softmax(Q K^T * scale + mask) V
+ * head_dim must be 64, L <= 512. Scores and softmax statistics are fp32; P is rounded to fp16
+ * for the P.V product (fp32 accumulate). */
+int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* ctx, int n_seq,
+                           int L, int heads, int head_dim, float scale, hipStream_t stream);
+/* out = LayerNorm(x + res) with x fp16 and res fp32 (nullable); writes fp32 out and, when out16
+ * is not null, its fp16 rounding (the next GEMM's operand). */
+int armi_enc_layernorm_residual_f16(const uint16_t* x, const float* res, const float* gamma,
+                                    const float* beta, float* out, uint16_t* out16,
+                                    int64_t n_rows, int width, float eps, hipStream_t stream);
+/* in-place exact (erf) GELU of fp16 x (+ fp32 bias[col], nullable), computed in fp32;
+ * width must be a multiple of 8. */
+int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

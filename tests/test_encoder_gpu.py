@@ -165,6 +165,101 @@ def test_bge_m3_embedder_outputs(gpu):
     assert r.sparse.indices == first
 
 
+def _attention_ref(qkv, mask, H, dh):
+    """Plain PyTorch fp32 eager attention (XLMRobertaSelfAttention) of the fp16 inputs."""
+    n, L, _ = qkv.shape
+    x = qkv.float().view(n, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    add = (1 - mask.float())[:, None, None, :] * torch.finfo(torch.float32).min
+    p = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(dh) + add, dim=-1)
+    return (p @ v).permute(0, 2, 1, 3).reshape(n, L, H * dh)
+
+
+@pytest.mark.parametrize("L", [1, 7, 33, 128, 200, 256, 512])
+def test_attention_f16_matches_fp32_reference(gpu, L):
+    """armi_enc_attention_f16 against fp32 eager attention of the same fp16 Q/K/V; tolerance
+    3e-3 absolute on O(1) outputs (P is rounded to fp16 before P.V)."""
+    g = torch.Generator().manual_seed(100 + L)
+    n, H, dh = 3, 12, 64
+    qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
+    mask = torch.ones(n, L, dtype=torch.int32)
+    mask[1, max(1, L // 2):] = 0
+    mask[2, 1:] = 0  # one key only
+    ref = _attention_ref(qkv, mask, H, dh)
+    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
+    out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
+    _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
+          1 / math.sqrt(dh))
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
+
+
+def test_attention_f16_peaked_scores(gpu):
+    """Large, one-hot-like scores (the running max jumps late in the key sweep)."""
+    n, L, H, dh = 2, 160, 12, 64
+    g = torch.Generator().manual_seed(7)
+    qkv = torch.randn(n, L, 3, H, dh, generator=g) * 0.1
+    qkv[:, :, 1, :, :] *= 0.1
+    qkv[:, 150, 1, :, :] = 4.0  # key 150 dominates every query
+    qkv[:, :, 0, :, :] = qkv[:, :, 0, :, :].abs() + 0.5
+    qkv = qkv.reshape(n, L, 3 * H * dh).half()
+    mask = torch.ones(n, L, dtype=torch.int32)
+    ref = _attention_ref(qkv, mask, H, dh)
+    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
+    out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
+    _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
+          1 / math.sqrt(dh))
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
+
+
+def test_layernorm_f16_and_gelu_f16(gpu):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(300, 768, generator=g).half()
+    r = torch.randn(300, 768, generator=g)
+    w, b = torch.randn(768, generator=g), torch.randn(768, generator=g)
+    ref = torch.nn.functional.layer_norm(x.float() + r, (768,), w, b, 1e-5)
+    X, R, W, B = (t.to(gpu) for t in (x, r, w, b))
+    out = torch.empty(300, 768, device=gpu)
+    out16 = torch.empty(300, 768, dtype=torch.float16, device=gpu)
+    _call("armi_enc_layernorm_residual_f16", X.data_ptr(), R.data_ptr(), W.data_ptr(),
+          B.data_ptr(), out.data_ptr(), out16.data_ptr(), 300, 768, 1e-5)
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=2e-5)
+    assert torch.equal(out16.cpu(), out.cpu().half())
+    y = (torch.randn(64, 3072, generator=g) * 3).half()
+    Y = y.to(gpu).contiguous()
+    _call("armi_enc_gelu_f16", Y.data_ptr(), None, 64, 3072)
+    torch.testing.assert_close(Y.cpu().float(), torch.nn.functional.gelu(y.float()), rtol=2e-3,
+                               atol=2e-3)
+
+
+@pytest.mark.parametrize("L", [64, 256])
+def test_cross_encoder_fp16_within_1e3(gpu, L):
+    """north_star: rerank scores within 1e-3 on the fp16 path (fp16 GEMMs + fused fp16
+    attention + fp32 LayerNorm statistics and residual stream) against transformers' fp32
+    forward of the same seeded bge-reranker-base-shaped weights, ragged pairs included."""
+    from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
+
+    hf = build_reranker(seed=5, arch=dict(attn_implementation="eager"))
+    g = torch.Generator().manual_seed(11)
+    n = 8
+    ids = torch.randint(4, hf.config.vocab_size, (n, L), generator=g)
+    ids[:, 0] = 0
+    mask = torch.ones(n, L, dtype=torch.long)
+    for i in range(n):
+        ln = L - 5 * i
+        ids[i, 16] = 2
+        ids[i, 17] = 2
+        ids[i, ln - 1] = 2
+        ids[i, ln:] = 1
+        mask[i, ln:] = 0
+    ref = _hf_scores(hf, ids, mask)
+    enc = CrossEncoderXLMR(hf, gpu)
+    enc.to_dtype(torch.float16)
+    got = enc.forward(ids.int().to(gpu), mask.int().to(gpu)).cpu()
+    err = (got - ref).abs().max().item()
+    print(f"fp16 path max |score error| = {err:.2e} at L={L}")
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-3)
+
+
 def test_cross_encoder_bf16_gemms_within_budget(gpu):
     """bf16 GEMM operands (fp32 accumulate, fp32 LN/softmax/GELU): measured distance to the fp32
     transformers forward at the full bge-reranker-base shape."""
