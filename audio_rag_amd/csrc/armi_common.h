@@ -133,6 +133,25 @@ __device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) 
   }
 }
 
+// Wave-level bitonic sort of (double key, int64 ordinal), one entry per lane, into descending
+// rank order (key desc, ordinal asc).
+__device__ __forceinline__ void wave_sort_rank_desc(double& key, int64_t& ord) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const double ok = __shfl_xor(key, stride);
+      const int64_t oo = __shfl_xor(ord, stride);
+      const bool lower = (lane & stride) == 0;
+      const bool desc = (lane & size) == 0;
+      const bool other_better = rank_better(ok, oo, key, ord);
+      const bool take_other = (lower == desc) ? other_better : !other_better;
+      if (take_other) { key = ok; ord = oo; }
+    }
+  }
+}
+
 // N independent wave sorts at once: every stage issues all N lists' shuffles before using any,
 // so the N dependent shuffle chains overlap instead of running back to back.
 template <int N>

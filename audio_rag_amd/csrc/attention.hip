@@ -11,14 +11,13 @@
 //   ctx  [n_seq][L][H][64]      attention output, already in the layout the output projection
 //                               consumes ([n*L][H*64]); no permute/copy
 //
-// Per workgroup: one (sequence, head, block of 128 queries); 4 waves x 32 queries.
+// Per workgroup: one (sequence, head, block of 256 queries), 8 waves x 32 queries, so K and V of
+// a (sequence, head) are read from HBM once for L <= 256.
 //   S^T = K . Q^T with v_mfma_f32_32x32x16_f16 puts one query on each lane (16 of a 32-key block
-//   per lane half), so row max / row sum are in-lane plus one cross-half shuffle.
-//   Pass 1 sweeps all key blocks for the exact row max m and sum l (online rescale of l only).
-//   Pass 2 recomputes S^T, forms P = exp(s - m) / l in fp16 straight from the accumulator
-//   registers (the accumulator of S^T is the A operand of P.V without any lane movement) and
-//   accumulates O = P . V against V^T in LDS. O needs no rescale, so it is final when the sweep
-//   ends. Recomputing QK^T costs 1/3 more attention MFMAs, ~2% of the encoder's FLOPs at L=256.
+//   per lane half): row max / row sum are in-lane plus one cross-half shuffle.
+//   O^T = V^T . P^T takes the S^T accumulator (P^T after exp, packed to fp16) as its B operand
+//   with no lane movement, and O^T keeps the query on the lane, so the online-softmax rescale of
+//   O is an in-lane multiply: a single pass over the keys, one exp per score.
 #include <cmath>
 #include <limits>
 
@@ -34,7 +33,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kDh = 64;           // head dim (XLM-R base and large)
 constexpr int kQPerWave = 32;
-constexpr int kWaves = 4;
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
 constexpr int kQPerWg = kQPerWave * kWaves;
 constexpr int kKStride = kDh + 8;  // K row stride in halves (144 B: conflict-free b128 reads)
 constexpr int kMaxL = 512;
@@ -65,7 +65,7 @@ __device__ __forceinline__ f32x16 score_block(const uint16_t* __restrict__ ks, i
   return acc;
 }
 
-__global__ __launch_bounds__(256) void attention_f16_kernel(
+__global__ __launch_bounds__(kThreads) void attention_f16_kernel(
     const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
     int L, int heads, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -83,13 +83,13 @@ __global__ __launch_bounds__(256) void attention_f16_kernel(
   const uint16_t* base = qkv + (size_t)seq * L * row_stride + head * kDh;
 
   // stage K (row-major) and V^T (two keys per 32-bit LDS word) of this (seq, head)
-  for (int e = tid; e < lp * (kDh / 8); e += 256) {
+  for (int e = tid; e < lp * (kDh / 8); e += kThreads) {
     const int j = e >> 3, c = e & 7;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (j < L) v = *reinterpret_cast<const u32x4*>(base + (size_t)j * row_stride + heads * kDh + 8 * c);
     *reinterpret_cast<u32x4*>(ks + j * kKStride + 8 * c) = v;
   }
-  for (int e = tid; e < (lp / 2) * (kDh / 8); e += 256) {
+  for (int e = tid; e < (lp / 2) * (kDh / 8); e += kThreads) {
     const int jp = e >> 3, c = e & 7;
     const int j = 2 * jp;
     u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
@@ -104,14 +104,15 @@ __global__ __launch_bounds__(256) void attention_f16_kernel(
       *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i + 1) * vts + j) = hi;
     }
   }
-  for (int j = tid; j < lp; j += 256)
+  for (int j = tid; j < lp; j += kThreads)
     kbias[j] = (j < L && mask[(size_t)seq * L + j] != 0) ? 0.f : -INFINITY;
 
   const int wave = armi::wave_id();
   const int lane = tid & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int q = qblk * kQPerWg + wave * kQPerWave + r;
+  const int qw0 = qblk * kQPerWg + wave * kQPerWave;
+  const int q = qw0 + r;
   u32x4 qf[kDh / 16];
 #pragma unroll
   for (int t = 0; t < kDh / 16; ++t) {
@@ -119,10 +120,16 @@ __global__ __launch_bounds__(256) void attention_f16_kernel(
     if (q < L) qf[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
   }
   __syncthreads();
+  if (qw0 >= L) return;  // wave-uniform: no query of this wave exists (after the only barrier)
   const int nkb = lp / 32;
 
-  // pass 1: row max and row sum (exp2 domain: s' = s * scale * log2 e)
+  // One pass, online softmax in the exp2 domain (s' = s * scale * log2 e). O is accumulated
+  // transposed, O^T = V^T . P^T: the P^T accumulator of S^T is the B operand as it stands and
+  // O^T's column (the query) is the lane, so the running max, sum and rescale are all in-lane.
   float m = -INFINITY, l = 0.f;
+  f32x16 o0 = {}, o1 = {};  // O^T rows (dims) (i&3)+8(i>>2)+4h and 32 + that, column q
+  const uint16_t* v0 = vt + r * vts + 4 * h;
+  const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
   for (int kb = 0; kb < nkb; ++kb) {
     const f32x16 acc = score_block(ks, kb, r, h, qf);
     float s[16];
@@ -134,57 +141,50 @@ __global__ __launch_bounds__(256) void attention_f16_kernel(
     }
     bm = fmaxf(bm, __shfl_xor(bm, 32));
     const float mn = fmaxf(m, bm);
-    if (mn != -INFINITY) {
-      float add = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) add += exp2f(s[i] - mn);
-      l = l * exp2f(m - mn) + add;  // m == -inf -> l == 0 and exp2f(-inf) == 0
-      m = mn;
-    }
-  }
-  l += __shfl_xor(l, 32);
-  const float inv_l = l > 0.f ? 1.0f / l : 0.f;
-
-  // pass 2: O = softmax(S) . V
-  f32x16 o0 = {}, o1 = {};
-  const uint16_t* v0 = vt + r * vts + 4 * h;
-  const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
-  for (int kb = 0; kb < nkb; ++kb) {
-    const f32x16 acc = score_block(ks, kb, r, h, qf);
+    if (mn == -INFINITY) continue;  // every key so far is padding (same for all lanes)
+    const float alpha = exp2f(m - mn);  // 0 on the first live block (m == -inf)
     float p[16];
+    float add = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float s = acc[i] * scale_log2 + kbias[kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
-      p[i] = (m == -INFINITY) ? 0.f : exp2f(s - m) * inv_l;
+      p[i] = exp2f(s[i] - mn);
+      add += p[i];
     }
+    l = l * alpha + add;
+    m = mn;
+    o0 *= alpha;
+    o1 *= alpha;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      // A fragment of k-step st: registers 8st..8st+7 = keys 16st + 8(j>>2) + 4h + (j&3)
-      u32x4 pa;
-      pa[0] = pack_h2(p[8 * st + 0], p[8 * st + 1]);
-      pa[1] = pack_h2(p[8 * st + 2], p[8 * st + 3]);
-      pa[2] = pack_h2(p[8 * st + 4], p[8 * st + 5]);
-      pa[3] = pack_h2(p[8 * st + 6], p[8 * st + 7]);
+      // B fragment of k-step st: registers 8st..8st+7 = keys 16st + 8(j>>2) + 4h + (j&3)
+      u32x4 pb;
+      pb[0] = pack_h2(p[8 * st + 0], p[8 * st + 1]);
+      pb[1] = pack_h2(p[8 * st + 2], p[8 * st + 3]);
+      pb[2] = pack_h2(p[8 * st + 4], p[8 * st + 5]);
+      pb[3] = pack_h2(p[8 * st + 6], p[8 * st + 7]);
       const int key0 = kb * 32 + 16 * st;
       const u32x2 a0 = *reinterpret_cast<const u32x2*>(v0 + key0);
       const u32x2 a1 = *reinterpret_cast<const u32x2*>(v0 + key0 + 8);
       const u32x2 b0 = *reinterpret_cast<const u32x2*>(v1 + key0);
       const u32x2 b1 = *reinterpret_cast<const u32x2*>(v1 + key0 + 8);
-      o0 = mfma16(pa, u32x4{a0[0], a0[1], a1[0], a1[1]}, o0);
-      o1 = mfma16(pa, u32x4{b0[0], b0[1], b1[0], b1[1]}, o1);
+      o0 = mfma16(u32x4{a0[0], a0[1], a1[0], a1[1]}, pb, o0);
+      o1 = mfma16(u32x4{b0[0], b0[1], b1[0], b1[1]}, pb, o1);
     }
   }
+  l += __shfl_xor(l, 32);  // both lane halves saw the same running max
+  const float inv_l = l > 0.f ? 1.0f / l : 0.f;
 
-  // O tile: register i holds query (i&3)+8(i>>2)+4h of the wave's 32, dims r and 32 + r
-  const int qw0 = qblk * kQPerWg + wave * kQPerWave;
-  uint16_t* out = ctx + ((size_t)seq * L) * (heads * kDh) + head * kDh;
+  // lane (r, h) holds query r, dims 8g + 4h + (0..3) (o0) and 32 + those (o1): 8-byte stores
+  if (q < L) {
+    uint16_t* dst = ctx + ((size_t)seq * L + q) * (heads * kDh) + head * kDh + 4 * h;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int qq = qw0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (qq < L) {
-      uint16_t* dst = out + (size_t)qq * (heads * kDh);
-      dst[r] = __builtin_bit_cast(uint16_t, (_Float16)o0[i]);
-      dst[32 + r] = __builtin_bit_cast(uint16_t, (_Float16)o1[i]);
+    for (int g = 0; g < 4; ++g) {
+      const u32x2 w0 = {pack_h2(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l),
+                        pack_h2(o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l)};
+      const u32x2 w1 = {pack_h2(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l),
+                        pack_h2(o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l)};
+      *reinterpret_cast<u32x2*>(dst + 8 * g) = w0;
+      *reinterpret_cast<u32x2*>(dst + 32 + 8 * g) = w1;
     }
   }
 }
@@ -281,7 +281,7 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
     ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_f16_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const float scale_log2 = scale * 1.4426950408889634f;
-  attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(256), lds,
+  attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(kThreads), lds,
                          stream>>>(qkv, mask, ctx, L, heads, scale_log2);
   ARMI_LAUNCHED("attention_f16_kernel");
   return ARMI_OK;

@@ -90,8 +90,8 @@ template <int DIM>
 __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
-    const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+    const uint16_t* __restrict__ queries, int nq, int q0, int q_stride,
+    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
   constexpr int KSTEPS = DIM / 16;
   constexpr int GROUPS = DIM / 64;
   static_assert(GROUPS % kDepth == 0, "prefetch ring must divide the tile");
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
     if (q >= nq) break;
-    const size_t base = (size_t)blockIdx.x * kQB + q;
+    const size_t base = (size_t)blockIdx.x * q_stride + q0 + q;
     if (lane < kKW) {
       cand_key[base * kKW + lane] = key[qq];
       cand_row[base * kKW + lane] = row[qq];
@@ -343,20 +343,31 @@ __global__ __launch_bounds__(64) void query_norms_kernel(const uint16_t* __restr
   }
 }
 
-// One workgroup per query of the pass: select, exact rescore, certify, emit.
+// Order-preserving map of a float to uint32 (larger float -> larger key; -inf lowest).
+__device__ __forceinline__ uint32_t ord_key(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float from_ord_key(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// One workgroup per query (all passes of the call): exact query norm, select, exact rescore,
+// certify, emit.
 //   Each scan workgroup's list is sorted, so its first entry is its maximum. The kc-th largest of
-//   those maxima, t0, is a lower bound of the pooled kc-th best, hence every entry of the pooled
-//   top-kc is >= t0: only entries >= t0 are kept (typically ~2*kc of n_wg*kKW) and sorted.
-//   Entries below t0 are discards and join the bound.
+//   those maxima, t0 (a radix select over the 256 maxima in one wave), is a lower bound of the
+//   pooled kc-th best, hence every entry of the pooled top-kc is >= t0: only entries >= t0 are
+//   kept (typically ~2*kc of n_wg*kKW) and sorted. Entries below t0 are discards and join the
+//   bound. Small sorts run inside one wave (shuffles, no barriers).
 constexpr int kSelCap = 1024;  // kept entries per query; overflow -> uncertified (exact fallback)
 constexpr int kRescoreBatch = 4;
 
 template <int DIM>
 __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
-    const float* __restrict__ cand_bound, int n_wg, int q_first, const uint16_t* __restrict__ rows,
+    const float* __restrict__ cand_bound, int n_wg, int q_stride, const uint16_t* __restrict__ rows,
     const double* __restrict__ inv_norm, const uint16_t* __restrict__ queries,
-    const double* __restrict__ inv_q, const double* __restrict__ qnorm_real, int k, int kc,
+    double* __restrict__ inv_q_out, double* __restrict__ qnorm_out, int k, int kc,
     int64_t ordinal_base, float* __restrict__ out_scores, int64_t* __restrict__ out_ids,
     double* __restrict__ out_rank, int32_t* __restrict__ out_count,
     uint32_t* __restrict__ out_flags) {
@@ -365,40 +376,71 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   int32_t* srow = reinterpret_cast<int32_t*>(smem + kSelCap * 4);            // [kSelCap]
   double* rkey = reinterpret_cast<double*>(smem + kSelCap * 8);              // [256]
   int64_t* rord = reinterpret_cast<int64_t*>(smem + kSelCap * 8 + 256 * 8);  // [256]
-  float* mx = reinterpret_cast<float*>(smem + kSelCap * 8 + 256 * 16);       // [256]
-  int32_t* mxr = reinterpret_cast<int32_t*>(smem + kSelCap * 8 + 256 * 20);  // [256]
-  float* red = reinterpret_cast<float*>(smem + kSelCap * 8 + 256 * 24);      // [8]
-  int* ctr = reinterpret_cast<int*>(smem + kSelCap * 8 + 256 * 24 + 32);     // [4]
+  float* red = reinterpret_cast<float*>(smem + kSelCap * 8 + 256 * 16);      // [16]
+  int* ctr = reinterpret_cast<int*>(smem + kSelCap * 8 + 256 * 16 + 64);     // [4]
 
-  const int ql = blockIdx.x;
-  const int qg = q_first + ql;
+  const int qg = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
 
-  // maxima + bound of the scan workgroups
-  float b = kNegInf;
-  for (int g = tid; g < 256; g += kMergeThreads) {
-    float m = kNegInf;
-    if (g < n_wg) {
-      m = cand_key[((size_t)g * kQB + ql) * kKW];
-      b = fmaxf(b, cand_bound[(size_t)g * kQB + ql]);
-    }
-    mx[g] = m;
-    mxr[g] = g;
-  }
-  if (tid == 0) ctr[0] = 0;
+  // exact query norm (every wave holds the fixed-point query for the rescore anyway)
+  int32_t qf[DIM / 64];
+  load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
+  int64_t n2q = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
-  if (lane == 0) red[wave] = b;
-  armi::lds_sort_approx_desc(mx, mxr, 256);
-  const float t0 = (n_wg >= kc) ? mx[kc - 1] : kNegInf;
+  for (int i = 0; i < DIM / 64; ++i) n2q += (int64_t)qf[i] * (int64_t)qf[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n2q += __shfl_xor(n2q, off);
+  const double inv_q = n2q > 0 ? 1.0 / sqrt((double)n2q) : 0.0;
+  const double qnorm_real = sqrt((double)n2q) * (1.0 / 16777216.0);
+  if (tid == 0) {
+    inv_q_out[qg] = inv_q;
+    qnorm_out[qg] = qnorm_real;
+  }
+
+  // wave 0: t0 = kc-th largest workgroup maximum, and the workgroup lists' own bounds
+  if (wave == 0) {
+    float b = kNegInf;
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int g = lane + 64 * i;
+      float m = kNegInf;
+      if (g < n_wg) {
+        m = cand_key[((size_t)g * q_stride + qg) * kKW];
+        b = fmaxf(b, cand_bound[(size_t)g * q_stride + qg]);
+      }
+      u[i] = ord_key(m);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+    float t0 = kNegInf;
+    if (n_wg >= kc) {
+      uint32_t prefix = 0;  // largest v with #{u >= v} >= kc, i.e. the kc-th largest key
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = prefix | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(u[i] >= cand));
+        if (cnt >= kc) prefix = cand;
+      }
+      t0 = from_ord_key(prefix);
+    }
+    if (lane == 0) {
+      red[8] = b;
+      red[9] = t0;
+      ctr[0] = 0;
+    }
+  }
+  __syncthreads();
+  const float t0 = red[9];
 
   // filter the pool
   float dmax = kNegInf;
   for (int e = tid; e < pool; e += kMergeThreads) {
-    const size_t src = ((size_t)(e / kKW) * kQB + ql) * kKW + (e % kKW);
+    const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
     const float kk = cand_key[src];
     if (kk == kNegInf) continue;
     if (kk >= t0) {
@@ -413,25 +455,35 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
-  if (lane == 0) red[4 + wave] = dmax;
+  if (lane == 0) red[wave] = dmax;
   __syncthreads();
   const int n_sel = ctr[0];
   const bool overflow = n_sel > kSelCap;
   const int n_keep = overflow ? kSelCap : n_sel;
-  const int n2 = armi::pow2_at_least(n_keep > kc ? n_keep : kc);
-  for (int e = n_keep + tid; e < n2; e += kMergeThreads) {
-    skey[e] = kNegInf;
-    srow[e] = 0x7fffffff;
+  int n2;
+  if (n_keep <= 64 && kc <= 64) {
+    if (wave == 0) {
+      float key = lane < n_keep ? skey[lane] : kNegInf;
+      int32_t row = lane < n_keep ? srow[lane] : 0x7fffffff;
+      armi::wave_sort_approx_desc(key, row);
+      skey[lane] = key;
+      srow[lane] = row;
+    }
+    __syncthreads();
+    n2 = 64;
+  } else {
+    n2 = armi::pow2_at_least(n_keep > kc ? n_keep : kc);
+    for (int e = n_keep + tid; e < n2; e += kMergeThreads) {
+      skey[e] = kNegInf;
+      srow[e] = 0x7fffffff;
+    }
+    armi::lds_sort_approx_desc(skey, srow, n2);
   }
-  armi::lds_sort_approx_desc(skey, srow, n2);
-  float bound = red[0];
-#pragma unroll
-  for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
-  if (n2 > kc) bound = fmaxf(bound, skey[kc]);
+  float bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  bound = fmaxf(bound, red[8]);
+  if (kc < n2) bound = fmaxf(bound, skey[kc]);
 
   // exact rescore of the kc best, kRescoreBatch rows in flight per wave
-  int32_t qf[DIM / 64];
-  load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
   const int per_wave = kc / 4;
   for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
     u32x2 raw[kRescoreBatch][DIM / 256];
@@ -460,20 +512,31 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
       }
     }
   }
-  armi::lds_sort_rank_desc(rkey, rord, kc);
-
-  if (tid == 0) {
-    int nv = 0;
-    while (nv < kc && rord[nv] != kNoOrd) ++nv;
-    ctr[1] = nv;
-  }
   __syncthreads();
-  const int n_valid = ctr[1];
+  if (kc <= 64) {
+    if (wave == 0) {
+      double key = lane < kc ? rkey[lane] : kNegInfD;
+      int64_t ord = lane < kc ? rord[lane] : kNoOrd;
+      armi::wave_sort_rank_desc(key, ord);
+      rkey[lane] = key;
+      rord[lane] = ord;
+    }
+    __syncthreads();
+  } else {
+    armi::lds_sort_rank_desc(rkey, rord, kc);
+  }
+
+  if (wave != 0) return;
+  // valid entries form a prefix of the sorted list
+  int n_valid = 0;
+  for (int c = lane; c < kc; c += 64) n_valid += rord[c] != kNoOrd;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
   bool certified;
   int n_out;
   if (n_valid >= k) {
     const double kth = rkey[k - 1] * (1.0 / 16777216.0);
-    const double delta = kDeltaSafety * (double)DIM * (1.0 / 16777216.0) * qnorm_real[qg];
+    const double delta = kDeltaSafety * (double)DIM * (1.0 / 16777216.0) * qnorm_real;
     certified = kth > (double)bound + delta;
     n_out = k;
   } else {
@@ -482,11 +545,10 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   }
   certified = certified && !overflow;
   if (certified) {
-    const double iq = inv_q[qg];
-    for (int c = tid; c < k; c += kMergeThreads) {
+    for (int c = lane; c < k; c += 64) {
       const size_t o = (size_t)qg * k + c;
       if (c < n_out) {
-        out_scores[o] = (float)(rkey[c] * iq);
+        out_scores[o] = (float)(rkey[c] * inv_q);
         out_ids[o] = rord[c];
         if (out_rank) out_rank[o] = rkey[c];
       } else {
@@ -496,13 +558,13 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
       }
     }
   }
-  if (tid == 0) {
+  if (lane == 0) {
     out_count[qg] = certified ? n_out : 0;
     out_flags[qg] = certified ? ARMI_FLAG_CERTIFIED : 0u;
   }
 }
 
-constexpr size_t kMergeLds = kSelCap * 8 + 256 * 24 + 64;
+constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16;
 
 // Exhaustive exact scan: grid (n_blocks, nq); block b scores rows [b*rpb, (b+1)*rpb) and keeps
 // its best `cap` (power of two) entries. Queries whose flag says CERTIFIED are skipped.
@@ -701,9 +763,9 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
   Workspace w{};
   if (fast) {
     const ScanPlan sp = plan_scan(idx, k);
-    w.cand_key = cv.take<float>((size_t)sp.n_wg * kQB * kKW);
-    w.cand_row = cv.take<int32_t>((size_t)sp.n_wg * kQB * kKW);
-    w.cand_bound = cv.take<float>((size_t)sp.n_wg * kQB);
+    w.cand_key = cv.take<float>((size_t)sp.n_wg * nq * kKW);
+    w.cand_row = cv.take<int32_t>((size_t)sp.n_wg * nq * kKW);
+    w.cand_bound = cv.take<float>((size_t)sp.n_wg * nq);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -788,8 +850,6 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                     const Workspace& w, hipStream_t stream) {
   const ScanPlan sp = plan_scan(idx, k);
   if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
-  query_norms_kernel<DIM><<<dim3(nq), dim3(64), 0, stream>>>(queries, nq, w.inv_q, w.qnorm);
-  ARMI_LAUNCHED("query_norms_kernel");
   for (int q0 = 0; q0 < nq; q0 += kQB) {
     const int nqp = std::min(kQB, nq - q0);
     std::pair<hipEvent_t, hipEvent_t> ev;
@@ -797,16 +857,18 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (timed < 0) return ARMI_ERR_HIP;
     dense_scan_kernel<DIM><<<dim3(sp.n_wg), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
         idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        queries + (size_t)q0 * DIM, nqp, w.cand_key, w.cand_row, w.cand_bound);
+        queries + (size_t)q0 * DIM, nqp, q0, nq, w.cand_key, w.cand_row, w.cand_bound);
     ARMI_LAUNCHED("dense_scan_kernel");
     if (timed == 1)
       if (int rc = timing_end(stream, ev)) return rc;
-    dense_merge_kernel<DIM><<<dim3(nqp), dim3(kMergeThreads), kMergeLds, stream>>>(
-        w.cand_key, w.cand_row, w.cand_bound, sp.n_wg, q0, idx->rows, idx->inv_norm, queries,
-        w.inv_q, w.qnorm, k, sp.kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
-        out_flags);
-    ARMI_LAUNCHED("dense_merge_kernel");
   }
+  // one merge for every query of the call: per-pass merges would serialise a latency-bound
+  // kernel per 64 queries (the multi-GPU step scans G*64 queries)
+  dense_merge_kernel<DIM><<<dim3(nq), dim3(kMergeThreads), kMergeLds, stream>>>(
+      w.cand_key, w.cand_row, w.cand_bound, sp.n_wg, nq, idx->rows, idx->inv_norm, queries,
+      w.inv_q, w.qnorm, k, sp.kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
+      out_flags);
+  ARMI_LAUNCHED("dense_merge_kernel");
   return launch_exact<DIM>(idx, queries, nq, k, row_mask, out_scores, out_ids, out_rank,
                            out_count, out_flags, 1, w, stream);
 }
