@@ -22,6 +22,7 @@
 //   3. dense_exact_scan + merge_lists: for queries that could not be certified, an exhaustive
 //      exact scan (workgroups of certified queries exit immediately).
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <mutex>
 #include <utility>
@@ -90,9 +91,22 @@ template <int DIM>
 __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
-    const uint16_t* __restrict__ queries, int nq, int q0, int q_stride,
+    int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
   constexpr int KSTEPS = DIM / 16;
+  // workgroup -> (64-query block qb, tile range rp). With several blocks, the blocks of one range
+  // get workgroup ids congruent mod 8, i.e. the same XCD: they stream the same rows at about the
+  // same time, so one block's HBM read is the others' L2 hit.
+  int qb = 0, rp = blockIdx.x;
+  if (n_qb > 1) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    qb = j % n_qb;
+    rp = (j / n_qb) * 8 + xcd;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int q0 = qb * kQB;
+  const int nq = min(kQB, q_stride - q0);
+  const uint16_t* __restrict__ queries = queries_all + (size_t)q0 * DIM;
   constexpr int GROUPS = DIM / 64;
   static_assert(GROUPS % kDepth == 0, "prefetch ring must divide the tile");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -117,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   const int lane = threadIdx.x & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int64_t t_begin = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
 
   float s0[kLaneList], s1[kLaneList];
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
     if (q >= nq) break;
-    const size_t base = (size_t)blockIdx.x * q_stride + q0 + q;
+    const size_t base = (size_t)rp * q_stride + q0 + q;
     if (lane < kKW) {
       cand_key[base * kKW + lane] = key[qq];
       cand_row[base * kKW + lane] = row[qq];
@@ -268,6 +282,250 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
+// step: G * 64 queries over a 1/G shard). A GEMM-tiled form of dense_scan_kernel: both operands
+// are staged through LDS in 64-wide k-steps, so each corpus row is read from HBM once per
+// 256-query block (once per call up to 256 queries) instead of once per 64 queries, and the
+// per-pass fixed cost (query image, workgroup merge, launch) is paid once.
+//   workgroup = (256-query block qb, contiguous row range rp); 8 waves as 4 (query groups of 64)
+//   x 2 (row groups of 64) over a 128-row tile; per wave 2 x 2 v_mfma_f32_32x32x16_f16 tiles
+//   (A = corpus rows, B = queries: the lane holds one query column, as in dense_scan_kernel, so
+//   the epilogue and the 4-deep lane lists are the same). LDS: double-buffered [rows][64+8] and
+//   [queries][64+8] fp16 images (144-B rows: conflict-free ds_read_b128), register-staged two
+//   k-steps ahead (two register sets), one barrier per k-step.
+//   The two query blocks of a 512-query call stream the same row range on one XCD (workgroup
+//   ids i and i+8), so the second read of each row tile can hit that XCD's L2.
+//   Output: per (rp, query) the 16 entries of the two row groups' lane lists, sorted: the
+//   candidate layout dense_merge_kernel reads (n_wg = number of row ranges).
+constexpr int kGQB = 256;           // queries per block
+constexpr int kGRT = 128;           // rows per tile iteration
+constexpr int kGStride = 64 + 8;    // LDS row stride (halves)
+constexpr int kGStage = (kGRT + kGQB) * kGStride;  // halves per LDS stage
+constexpr int kGThreads = kThreads;
+constexpr int kGChunks = (kGRT + kGQB) * 8 / kGThreads;  // 16-B staging chunks per thread
+
+template <int DIM>
+__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
+    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+  constexpr int KT = DIM / 64;  // k-steps per row tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][kGStage]
+
+  // workgroup -> (query block, row range); ids i and i+8 share a row range (same XCD)
+  const int id = blockIdx.x;
+  int qb, rp;
+  if (n_qb == 2) {
+    qb = (id >> 3) & 1;
+    rp = (id >> 4) * 8 + (id & 7);
+  } else {
+    qb = id % n_qb;
+    rp = id / n_qb;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int64_t lo = (int64_t)rp * rows_per_range;
+  const int64_t hi = min(lo + rows_per_range, n_rows);
+  const int q_base = qb * kGQB;
+
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int wq = wave & 3;   // query group: queries wq*64 + qt*32 + r
+  const int wr = wave >> 2;  // row group: rows wr*64 + rt*32 + ...
+
+  float s0[kLaneList], s1[kLaneList];
+  int32_t i0[kLaneList], i1[kLaneList];
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
+  }
+  float d0 = kNegInf, d1 = kNegInf;
+
+  auto load_stage = [&](int64_t st, u32x4 (&reg)[kGChunks]) {
+    const int64_t tn = st / KT;
+    const int t = (int)(st - tn * KT);
+    const int64_t row0 = lo + tn * kGRT;
+#pragma unroll
+    for (int c = 0; c < kGChunks; ++c) {
+      const int e = tid + c * kGThreads;
+      const int rr = e >> 3, ch = e & 7;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (rr < kGRT) {
+        int64_t row = row0 + rr;
+        row = row < n_rows ? row : n_rows - 1;
+        v = *reinterpret_cast<const u32x4*>(rows + row * DIM + 64 * t + 8 * ch);
+      } else {
+        const int q = q_base + rr - kGRT;
+        if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 64 * t + 8 * ch);
+      }
+      reg[c] = v;
+    }
+  };
+  auto store_stage = [&](int buf, const u32x4 (&reg)[kGChunks]) {
+    uint16_t* st = lds + buf * kGStage;
+#pragma unroll
+    for (int c = 0; c < kGChunks; ++c) {
+      const int e = tid + c * kGThreads;
+      const int rr = e >> 3, ch = e & 7;
+      *reinterpret_cast<u32x4*>(st + rr * kGStride + 8 * ch) = reg[c];
+    }
+  };
+
+  const int64_t n_tiles = (hi - lo + kGRT - 1) / kGRT;
+  const int64_t n_steps = n_tiles * KT;
+  f32x16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};  // [row tile][query tile]
+  // one k-step from LDS buffer buf; the row tile's epilogue after its last k-step
+  auto compute = [&](int64_t st, int buf) {
+    const int64_t tile = st / KT;
+    const int t = (int)(st - tile * KT);
+    const uint16_t* xs = lds + buf * kGStage + (wr * 64 + r) * kGStride + 8 * h;
+    const uint16_t* qs = lds + buf * kGStage + (kGRT + wq * 64 + r) * kGStride + 8 * h;
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      const u32x4 a0 = *reinterpret_cast<const u32x4*>(xs + 16 * sub);
+      const u32x4 a1 = *reinterpret_cast<const u32x4*>(xs + 32 * kGStride + 16 * sub);
+      const u32x4 b0 = *reinterpret_cast<const u32x4*>(qs + 16 * sub);
+      const u32x4 b1 = *reinterpret_cast<const u32x4*>(qs + 32 * kGStride + 16 * sub);
+      acc00 = mfma16(a0, b0, acc00);
+      acc01 = mfma16(a0, b1, acc01);
+      acc10 = mfma16(a1, b0, acc10);
+      acc11 = mfma16(a1, b1, acc11);
+    }
+    if (t != KT - 1) return;
+    // epilogue of the row tile: lane holds rows (j&3)+8(j>>2)+4h of each 32-row tile
+    const int64_t row0 = lo + tile * kGRT + wr * 64;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int64_t rb = row0 + rt * 32;
+      float inv[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t rr = rb + 8 * g + 4 * h + e;
+          inv[4 * g + e] = rr < hi ? inv_norm32[rr] : __builtin_nanf("");
+        }
+      }
+      uint32_t mbits = 0xffffffffu;
+      if (row_mask) mbits = rb < hi ? (uint32_t)(row_mask[rb >> 6] >> (rb & 63)) : 0u;
+      const f32x16& x0 = rt == 0 ? acc00 : acc10;
+      const f32x16& x1 = rt == 0 ? acc01 : acc11;
+      const int32_t rbase = (int32_t)rb + 4 * h;
+      float y0[16], y1[16];
+      float mx0 = kNegInf, mx1 = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int rt_in = (j & 3) + 8 * (j >> 2) + 4 * h;
+        const float a0 = x0[j] * inv[j];
+        const float a1 = x1[j] * inv[j];
+        const bool ok = ((mbits >> rt_in) & 1u) && (a0 == a0) && (a1 == a1);
+        y0[j] = ok ? a0 : kNegInf;
+        y1[j] = ok ? a1 : kNegInf;
+        mx0 = fmaxf(mx0, y0[j]);
+        mx1 = fmaxf(mx1, y1[j]);
+      }
+      if (__any(mx0 > s0[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          topm_insert<kLaneList>(y0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+      } else {
+        d0 = fmaxf(d0, mx0);
+      }
+      if (__any(mx1 > s1[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          topm_insert<kLaneList>(y1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+      } else {
+        d1 = fmaxf(d1, mx1);
+      }
+    }
+    acc00 = f32x16{}; acc01 = f32x16{}; acc10 = f32x16{}; acc11 = f32x16{};
+  };
+  if (n_steps > 0) {
+    // k-step s lives in LDS buffer s & 1; its registers were loaded two k-steps earlier (two
+    // register sets), so a global load has two k-steps of MFMA work to land
+    u32x4 regA[kGChunks], regB[kGChunks];
+    load_stage(0, regA);
+    store_stage(0, regA);
+    if (n_steps > 1) load_stage(1, regB);
+    __syncthreads();
+    for (int64_t st = 0; st < n_steps; st += 2) {
+      if (st + 2 < n_steps) load_stage(st + 2, regA);
+      compute(st, 0);
+      if (st + 1 < n_steps) store_stage(1, regB);
+      __syncthreads();
+      if (st + 1 >= n_steps) break;
+      if (st + 3 < n_steps) load_stage(st + 3, regB);
+      compute(st + 1, 1);
+      if (st + 2 < n_steps) store_stage(0, regA);
+      __syncthreads();
+    }
+  }
+
+  // workgroup lists: per query the 16 entries of (row group, lane half, 4), sorted
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                          // [256][16]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);      // [256][16]
+  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);         // [256][4]
+  {
+    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
+    const int slot = (wr * 2 + h) * kLaneList;
+#pragma unroll
+    for (int j = 0; j < kLaneList; ++j) {
+      lkey[qa * 16 + slot + j] = s0[j];
+      lrow[qa * 16 + slot + j] = i0[j];
+      lkey[qc * 16 + slot + j] = s1[j];
+      lrow[qc * 16 + slot + j] = i1[j];
+    }
+    ldisc[qa * 4 + wr * 2 + h] = d0;
+    ldisc[qc * 4 + wr * 2 + h] = d1;
+  }
+  __syncthreads();
+  // each wave sorts 4 queries (16 lanes each) per round, 8 rounds
+  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
+    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
+    float key = lkey[ql * 16 + (lane & 15)];
+    int32_t row = lrow[ql * 16 + (lane & 15)];
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const float ok = __shfl_xor(key, stride);
+        const int32_t orow = __shfl_xor(row, stride);
+        const bool lower = (lane & stride) == 0;
+        const bool desc = (lane & size) == 0;
+        const bool other_better = armi::approx_better(ok, orow, key, row);
+        const bool take_other = (lower == desc) ? other_better : !other_better;
+        if (take_other) { key = ok; row = orow; }
+      }
+    }
+    // 16-lane segments with (lane & 16) == 0 end descending, the others ascending
+    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
+    const int qg = q_base + ql;
+    if (qg < nq) {
+      const size_t base = (size_t)rp * nq + qg;
+      cand_key[base * kKW + rank] = key;
+      cand_row[base * kKW + rank] = row;
+      if (rank == 0) {
+        const float* dd = ldisc + ql * 4;
+        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
+      }
+    }
+  }
+}
+
+template <int DIM>
+constexpr size_t gemm_scan_lds_bytes() {
+  constexpr size_t stages = (size_t)2 * kGStage * 2;
+  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
+  return stages > lists ? stages : lists;
+}
+
 
 // This lane's DIM/64 contiguous fp16 elements of a vector, as raw 8-byte words.
 template <int DIM>
@@ -711,20 +969,63 @@ __global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
 size_t merge_lds_bytes(int pool2) { return (size_t)pool2 * 24 + 16; }
 
 struct ScanPlan {
-  int n_wg = 0;
+  int n_qb = 1;   // 64-query blocks of the call
+  int grid = 0;   // workgroups launched
+  int n_wg = 0;   // tile ranges (candidate lists per query)
   int tiles_per_wg = 0;
   int pool2 = 0;
   int kc = 0;
 };
 
-ScanPlan plan_scan(const armi_index* idx, int k) {
+ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
   ScanPlan p;
   const int64_t tiles = std::max<int64_t>(idx->n_tiles, 1);
-  const int64_t wgs = std::min<int64_t>(std::min(std::max(idx->num_cus, 1), 256), tiles);
+  const int cus = std::min(std::max(idx->num_cus, 1), 256);
+  p.n_qb = std::max(1, (nq + kQB - 1) / kQB);
+  int64_t want = cus;
+  if (p.n_qb > 1) want = std::max<int64_t>(8, ((cus + p.n_qb - 1) / p.n_qb + 7) / 8 * 8);
+  const int64_t wgs = std::min<int64_t>(want, tiles);
   p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
   p.n_wg = (int)((tiles + p.tiles_per_wg - 1) / p.tiles_per_wg);
+  p.grid = p.n_qb == 1 ? p.n_wg : p.n_qb * 8 * ((p.n_wg + 7) / 8);
   p.pool2 = armi::pow2_at_least(p.n_wg * kKW);
   p.kc = std::max(4, std::min(armi::pow2_at_least(k + 8), 256));
+  return p;
+}
+
+// Multi-block calls (more than kQB queries): up to 2 blocks the XCD-grouped dense_scan_kernel
+// (HBM-bound, rows shared through L2), beyond that the LDS-tiled dense_gemm_scan_kernel (rows
+// read once per 256 queries). Measured per-GPU call times, 1M rows / G with G*64 queries:
+// G=2 366 vs 497 us, G=4 326 vs 272-318 us, G=8 308 vs 251-269 us (grouped vs tiled).
+// ARMI_DENSE_SCAN=grouped|tiled forces one of them (A/B measurements).
+bool use_gemm_scan(int nq) {
+  static const int force = [] {
+    const char* e = getenv("ARMI_DENSE_SCAN");
+    if (!e) return 0;
+    return e[0] == 't' ? 1 : (e[0] == 'g' ? 2 : 0);
+  }();
+  if (nq <= kQB) return false;
+  if (force) return force == 1;
+  return nq > 2 * kQB;
+}
+
+struct GemmPlan {
+  int n_qb = 0;
+  int n_ranges = 0;
+  int64_t rows_per_range = 0;
+  int grid = 0;
+};
+
+GemmPlan plan_gemm(const armi_index* idx, int nq) {
+  GemmPlan p;
+  p.n_qb = (nq + kGQB - 1) / kGQB;
+  const int cus = std::min(std::max(idx->num_cus, 1), 256);
+  const int64_t rows = std::max<int64_t>(idx->n_rows, 1);
+  int want = std::max(1, (cus + p.n_qb - 1) / p.n_qb);
+  want = (int)std::min<int64_t>(want, (rows + kGRT - 1) / kGRT);  // >= one row tile per range
+  p.rows_per_range = ((rows + want - 1) / want + 31) / 32 * 32;
+  p.n_ranges = (int)((rows + p.rows_per_range - 1) / p.rows_per_range);
+  p.grid = p.n_qb == 2 ? 16 * ((p.n_ranges + 7) / 8) : p.n_qb * p.n_ranges;
   return p;
 }
 
@@ -762,10 +1063,10 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
   armi::Carver cv(base);
   Workspace w{};
   if (fast) {
-    const ScanPlan sp = plan_scan(idx, k);
-    w.cand_key = cv.take<float>((size_t)sp.n_wg * nq * kKW);
-    w.cand_row = cv.take<int32_t>((size_t)sp.n_wg * nq * kKW);
-    w.cand_bound = cv.take<float>((size_t)sp.n_wg * nq);
+    const int n_wg = use_gemm_scan(nq) ? plan_gemm(idx, nq).n_ranges : plan_scan(idx, k, nq).n_wg;
+    w.cand_key = cv.take<float>((size_t)n_wg * nq * kKW);
+    w.cand_row = cv.take<int32_t>((size_t)n_wg * nq * kKW);
+    w.cand_bound = cv.take<float>((size_t)n_wg * nq);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -848,16 +1149,30 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
                     const Workspace& w, hipStream_t stream) {
-  const ScanPlan sp = plan_scan(idx, k);
-  if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
-  for (int q0 = 0; q0 < nq; q0 += kQB) {
-    const int nqp = std::min(kQB, nq - q0);
+  const ScanPlan sp = plan_scan(idx, k, nq);
+  int n_wg = sp.n_wg;
+  if (use_gemm_scan(nq)) {
+    const GemmPlan gp = plan_gemm(idx, nq);
+    n_wg = gp.n_ranges;
+    if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
     std::pair<hipEvent_t, hipEvent_t> ev;
     const int timed = timing_begin(stream, &ev);
     if (timed < 0) return ARMI_ERR_HIP;
-    dense_scan_kernel<DIM><<<dim3(sp.n_wg), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
+    dense_gemm_scan_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads), gemm_scan_lds_bytes<DIM>(),
+                                  stream>>>(idx->rows, idx->inv_norm32, row_mask, idx->n_rows,
+                                            gp.rows_per_range, gp.n_ranges, gp.n_qb, queries, nq,
+                                            w.cand_key, w.cand_row, w.cand_bound);
+    ARMI_LAUNCHED("dense_gemm_scan_kernel");
+    if (timed == 1)
+      if (int rc = timing_end(stream, ev)) return rc;
+  } else {
+    if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    const int timed = timing_begin(stream, &ev);
+    if (timed < 0) return ARMI_ERR_HIP;
+    dense_scan_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
         idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        queries + (size_t)q0 * DIM, nqp, q0, nq, w.cand_key, w.cand_row, w.cand_bound);
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
     ARMI_LAUNCHED("dense_scan_kernel");
     if (timed == 1)
       if (int rc = timing_end(stream, ev)) return rc;
@@ -865,7 +1180,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kMergeThreads), kMergeLds, stream>>>(
-      w.cand_key, w.cand_row, w.cand_bound, sp.n_wg, nq, idx->rows, idx->inv_norm, queries,
+      w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, sp.kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
       out_flags);
   ARMI_LAUNCHED("dense_merge_kernel");

@@ -54,7 +54,9 @@ def test_norms_bitwise(gpu, oracle_mod, dim):
 
 @pytest.mark.parametrize("n,dim,b,k", [
     (1000, 256, 8, 5), (4099, 1024, 16, 5), (20000, 1024, 64, 40), (3001, 512, 70, 20),
-    (50, 768, 3, 5), (5, 256, 4, 8), (1, 1024, 2, 5)])
+    (50, 768, 3, 5), (5, 256, 4, 8), (1, 1024, 2, 5),
+    # > 64 queries: the GEMM-tiled multi-block scan (one / two / three 256-query blocks)
+    (20000, 1024, 300, 5), (5000, 256, 130, 40), (100, 768, 513, 5), (33, 1024, 600, 7)])
 def test_dense_topk_matches_oracle(gpu, oracle_mod, n, dim, b, k):
     rows = oracle_mod.unit_fp16(n, dim, seed=10 + n)
     qs = oracle_mod.unit_fp16(b, dim, seed=11 + n)
@@ -75,6 +77,25 @@ def test_fast_path_certifies(gpu, oracle_mod):
         assert (got["flags"] == 1).all(), got["flags"]
         ref = oracle_mod.dense_topk(rows, qs, k)
         _assert_same(got, ref, k)
+
+
+def test_multi_block_scan_certifies_and_masks(gpu, oracle_mod):
+    """512 queries (the all-gathered batch of an 8-GPU step) over one shard: the multi-block
+    scan must certify by itself, honour a row mask and equal the oracle."""
+    n = 20000
+    rows = oracle_mod.unit_fp16(n, 1024, seed=17)
+    qs = oracle_mod.unit_fp16(512, 1024, seed=18)
+    idx = _index(rows, gpu, base=123)
+    got = _run(idx, qs, 5, gpu)
+    assert (got["flags"] == 1).all(), np.unique(got["flags"], return_counts=True)
+    _assert_same(got, oracle_mod.dense_topk(rows, qs, 5, ordinal_base=123), 5)
+    rng = np.random.default_rng(3)
+    mask = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in np.nonzero(rng.random(n) < 0.4)[0]:
+        mask[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    got = _run(idx, qs[:200], 20, gpu, mask=mask)
+    _assert_same(got, oracle_mod.dense_topk(rows, qs[:200], 20, row_mask=mask,
+                                            ordinal_base=123), 20)
 
 
 def test_exact_entry_point(gpu, oracle_mod):
