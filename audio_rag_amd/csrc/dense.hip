@@ -112,6 +112,29 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
 
+  const int wave = armi::wave_id();
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
+  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
+  int64_t t = t_begin + wave;
+  auto row_ptr = [&](int64_t tile) -> const u32x4* {
+    int64_t rr = tile * TILE_ROWS + r;
+    rr = rr < n_rows ? rr : n_rows - 1;
+    return reinterpret_cast<const u32x4*>(rows + rr * DIM) + 4 * h;
+  };
+  // the first tile's loads go out before the query image is staged: the HBM latency of the
+  // first groups overlaps the image fill
+  const u32x4* cur = row_ptr(t < t_end ? t : t_begin);
+  u32x4 buf[kDepth][4];
+  if (t < t_end) {
+#pragma unroll
+    for (int g = 0; g < kDepth; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 8 * g + i);
+  }
+
   // 1. Query fragment image. K-step s, lane half h takes the 8 elements of chunk
   //    c = 8*(s/4) + 4*h + s%4, matching the corpus chunk that lane half loads (any k order
   //    is valid for a dot product as long as A and B agree).
@@ -127,13 +150,6 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   }
   __syncthreads();
 
-  const int wave = armi::wave_id();
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
-  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
-
   float s0[kLaneList], s1[kLaneList];
   int32_t i0[kLaneList], i1[kLaneList];
 #pragma unroll
@@ -142,20 +158,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
   }
   float d0 = kNegInf, d1 = kNegInf;
 
-  int64_t t = t_begin + wave;
   if (t < t_end) {
-    auto row_ptr = [&](int64_t tile) -> const u32x4* {
-      int64_t rr = tile * TILE_ROWS + r;
-      rr = rr < n_rows ? rr : n_rows - 1;
-      return reinterpret_cast<const u32x4*>(rows + rr * DIM) + 4 * h;
-    };
-    const u32x4* cur = row_ptr(t);
-    u32x4 buf[kDepth][4];
-#pragma unroll
-    for (int g = 0; g < kDepth; ++g)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 8 * g + i);
-
     for (; t < t_end; t += kWaves) {
       const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
       const u32x4* nxt = row_ptr(tn);

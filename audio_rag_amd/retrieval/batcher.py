@@ -1,0 +1,171 @@
+"""Streaming query front end: concurrent callers' searches coalesced into device batches.
+
+The reference answers one query per request: the REST layer calls pipeline.query() once per
+request in each of its 4 uvicorn processes (src/audio_rag/api/v1/query.py:90-115,
+Dockerfile.api:85-86), so Qdrant sees batch-1 searches. On the MI355X a batch-1 scan costs the
+same HBM pass as a batch-64 scan, so a server must batch across requests. QueryBatcher is that
+layer (BASELINE config 5 "streaming query at fixed QPS"): callers
+submit single queries from any thread and get a Future of the reference-shaped
+list[RetrievalResult]; one worker thread drains the queue into batches of up to max_batch
+queries, waiting at most max_wait_ms after the first arrival, and runs one
+MI355XRetriever.search_batch per (filter, has-sparse) group. Per-query semantics are those of
+MI355XRetriever.search (qdrant.py:227-352); only the grouping is new.
+"""
+
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from audio_rag_amd.core.base import EmbeddingResult, RetrievalResult
+from audio_rag_amd.core.exceptions import RetrievalError
+from audio_rag_amd.retrieval.mi355x import MI355XRetriever, QueryBatch, sparse_arrays
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class _Request:
+    dense: np.ndarray                       # float16 [dim]
+    sparse: tuple[np.ndarray, np.ndarray] | None
+    filter_metadata: dict | None
+    future: Future
+    t_submit: float = field(default_factory=time.perf_counter)
+
+
+def _filter_key(f: dict | None):
+    return None if not f else tuple(sorted((k, repr(v)) for k, v in f.items()))
+
+
+class QueryBatcher:
+    def __init__(self, retriever: MI355XRetriever, collection_name: str | None = None,
+                 top_k: int | None = None, search_type: str | None = None, max_batch: int = 64,
+                 max_wait_ms: float = 2.0):
+        if max_batch < 1:
+            raise ValueError("max_batch must be >= 1")
+        self.retriever = retriever
+        self.collection_name = collection_name
+        self.top_k = top_k
+        self.search_type = search_type
+        self.max_batch = max_batch
+        self.max_wait = max_wait_ms * 1e-3
+        self._q: queue.Queue[_Request | None] = queue.Queue()
+        self._closed = False
+        self.batches = 0
+        self.queries = 0
+        self._worker = threading.Thread(target=self._run, name="armi-query-batcher", daemon=True)
+        self._worker.start()
+
+    # ------------------------------------------------------------------------ callers
+
+    def submit_arrays(self, dense: np.ndarray, sparse: tuple[np.ndarray, np.ndarray] | None = None,
+                      filter_metadata: dict | None = None) -> Future:
+        """dense: [dim] query vector (cast to fp16 as the store holds it); sparse: (indices,
+        values) or None. Returns a Future of list[RetrievalResult]."""
+        if self._closed:
+            raise RetrievalError("QueryBatcher is closed")
+        fut: Future = Future()
+        d = np.ascontiguousarray(dense, dtype=np.float16).reshape(-1)
+        self._q.put(_Request(d, sparse, filter_metadata, fut))
+        return fut
+
+    def submit(self, query: EmbeddingResult, filter_metadata: dict | None = None) -> Future:
+        """EmbeddingResult (BGEM3Embedder.embed_query output) -> Future[list[RetrievalResult]]."""
+        return self.submit_arrays(np.asarray(query.dense, dtype=np.float32),
+                                  sparse_arrays(query.sparse), filter_metadata)
+
+    def search(self, query: EmbeddingResult, filter_metadata: dict | None = None,
+               timeout: float | None = None) -> list[RetrievalResult]:
+        return self.submit(query, filter_metadata).result(timeout)
+
+    def close(self) -> None:
+        if not self._closed:
+            self._closed = True
+            self._q.put(None)
+            self._worker.join()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ------------------------------------------------------------------------- worker
+
+    def _collect(self, first: _Request) -> tuple[list[_Request], bool]:
+        batch = [first]
+        deadline = first.t_submit + self.max_wait
+        stop = False
+        while len(batch) < self.max_batch:
+            wait = deadline - time.perf_counter()
+            try:
+                item = self._q.get(timeout=max(wait, 0.0)) if wait > 0 else self._q.get_nowait()
+            except queue.Empty:
+                break
+            if item is None:
+                stop = True
+                break
+            batch.append(item)
+        return batch, stop
+
+    def _run(self) -> None:
+        if self.retriever.device.type == "cuda":
+            torch.cuda.set_device(self.retriever.device)
+        while True:
+            first = self._q.get()
+            if first is None:
+                break
+            batch, stop = self._collect(first)
+            groups: dict = {}
+            for r in batch:
+                groups.setdefault((_filter_key(r.filter_metadata), r.sparse is not None), []).append(r)
+            for reqs in groups.values():
+                self._serve(reqs)
+            if stop:
+                break
+        # fail whatever is left (closed while callers were still submitting)
+        while True:
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if item is not None and not item.future.done():
+                item.future.set_exception(RetrievalError("QueryBatcher closed"))
+
+    def _serve(self, reqs: list[_Request]) -> None:
+        try:
+            r = self.retriever
+            dev = r.device
+            dense = torch.from_numpy(np.stack([q.dense for q in reqs])).to(dev, non_blocking=True)
+            qb = QueryBatch(dense=dense)
+            if reqs[0].sparse is not None:
+                indptr = np.zeros(len(reqs) + 1, dtype=np.int32)
+                np.cumsum([len(q.sparse[0]) for q in reqs], out=indptr[1:])
+                idx = np.concatenate([q.sparse[0] for q in reqs]).astype(np.int32)
+                val = np.concatenate([q.sparse[1] for q in reqs]).astype(np.float32)
+                t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                qb = QueryBatch(dense=dense, sparse_indptr=t(indptr), sparse_indices=t(idx),
+                                sparse_values=t(val))
+            resolved = r._resolve_collection(self.collection_name)
+            out, mode = r.search_batch(qb, self.top_k, resolved, reqs[0].filter_metadata,
+                                       self.search_type)
+            thr = None
+            if mode == "legacy_dense" and r.config.score_threshold > 0:
+                thr = r.config.score_threshold
+            results = r.materialize_batch(out, mode, resolved, thr)
+            for q, res in zip(reqs, results):
+                q.future.set_result(res)
+            self.batches += 1
+            self.queries += len(reqs)
+        except Exception as e:  # every caller of the batch sees the failure, as search() raises
+            err = e if isinstance(e, RetrievalError) else RetrievalError(f"Search failed: {e}")
+            for q in reqs:
+                if not q.future.done():
+                    q.future.set_exception(err)

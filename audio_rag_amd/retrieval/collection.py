@@ -51,6 +51,7 @@ class ChunkCollection:
     _built_rows: int = -1
     _mask_cache: dict = field(default_factory=dict)
     _lock: threading.Lock = field(default_factory=threading.Lock)
+    _frozen: bool = False
 
     @property
     def count(self) -> int:
@@ -66,6 +67,8 @@ class ChunkCollection:
             raise ValueError(f"dense vectors must be float16 [n, {self.dim}]")
         if not (len(sparse) == len(payloads) == dense.shape[0]):
             raise ValueError("dense / sparse / payload counts differ")
+        if self._frozen:
+            raise ValueError(f"collection {self.name} is read-only (built from device indexes)")
         bits = dense.view(np.uint16)
         if ((bits >> 10) & 31).max(initial=0) > 15:
             raise ValueError("dense components must be finite with |x| < 2 (unit embeddings)")
@@ -136,6 +139,46 @@ class ChunkCollection:
         mask = torch.from_numpy(words.view(np.int64)).to(self.device)
         self._mask_cache[key] = (n, mask)
         return mask
+
+    @classmethod
+    def from_indexes(cls, name: str, dense: DenseIndex, payloads: list[dict],
+                     sparse: SparseIndex | None = None) -> "ChunkCollection":
+        """A read-only collection over device indexes built elsewhere (a loaded store shard, a
+        synthetic benchmark corpus). Nothing is staged on the host, so it cannot be saved or
+        extended with upsert()."""
+        if len(payloads) != dense.n_rows:
+            raise ValueError("one payload per row is required")
+        coll = cls(name, dense.dim, sparse is not None, dense.device)
+        coll.payloads = payloads
+        coll._dense, coll._sparse = dense, sparse
+        coll._built_rows = len(payloads)
+        coll._frozen = True
+        return coll
+
+    # ------------------------------------------------------------------------ persistence
+
+    def save(self, path) -> None:
+        """Writes the collection as an on-disk chunk store (retrieval/store.py)."""
+        from audio_rag_amd.retrieval.store import save_arrays
+
+        if self._frozen:
+            raise ValueError(f"collection {self.name} has no host copy (built from device indexes)")
+        with self._lock:
+            rows = (np.concatenate(self.dense_rows) if self.dense_rows
+                    else np.zeros((0, self.dim), dtype=np.float16))
+            save_arrays(path, self.name, rows, list(self.sparse_rows), list(self.payloads),
+                        self.hybrid)
+
+    @classmethod
+    def load(cls, path, device: torch.device, name: str | None = None) -> "ChunkCollection":
+        """A collection holding every point of an on-disk chunk store, in ordinal order."""
+        from audio_rag_amd.retrieval.store import load_shard
+
+        sh = load_shard(path)
+        coll = cls(name or sh.name, sh.dim, sh.hybrid, device)
+        coll.upsert(np.ascontiguousarray(sh.dense, dtype=np.float16), sh.sparse_rows(),
+                    sh.payloads)
+        return coll
 
     def close(self) -> None:
         for ix in (self._dense, self._sparse):

@@ -165,6 +165,43 @@ class MI355XRetriever(BaseRetriever):
             sparse = [None] * len(payloads)
         coll.upsert(np.ascontiguousarray(dense, dtype=np.float16), sparse, payloads)
 
+    # ---------------------------------------------------------------------- persistence
+
+    def save_collection(self, path, collection_name: str | None = None) -> None:
+        """Persists a collection as an on-disk chunk store (retrieval/store.py), the durable
+        form of the Qdrant collection qdrant.py:59-225 maintains."""
+        resolved = self._resolve_collection(collection_name)
+        if resolved not in self._collections:
+            raise RetrievalError(f"Collection '{resolved}' does not exist")
+        try:
+            self._collections[resolved].save(path)
+        except Exception as e:
+            raise RetrievalError(f"Failed to save collection '{resolved}': {e}")
+
+    def attach_collection(self, coll: ChunkCollection) -> None:
+        """Registers a collection built elsewhere (ChunkCollection.from_indexes)."""
+        old = self._collections.pop(coll.name, None)
+        if old is not None and old is not coll:
+            old.close()
+        self._collections[coll.name] = coll
+
+    def load_collection(self, path, collection_name: str | None = None) -> str:
+        """Loads an on-disk chunk store as a collection (replacing one of the same name);
+        returns the collection name."""
+        try:
+            from audio_rag_amd.retrieval.store import read_meta
+
+            resolved = collection_name or read_meta(path)["name"]
+            coll = ChunkCollection.load(path, self.device, resolved)
+        except Exception as e:
+            raise RetrievalError(f"Failed to load chunk store '{path}': {e}")
+        old = self._collections.pop(resolved, None)
+        if old is not None:
+            old.close()
+        self._collections[resolved] = coll
+        logger.info(f"Loaded collection {resolved}: {coll.count} points (hybrid={coll.hybrid})")
+        return resolved
+
     # --------------------------------------------------------------------------- search
 
     def _mode(self, coll: ChunkCollection, search_type: str, has_sparse: bool) -> str:
@@ -231,6 +268,28 @@ class MI355XRetriever(BaseRetriever):
                                metadata=p.get("metadata"))
             results.append(RetrievalResult(chunk=chunk, score=float(score), source=resolved))
         return results
+
+    def materialize_batch(self, out: TopK, mode: str, resolved: str,
+                          threshold: float | None = None) -> list[list[RetrievalResult]]:
+        """Every row of a device TopK -> RetrievalResult lists, with one device-to-host copy per
+        tensor for the whole batch (materialize() copies per row)."""
+        coll = self._collections[resolved]
+        counts = out.count.cpu().tolist()
+        ids = out.ids.cpu().tolist()
+        scores = (out.rank if mode == "hybrid" else out.scores).cpu().tolist()
+        batch = []
+        for c, row_ids, row_sc in zip(counts, ids, scores):
+            results = []
+            for pid, score in zip(row_ids[:c], row_sc[:c]):
+                if threshold is not None and score < threshold:
+                    continue
+                p = coll.payloads[pid]
+                chunk = AudioChunk(text=p.get("text", ""), start=p.get("start", 0.0),
+                                   end=p.get("end", 0.0), speaker=p.get("speaker"),
+                                   metadata=p.get("metadata"))
+                results.append(RetrievalResult(chunk=chunk, score=float(score), source=resolved))
+            batch.append(results)
+        return batch
 
     @timed
     def search(self, query_embedding: EmbeddingResult, top_k: int | None = None,
