@@ -238,6 +238,105 @@ __global__ __launch_bounds__(256) void layernorm_residual_f16_kernel(
   }
 }
 
+// Vectorised form for width = 256 * CPL: lane owns elements 4c .. 4c+3 of chunks c = lane + 64 i,
+// so every access is an 8-byte (fp16) or 16-byte (fp32) vector; same arithmetic as above.
+template <int CPL>
+__global__ __launch_bounds__(256) void layernorm_residual_f16_vec_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ res, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ out, uint16_t* __restrict__ out16,
+    int64_t n_rows, float eps) {
+  constexpr int W = 256 * CPL;
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  float v[CPL][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const u32x2 xv = *reinterpret_cast<const u32x2*>(x + row * W + 4 * c);
+    const half2v h0 = __builtin_bit_cast(half2v, (uint32_t)xv[0]);
+    const half2v h1 = __builtin_bit_cast(half2v, (uint32_t)xv[1]);
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) rv = *reinterpret_cast<const float4*>(res + row * W + 4 * c);
+    v[i][0] = (float)h0[0] + rv.x;
+    v[i][1] = (float)h0[1] + rv.y;
+    v[i][2] = (float)h1[0] + rv.z;
+    v[i][3] = (float)h1[1] + rv.w;
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = wave_sum(s) / (float)W;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      ss += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)W + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const float4 g = *reinterpret_cast<const float4*>(gamma + 4 * c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + 4 * c);
+    const float4 y = make_float4((v[i][0] - mean) * rstd * g.x + b.x, (v[i][1] - mean) * rstd * g.y + b.y,
+                                 (v[i][2] - mean) * rstd * g.z + b.z, (v[i][3] - mean) * rstd * g.w + b.w);
+    *reinterpret_cast<float4*>(out + row * W + 4 * c) = y;
+    if (out16)
+      *reinterpret_cast<u32x2*>(out16 + row * W + 4 * c) = u32x2{pack_h2(y.x, y.y), pack_h2(y.z, y.w)};
+  }
+}
+
+// out16 = LayerNorm(x16 + res16): the all-fp16 residual stream variant (statistics in fp32),
+// width = 256 * CPL; 6 bytes of HBM traffic per element instead of 12.
+template <int CPL>
+__global__ __launch_bounds__(256) void add_layernorm_f16_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const float* __restrict__ gamma, const float* __restrict__ beta, uint16_t* __restrict__ out16,
+    int64_t n_rows, float eps) {
+  constexpr int W = 256 * CPL;
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  float v[CPL][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const u32x2 xv = *reinterpret_cast<const u32x2*>(x + row * W + 4 * c);
+    const u32x2 rv = *reinterpret_cast<const u32x2*>(res + row * W + 4 * c);
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const uint32_t xw = xv[w], rw = rv[w];
+      const half2v hx = __builtin_bit_cast(half2v, xw);
+      const half2v hr = __builtin_bit_cast(half2v, rw);
+      v[i][2 * w] = (float)hx[0] + (float)hr[0];
+      v[i][2 * w + 1] = (float)hx[1] + (float)hr[1];
+    }
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = wave_sum(s) / (float)W;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      ss += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)W + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const float4 g = *reinterpret_cast<const float4*>(gamma + 4 * c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + 4 * c);
+    *reinterpret_cast<u32x2*>(out16 + row * W + 4 * c) =
+        u32x2{pack_h2((v[i][0] - mean) * rstd * g.x + b.x, (v[i][1] - mean) * rstd * g.y + b.y),
+              pack_h2((v[i][2] - mean) * rstd * g.z + b.z, (v[i][3] - mean) * rstd * g.w + b.w)};
+  }
+}
+
 // in-place exact-erf GELU of fp16 x (+ fp32 bias[col], nullable), computed in fp32
 __global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
                                                        const float* __restrict__ bias, int64_t n,
@@ -294,9 +393,38 @@ int armi_enc_layernorm_residual_f16(const uint16_t* x, const float* res, const f
                "layernorm_f16: width must be in [1, 1024]");
   if (n_rows <= 0) return ARMI_OK;
   ARMI_REQUIRE(x && gamma && beta && out, "layernorm_f16: null pointer argument");
-  layernorm_residual_f16_kernel<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, stream>>>(
-      x, res, gamma, beta, out, out16, n_rows, width, eps);
+  const dim3 grid((unsigned)((n_rows + 3) / 4));
+  switch (width) {  // the XLM-R widths take the vectorised kernel
+    case 768:
+      layernorm_residual_f16_vec_kernel<3><<<grid, dim3(256), 0, stream>>>(x, res, gamma, beta,
+                                                                          out, out16, n_rows, eps);
+      break;
+    case 1024:
+      layernorm_residual_f16_vec_kernel<4><<<grid, dim3(256), 0, stream>>>(x, res, gamma, beta,
+                                                                          out, out16, n_rows, eps);
+      break;
+    default:
+      layernorm_residual_f16_kernel<<<grid, dim3(256), 0, stream>>>(x, res, gamma, beta, out,
+                                                                    out16, n_rows, width, eps);
+  }
   ARMI_LAUNCHED("layernorm_residual_f16_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_add_layernorm_f16(const uint16_t* x, const uint16_t* res, const float* gamma,
+                               const float* beta, uint16_t* out16, int64_t n_rows, int width,
+                               float eps, hipStream_t stream) {
+  ARMI_REQUIRE(width == 768 || width == 1024, "add_layernorm_f16: width must be 768 or 1024");
+  if (n_rows <= 0) return ARMI_OK;
+  ARMI_REQUIRE(x && res && gamma && beta && out16, "add_layernorm_f16: null pointer argument");
+  const dim3 grid((unsigned)((n_rows + 3) / 4));
+  if (width == 768)
+    add_layernorm_f16_kernel<3><<<grid, dim3(256), 0, stream>>>(x, res, gamma, beta, out16, n_rows,
+                                                                eps);
+  else
+    add_layernorm_f16_kernel<4><<<grid, dim3(256), 0, stream>>>(x, res, gamma, beta, out16, n_rows,
+                                                                eps);
+  ARMI_LAUNCHED("add_layernorm_f16_kernel");
   return ARMI_OK;
 }
 

@@ -5,7 +5,10 @@ through torch.
 Restates what sentence-transformers' CrossEncoder.predict runs for BGEReranker
 (src/audio_rag/reranking/bge.py:51-55, 119-123): XLMRobertaForSequenceClassification with
 num_labels = 1 (12 layers, d 768, 12 heads, FFN 3072, exact-erf GELU, LN eps 1e-5), head
-dense -> tanh -> out_proj on <s>, then sigmoid. Activations are fp32 (ST's default dtype).
+dense -> tanh -> out_proj on <s>, then sigmoid. The fp32 path keeps ST's default dtype; the fp16
+path (to_dtype(torch.float16)) runs fp16 GEMMs, the fused fp16 attention and an fp16 residual
+stream with fp32 LayerNorm statistics: max |score error| 6.5e-5 - 9.6e-5 vs the fp32 forward
+(budget 1e-3, tests/test_encoder_gpu.py).
 """
 
 from __future__ import annotations
@@ -69,15 +72,20 @@ class CrossEncoderXLMR:
                 ln2=(sd[p + "output.LayerNorm.weight"], sd[p + "output.LayerNorm.bias"]),
             ))
         self.gemm_dtype = torch.float32
+        self.residual = "fp32"
         self.head = (sd["classifier.dense.weight"], sd["classifier.dense.bias"],
                      sd["classifier.out_proj.weight"].reshape(-1).contiguous(),
                      sd["classifier.out_proj.bias"])
 
-    def to_dtype(self, dtype: torch.dtype) -> None:
+    def to_dtype(self, dtype: torch.dtype, residual: str = "fp16") -> None:
         """GEMM operand dtype, fp32 accumulate.
         fp32 / bf16: LayerNorm / softmax / GELU / head stay fp32 in the armi kernels.
         fp16: the fp16 forward (_forward_f16): fp16 GEMM outputs, fused fp16 attention
-        (armi_enc_attention_f16), fp32 residual stream and LayerNorm statistics."""
+        (armi_enc_attention_f16), LayerNorm statistics in fp32; the residual stream is fp16
+        (residual="fp16", the default: half the LayerNorm traffic) or fp32 ("fp32")."""
+        if residual not in ("fp16", "fp32"):
+            raise ValueError("residual must be 'fp16' or 'fp32'")
+        self.residual = residual
         self.gemm_dtype = dtype
         for ly in self.layers:
             for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
@@ -101,6 +109,8 @@ class CrossEncoderXLMR:
              self.word.shape[0], self.pos.shape[0], self.eps, s)
         h16 = h.half()
         scale = 1.0 / math.sqrt(dh)
+        if self.residual == "fp16":
+            return self._layers_f16_residual(h16, mask, n, L)
         for ly in self.layers:
             qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])                     # [n*L, 3d] fp16
             ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
@@ -120,6 +130,35 @@ class CrossEncoderXLMR:
         probs = torch.empty(n, dtype=torch.float32, device=self.device)
         call("armi_enc_cls_head_sigmoid", ptr(h), ptr(self.head[0]), ptr(self.head[1]),
              ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, L, d, s)
+        return probs
+
+    def _layers_f16_residual(self, h16: torch.Tensor, mask: torch.Tensor, n: int,
+                             L: int) -> torch.Tensor:
+        """Encoder layers with an all-fp16 residual stream (armi_enc_add_layernorm_f16: fp16 in
+        and out, fp32 statistics), then the classification head on the fp32 <s> rows."""
+        d, H, dh = self.d, self.heads, self.dh
+        s = stream_handle()
+        rows = n * L
+        lin = torch.nn.functional.linear
+        scale = 1.0 / math.sqrt(dh)
+        for ly in self.layers:
+            qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])
+            ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
+            call("armi_enc_attention_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh, scale, s)
+            attn = lin(ctx, ly["wo_h"], ly["bo_h"])
+            h1 = torch.empty_like(h16)
+            call("armi_enc_add_layernorm_f16", ptr(attn), ptr(h16), ptr(ly["ln1"][0]),
+                 ptr(ly["ln1"][1]), ptr(h1), rows, d, self.eps, s)
+            inter = lin(h1, ly["wi_h"], ly["bi_h"])
+            call("armi_enc_gelu_f16", ptr(inter), None, rows, inter.shape[1], s)
+            out = lin(inter, ly["wo2_h"], ly["bo2_h"])
+            h16 = torch.empty_like(h1)
+            call("armi_enc_add_layernorm_f16", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
+                 ptr(ly["ln2"][1]), ptr(h16), rows, d, self.eps, s)
+        cls = h16.view(n, L, d)[:, 0].float().contiguous()  # [n, d]
+        probs = torch.empty(n, dtype=torch.float32, device=self.device)
+        call("armi_enc_cls_head_sigmoid", ptr(cls), ptr(self.head[0]), ptr(self.head[1]),
+             ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, 1, d, s)
         return probs
 
     def flops(self, n: int, L: int) -> float:

@@ -207,6 +207,11 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
 int armi_enc_layernorm_residual_f16(const uint16_t* x, const float* res, const float* gamma,
                                     const float* beta, float* out, uint16_t* out16,
                                     int64_t n_rows, int width, float eps, hipStream_t stream);
+/* out16 = LayerNorm(x + res) with fp16 x, res and output (fp32 statistics): the all-fp16
+ * residual stream of the default fp16 cross-encoder forward. width must be 768 or 1024. */
+int armi_enc_add_layernorm_f16(const uint16_t* x, const uint16_t* res, const float* gamma,
+                               const float* beta, uint16_t* out16, int64_t n_rows, int width,
+                               float eps, hipStream_t stream);
 /* in-place exact (erf) GELU of fp16 x (+ fp32 bias[col], nullable), computed in fp32;
  * width must be a multiple of 8. */
 int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
