@@ -55,6 +55,9 @@ class RerankingConfig(BaseModel):
     # MI355X build
     seed: int = 5
     max_length: int = Field(default=512, ge=8, le=512)
+    # cross-encoder compute: "fp16" = fp16 GEMMs + fused fp16 attention (scores within 1e-4 of
+    # the fp32 forward, north_star budget 1e-3); "fp32" = sentence-transformers' default dtype
+    dtype: Literal["fp16", "fp32"] = "fp16"
 
 
 class ExpansionConfig(BaseModel):

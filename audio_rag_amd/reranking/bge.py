@@ -50,6 +50,8 @@ class BGEReranker(BaseReranker):
         try:
             hf = build_reranker(self.config.seed, self._arch)
             self._model = CrossEncoderXLMR(hf, self._device)
+            if self.config.dtype == "fp16":
+                self._model.to_dtype(torch.float16)
             self._is_loaded = True
         except Exception as e:
             raise RerankingError(f"Failed to load reranker: {e}") from e
