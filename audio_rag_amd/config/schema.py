@@ -26,6 +26,9 @@ class EmbeddingConfig(BaseModel):
     # MI355X build: weights are not on disk; the encoder is initialised from this seed
     seed: int = 0
     max_length: int = Field(default=8192, ge=8)
+    # batch-1 query encodes replay a HIP graph captured per padded length bucket (16, 32, 64,
+    # ..., 512 tokens) instead of re-launching the 24-layer forward kernel by kernel
+    query_graphs: bool = True
 
 
 class RetrievalConfig(BaseModel):

@@ -74,6 +74,7 @@ class BGEM3Embedder(BaseEmbedder):
         self._arch = arch
         self._model = None
         self._sparse = None
+        self._graphs: dict[int, tuple] = {}
         self.tokenizer = HashTokenizer()
         logger.info(f"BGEM3Embedder initialized: model={config.model}, device={self._device}, "
                     f"sparse={self._use_sparse}")
@@ -93,6 +94,7 @@ class BGEM3Embedder(BaseEmbedder):
             return
         self._model = None
         self._sparse = None
+        self._graphs.clear()
         gc.collect()
         torch.cuda.empty_cache()
 
@@ -128,6 +130,60 @@ class BGEM3Embedder(BaseEmbedder):
             tw = torch.relu(self._sparse(hidden)).squeeze(-1).float().cpu().tolist()
             lex = [lexical_weights(tw[i][: len(s)], s) for i, s in enumerate(seqs)]
         return dense.contiguous(), lex
+
+    # ------------------------------------------------------------- captured query encode
+
+    GRAPH_BUCKETS = (16, 32, 64, 128, 256, 512)
+
+    def _forward_static(self, ids_t: torch.Tensor, mask_t: torch.Tensor):
+        hidden = self._model(input_ids=ids_t, attention_mask=mask_t).last_hidden_state
+        dense = torch.nn.functional.normalize(hidden[:, 0], dim=-1)
+        tw = torch.relu(self._sparse(hidden)).squeeze(-1).float() if self._use_sparse else None
+        return dense, tw
+
+    def _graph_for(self, bucket: int):
+        """(graph, static ids, static mask, static dense, static token weights) for a batch-1
+        query padded to `bucket` tokens; captured on first use (torch.cuda.CUDAGraph = a HIP
+        graph on ROCm), warmed up on a side stream first as capture requires."""
+        g = self._graphs.get(bucket)
+        if g is not None:
+            return g
+        ids_t = torch.full((1, bucket), 1, dtype=torch.long, device=self._device)
+        mask_t = torch.zeros((1, bucket), dtype=torch.long, device=self._device)
+        ids_t[0, 0] = 0
+        mask_t[0, 0] = 1
+        side = torch.cuda.Stream(device=self._device)
+        side.wait_stream(torch.cuda.current_stream(self._device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._forward_static(ids_t, mask_t)
+        torch.cuda.current_stream(self._device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            dense, tw = self._forward_static(ids_t, mask_t)
+        g = (graph, ids_t, mask_t, dense, tw)
+        self._graphs[bucket] = g
+        return g
+
+    @torch.inference_mode()
+    def encode_query_ids(self, seq: list[int]) -> tuple[torch.Tensor, list[dict[int, float]] | None]:
+        """encode_ids for one sequence through the captured graph of its length bucket (right
+        padding with <pad> and a zero mask leaves the real tokens' outputs unchanged, as in any
+        padded batch); sequences longer than the largest bucket run eagerly."""
+        L = len(seq)
+        bucket = next((b for b in self.GRAPH_BUCKETS if b >= L), None)
+        if not self.config.query_graphs or bucket is None:
+            return self.encode_ids([seq])
+        graph, ids_t, mask_t, dense, tw = self._graph_for(bucket)
+        ids_t.fill_(1)
+        mask_t.zero_()
+        ids_t[0, :L] = torch.tensor(seq, dtype=torch.long).to(self._device, non_blocking=True)
+        mask_t[0, :L] = 1
+        graph.replay()
+        lex = None
+        if self._use_sparse:
+            lex = [lexical_weights(tw[0, :L].cpu().tolist(), seq)]
+        return dense.clone(), lex
 
     def _results(self, dense: torch.Tensor, lex) -> list[EmbeddingResult]:
         rows = dense.cpu().tolist()
@@ -166,8 +222,8 @@ class BGEM3Embedder(BaseEmbedder):
     @require_loaded
     def embed_query(self, query: str) -> EmbeddingResult:
         try:
-            seqs = [self.tokenizer.encode(query, self.config.max_length)]
-            return self._results(*self.encode_ids(seqs))[0]
+            seq = self.tokenizer.encode(query, self.config.max_length)
+            return self._results(*self.encode_query_ids(seq))[0]
         except Exception as e:
             raise EmbeddingError(f"Query embedding failed: {e}")
 

@@ -192,13 +192,17 @@ def main() -> None:
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=30)
-    ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream"],
+    ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline"],
                     default="dense",
                     help="dense: BASELINE metric (default); hybrid: dense+sparse prefetch 2k + RRF "
                          "(configs[2] without rerank); hybrid_rerank: configs[2]: top-20 fused -> "
                          "cross-encoder -> top-k; stream: single queries arriving at --qps "
                          "(Poisson) through QueryBatcher -> MI355XRetriever, reference-shaped "
-                         "results (configs[4]'s streaming query, 1 GPU)")
+                         "results (configs[4]'s streaming query, 1 GPU); pipeline: "
+                         "QueryPipeline.query() one query at a time (BGE-M3 encode -> hybrid "
+                         "search -> rerank), per-stage latency beside the reference's published "
+                         "numbers")
+    ap.add_argument("--queries", type=int, default=200, help="pipeline: timed queries")
     ap.add_argument("--qps", type=float, default=20000.0, help="stream: offered queries/s")
     ap.add_argument("--duration", type=float, default=4.0, help="stream: seconds of arrivals")
     ap.add_argument("--initial-k", type=int, default=20)
@@ -209,6 +213,8 @@ def main() -> None:
 
     if args.workload == "stream":
         return stream_main(args)
+    if args.workload == "pipeline":
+        return pipeline_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -453,6 +459,109 @@ def main() -> None:
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+WORDS = ("gradient descent learning rate loss function model training data neural network layer "
+         "weights bias optimizer batch epoch regression classification feature vector matrix "
+         "probability distribution bayes kernel margin support vector tree boosting variance "
+         "lecture professor example equation derivative convex objective parameter sample").split()
+
+
+def pipeline_main(args) -> None:
+    """The reference's query path one query at a time, as AudioRAG.query() runs it
+    (pipeline/query.py:97-215): BGE-M3 query encode (XLM-R large, 24 layers, fp16, HIP-graph
+    replay), hybrid search (dense + sparse prefetch 2 x initial_k = 40 each, RRF -> 20) over the
+    chunk store, cross-encoder rerank 20 -> 5 (XLM-R base, fp16), RetrievalResult objects; answer
+    generation off. Weights are seeded (no checkpoints offline), so only timing is meaningful.
+    value = 1 / mean end-to-end latency (one stream); the reference publishes single-GPU
+    latencies for the same stages (on a ~100s-of-chunks corpus)."""
+    import logging
+
+    from audio_rag_amd.config.schema import AudioRAGConfig
+    from audio_rag_amd.embeddings.bge_m3 import BGEM3Embedder
+    from audio_rag_amd.pipeline.query import QueryPipeline
+    from audio_rag_amd.reranking.bge import BGEReranker
+    from audio_rag_amd.retrieval.collection import ChunkCollection
+    from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex
+    from audio_rag_amd.retrieval.mi355x import MI355XRetriever
+
+    logging.disable(logging.INFO)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, dim = args.chunks, args.dim
+    cfg = AudioRAGConfig()
+    cfg.retrieval.search_type = "hybrid"
+    rng = np.random.default_rng(11)
+    texts = [" ".join(rng.choice(WORDS, size=int(rng.integers(30, 60)))) for _ in range(4096)]
+    payloads = [{"text": texts[i % 4096], "start": float(i), "end": float(i) + 30.0,
+                 "speaker": None, "metadata": {}} for i in range(n)]
+    rows = make_rows(0, n, dim, dev)
+    sindex = SparseIndex(*make_sparse_rows(0, n, dev), vocab=VOCAB)
+    ret = MI355XRetriever(cfg.retrieval, dim)
+    ret.attach_collection(ChunkCollection.from_indexes(cfg.retrieval.collection_name,
+                                                       DenseIndex(rows), payloads, sindex))
+    emb = BGEM3Embedder(cfg.embedding, device=dev)
+    emb.load()
+    rr = BGEReranker(cfg.reranking, device=dev)
+    rr.load()
+    pipe = QueryPipeline(cfg)
+    pipe._embedder, pipe._retriever = emb, ret
+    pipe._reranker, pipe._reranker_created = rr, True
+    queries = [" ".join(rng.choice(WORDS, size=int(rng.integers(6, 16)))) for _ in range(256)]
+
+    def sync_time(fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        return out, time.perf_counter() - t
+
+    for q in queries[:16]:  # warm-up: graph capture per length bucket, kernel autotuning
+        pipe.query(q, generate_answer=False)
+    e2e, t_emb, t_search, t_rerank = [], [], [], []
+    for i in range(args.queries):
+        q = queries[i % len(queries)]
+        res, t = sync_time(lambda: pipe.query(q, generate_answer=False))
+        assert res.reranked and len(res.results) == cfg.reranking.top_k
+        e2e.append(t)
+        e, t = sync_time(lambda: emb.embed_query(q))
+        t_emb.append(t)
+        hits, t = sync_time(lambda: ret.search(e, top_k=cfg.reranking.initial_k,
+                                               search_type="hybrid"))
+        t_search.append(t)
+        _, t = sync_time(lambda: rr.rerank(q, hits, top_k=cfg.reranking.top_k))
+        t_rerank.append(t)
+    ms = lambda xs, p: float(np.percentile(np.array(xs) * 1e3, p))
+    print(json.dumps({
+        "metric": METRIC,
+        "value": 1.0 / float(np.mean(e2e)),
+        "unit": "queries/sec",
+        "n_gpus": 1,
+        "steps": args.queries,
+        "warmup": 16,
+        "ms_per_step": float(np.mean(e2e)) * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": ("synthetic: seeded BGE-M3 / reranker weights, N(0,1) unit fp16 chunk vectors, "
+                 "Zipf sparse vectors, synthetic chunk and query texts"),
+        "config": {"workload": (f"QueryPipeline.query() single-stream: BGE-M3 encode -> hybrid "
+                                f"search (prefetch 40 + 40, RRF 20) over {n} chunks -> rerank "
+                                f"20 -> 5 (fp16), one query at a time"),
+                   "n_chunks": n, "dim": dim, "initial_k": cfg.reranking.initial_k,
+                   "top_k": cfg.reranking.top_k, "parallelism": "single GPU, batch 1"},
+        "p50_ms": ms(e2e, 50), "p95_ms": ms(e2e, 95), "p99_ms": ms(e2e, 99),
+        "stage_p50_ms": {"embed": ms(t_emb, 50), "hybrid_search": ms(t_search, 50),
+                         "rerank": ms(t_rerank, 50)},
+        "reference_published_p50_ms": {"embed": 18, "hybrid_search": 48, "rerank": 38,
+                                       "warm_query": 141,
+                                       "source": "docs/SALES_TECHNICAL_GUIDE.md:563-565, "
+                                                 "README.md:37-38 (single unspecified GPU, "
+                                                 "~100s of chunks)"},
+        "roofline": None,
+        "cpu_baseline": None,
+    }), flush=True)
 
 
 def stream_main(args) -> None:

@@ -289,3 +289,28 @@ def test_cross_encoder_bf16_gemms_within_budget(gpu):
     err = (got - ref).abs().max().item()
     print(f"bf16 GEMM max |score error| = {err:.2e}")
     assert err < 1e-2
+
+
+def test_bge_m3_query_graph_equals_eager(gpu):
+    """The HIP-graph replay of a batch-1 query encode (padded to its length bucket) gives the
+    eager forward's dense vector and lexical weights."""
+    from audio_rag_amd.config import EmbeddingConfig
+    from audio_rag_amd.embeddings.bge_m3 import BGEM3Embedder
+
+    e = BGEM3Embedder(EmbeddingConfig(), device=gpu, arch=dict(num_hidden_layers=3))
+    e.load()
+    for text in ("short query", "what does the lecturer say about gradient descent and the "
+                 "learning rate schedule in the third lecture of the course " * 2):
+        seq = e.tokenizer.encode(text)
+        dg, lg = e.encode_query_ids(seq)
+        de, le = e.encode_ids([seq])
+        torch.cuda.synchronize()
+        cos = torch.nn.functional.cosine_similarity(dg.float(), de.float()).item()
+        assert cos > 0.9999, cos
+        clear = [t for t, w in le[0].items() if w > 0.02]
+        assert all(t in lg[0] for t in clear)
+        assert all(le[0].get(t, 0.0) > 0 for t, w in lg[0].items() if w > 0.02)
+        np.testing.assert_allclose([lg[0][t] for t in clear], [le[0][t] for t in clear],
+                                   rtol=5e-3, atol=1e-3)
+    assert len(e._graphs) == 2  # one captured graph per length bucket used
+
