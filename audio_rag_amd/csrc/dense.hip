@@ -349,24 +349,26 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
   }
   float d0 = kNegInf, d1 = kNegInf;
 
+  // Branch-free staging loads (clamped addresses, nothing consumes them before the store): the compiler can
+  // count them, so storing k-step s+1 waits only for its own loads (vmcnt(6)) and the k-step s+2
+  // loads issued after them stay in flight across the MFMAs and the barrier.
+  static_assert(kGRT * 8 == 2 * kGThreads && kGQB * 8 == 4 * kGThreads, "staging split");
   auto load_stage = [&](int64_t st, u32x4 (&reg)[kGChunks]) {
     const int64_t tn = st / KT;
     const int t = (int)(st - tn * KT);
     const int64_t row0 = lo + tn * kGRT;
 #pragma unroll
-    for (int c = 0; c < kGChunks; ++c) {
+    for (int c = 0; c < 2; ++c) {  // 128 rows x 8 chunks
       const int e = tid + c * kGThreads;
-      const int rr = e >> 3, ch = e & 7;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (rr < kGRT) {
-        int64_t row = row0 + rr;
-        row = row < n_rows ? row : n_rows - 1;
-        v = *reinterpret_cast<const u32x4*>(rows + row * DIM + 64 * t + 8 * ch);
-      } else {
-        const int q = q_base + rr - kGRT;
-        if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 64 * t + 8 * ch);
-      }
-      reg[c] = v;
+      const int64_t row = min(row0 + (e >> 3), n_rows - 1);
+      reg[c] = *reinterpret_cast<const u32x4*>(rows + row * DIM + 64 * t + 8 * (e & 7));
+    }
+#pragma unroll
+    for (int c = 2; c < kGChunks; ++c) {  // 256 queries x 8 chunks
+      const int e = tid + c * kGThreads;
+      // query columns past nq load a copy of the last query: their scores are never emitted
+      const int q = min(q_base + (e >> 3) - kGRT, nq - 1);
+      reg[c] = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 64 * t + 8 * (e & 7));
     }
   };
   auto store_stage = [&](int buf, const u32x4 (&reg)[kGChunks]) {
@@ -450,22 +452,19 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
     acc00 = f32x16{}; acc01 = f32x16{}; acc10 = f32x16{}; acc11 = f32x16{};
   };
   if (n_steps > 0) {
-    // k-step s lives in LDS buffer s & 1; its registers were loaded two k-steps earlier (two
-    // register sets), so a global load has two k-steps of MFMA work to land
-    u32x4 regA[kGChunks], regB[kGChunks];
-    load_stage(0, regA);
-    store_stage(0, regA);
-    if (n_steps > 1) load_stage(1, regB);
+    // k-step s lives in LDS buffer s & 1. Step s: store the registers of s+1 (loaded during step
+    // s-1, so their wait is a whole step old), load s+2 into the same registers, MFMAs of s,
+    // epilogue, barrier. One register set; every load has the MFMA phase of a step to land.
+    u32x4 reg[kGChunks];
+    load_stage(0, reg);
+    store_stage(0, reg);
+    if (n_steps > 1) load_stage(1, reg);
     __syncthreads();
-    for (int64_t st = 0; st < n_steps; st += 2) {
-      if (st + 2 < n_steps) load_stage(st + 2, regA);
-      compute(st, 0);
-      if (st + 1 < n_steps) store_stage(1, regB);
-      __syncthreads();
-      if (st + 1 >= n_steps) break;
-      if (st + 3 < n_steps) load_stage(st + 3, regB);
-      compute(st + 1, 1);
-      if (st + 2 < n_steps) store_stage(0, regA);
+    for (int64_t st = 0; st < n_steps; ++st) {
+      const int buf = (int)(st & 1);
+      if (st + 1 < n_steps) store_stage(buf ^ 1, reg);
+      if (st + 2 < n_steps) load_stage(st + 2, reg);
+      compute(st, buf);
       __syncthreads();
     }
   }
