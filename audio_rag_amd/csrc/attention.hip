@@ -82,43 +82,68 @@ __global__ __launch_bounds__(kThreads) void attention_f16_kernel(
   const int row_stride = 3 * heads * kDh;  // halves between consecutive tokens
   const uint16_t* base = qkv + (size_t)seq * L * row_stride + head * kDh;
 
-  // stage K (row-major) and V^T (two keys per 32-bit LDS word) of this (seq, head)
-  for (int e = tid; e < lp * (kDh / 8); e += kThreads) {
-    const int j = e >> 3, c = e & 7;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (j < L) v = *reinterpret_cast<const u32x4*>(base + (size_t)j * row_stride + heads * kDh + 8 * c);
-    *reinterpret_cast<u32x4*>(ks + j * kKStride + 8 * c) = v;
-  }
-  for (int e = tid; e < (lp / 2) * (kDh / 8); e += kThreads) {
-    const int jp = e >> 3, c = e & 7;
-    const int j = 2 * jp;
-    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
-    const uint16_t* vbase = base + 2 * heads * kDh + 8 * c;
-    if (j < L) a = *reinterpret_cast<const u32x4*>(vbase + (size_t)j * row_stride);
-    if (j + 1 < L) b = *reinterpret_cast<const u32x4*>(vbase + (size_t)(j + 1) * row_stride);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
-      const uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
-      *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i) * vts + j) = lo;
-      *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i + 1) * vts + j) = hi;
-    }
-  }
-  for (int j = tid; j < lp; j += kThreads)
-    kbias[j] = (j < L && mask[(size_t)seq * L + j] != 0) ? 0.f : -INFINITY;
-
   const int wave = armi::wave_id();
   const int lane = tid & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
   const int qw0 = qblk * kQPerWg + wave * kQPerWave;
   const int q = qw0 + r;
+  // The Q fragments and every K / V load of a 256-key round are issued before the first LDS
+  // store, so a workgroup waits for HBM once per round instead of once per load.
   u32x4 qf[kDh / 16];
 #pragma unroll
   for (int t = 0; t < kDh / 16; ++t) {
     qf[t] = u32x4{0u, 0u, 0u, 0u};
     if (q < L) qf[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
   }
+  // Stage K (row-major) and V^T (two keys per 32-bit LDS word) of this (seq, head). Per round of
+  // 256 keys thread tid loads K chunks e = tid + 512u (u < 4) and V key pairs e = tid + 512u
+  // (u < 2): chunk e & 7 (8 halves) of key (pair) e >> 3.
+  const uint16_t* kbase = base + heads * kDh;
+  const uint16_t* vbase = base + 2 * heads * kDh;
+  for (int j0 = 0; j0 < lp; j0 += 256) {
+    u32x4 kv[4], va[2], vb[2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + kThreads * u;
+      const int j = j0 + (e >> 3);
+      kv[u] = u32x4{0u, 0u, 0u, 0u};
+      if (j < L) kv[u] = *reinterpret_cast<const u32x4*>(kbase + (size_t)j * row_stride + 8 * (e & 7));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + kThreads * u;
+      const int j = j0 + 2 * (e >> 3);
+      const uint16_t* vp = vbase + 8 * (e & 7);
+      va[u] = u32x4{0u, 0u, 0u, 0u};
+      vb[u] = u32x4{0u, 0u, 0u, 0u};
+      if (j < L) va[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)j * row_stride);
+      if (j + 1 < L) vb[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)(j + 1) * row_stride);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + kThreads * u;
+      const int j = j0 + (e >> 3);
+      if (j < lp) *reinterpret_cast<u32x4*>(ks + j * kKStride + 8 * (e & 7)) = kv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + kThreads * u;
+      const int j = j0 + 2 * (e >> 3);
+      const int c = e & 7;
+      if (j < lp) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t lo = (va[u][i] & 0xffffu) | (vb[u][i] << 16);
+          const uint32_t hi = (va[u][i] >> 16) | (vb[u][i] & 0xffff0000u);
+          *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i) * vts + j) = lo;
+          *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i + 1) * vts + j) = hi;
+        }
+      }
+    }
+  }
+  for (int j = tid; j < lp; j += kThreads)
+    kbias[j] = (j < L && mask[(size_t)seq * L + j] != 0) ? 0.f : -INFINITY;
   __syncthreads();
   if (qw0 >= L) return;  // wave-uniform: no query of this wave exists (after the only barrier)
   const int nkb = lp / 32;
@@ -130,8 +155,13 @@ __global__ __launch_bounds__(kThreads) void attention_f16_kernel(
   f32x16 o0 = {}, o1 = {};  // O^T rows (dims) (i&3)+8(i>>2)+4h and 32 + that, column q
   const uint16_t* v0 = vt + r * vts + 4 * h;
   const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
+  // S^T of block kb + 1 is issued before the softmax of block kb, so its MFMAs run under that
+  // VALU work. exp2 is the bare v_exp_f32 (arguments are <= 0; a result below 2^-126 flushes to
+  // 0, which no fp16 P or fp32 running sum can represent next to the block maximum's 1 anyway).
+  f32x16 nxt = score_block(ks, 0, r, h, qf);
   for (int kb = 0; kb < nkb; ++kb) {
-    const f32x16 acc = score_block(ks, kb, r, h, qf);
+    const f32x16 acc = nxt;
+    if (kb + 1 < nkb) nxt = score_block(ks, kb + 1, r, h, qf);
     float s[16];
     float bm = -INFINITY;
 #pragma unroll
@@ -142,12 +172,12 @@ __global__ __launch_bounds__(kThreads) void attention_f16_kernel(
     bm = fmaxf(bm, __shfl_xor(bm, 32));
     const float mn = fmaxf(m, bm);
     if (mn == -INFINITY) continue;  // every key so far is padding (same for all lanes)
-    const float alpha = exp2f(m - mn);  // 0 on the first live block (m == -inf)
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);  // 0 on the first live block (m == -inf)
     float p[16];
     float add = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      p[i] = exp2f(s[i] - mn);
+      p[i] = __builtin_amdgcn_exp2f(s[i] - mn);
       add += p[i];
     }
     l = l * alpha + add;
