@@ -556,29 +556,35 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       if (lane < kHold && u < nU) gcur[u] = scv;
     }
   };
-  // seg_first (lane s): first list index whose term lies in segment s or later
-  int seg_first = n_w;
-  if (lane <= nSeg) {
+  // seg_first (lane s) / seg_first2 (lane s - 64): first list index whose term lies in segment
+  // s or later (a pass has at most kMaxU / kU = 128 segments)
+  static_assert(kMaxU / kU <= 128, "two lane slots per segment boundary");
+  auto lower_seg = [&](int sg) {
     int a0 = 0, n = n_w;
     while (n > 0) {
       const int h = n >> 1;
-      if (my[a0 + h].u < lane * kU) {
+      if (my[a0 + h].u < sg * kU) {
         a0 += h + 1;
         n -= h + 1;
       } else {
         n = h;
       }
     }
-    seg_first = a0;
-  }
+    return a0;
+  };
+  const int seg_first = lane <= nSeg ? lower_seg(lane) : n_w;
+  const int seg_first2 = lane + 64 <= nSeg ? lower_seg(lane + 64) : n_w;
+  auto first_of = [&](int sg) {  // sg is wave-uniform
+    return sg >= nSeg ? n_w : (sg < 64 ? rl_i(seg_first, sg) : rl_i(seg_first2, sg - 64));
+  };
   // bit i: this lane's row got a posting of one of query i's terms in the current tile
   uint32_t hb = 0;
   auto compute = [&](int s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
     (void)tile;
     const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)(s & 1) * kU * 64 + lane);
-    const int j0 = rl_i(seg_first, seg);
-    const int j1 = seg + 1 < 64 ? rl_i(seg_first, seg + 1) : n_w;
+    const int j0 = first_of(seg);
+    const int j1 = first_of(seg + 1);
     // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; an
     // absent query weight is 0 and adding fl32(0 * v) = +-0 leaves an fp32 sum unchanged, so
     // every term updates all four accumulators without branches

@@ -153,3 +153,23 @@ def test_sparse_golden_corpus_repeatable(gpu, oracle_mod):
                 want1 = oracle_mod.sparse_topk(*csr, *one, k, row_mask=mask)
                 for _ in range(3):
                     _same(_run(idx, one, k, gpu, mask=mask), want1)
+
+
+def test_sparse_pass_with_many_distinct_terms(gpu, oracle_mod):
+    """64 queries x 200 distinct corpus terms, disjoint across queries: one pass holds 12 800
+    distinct terms, i.e. 100 staging segments of 128 terms (more segments than wave lanes)."""
+    csr = oracle_mod.sparse_corpus(20000, seed=51)
+    rng = np.random.default_rng(52)
+    nq, nt = 64, 200
+    present = np.unique(csr[1])
+    assert present.size >= nq * nt
+    # ascending within each query, as the host layer hands query CSRs to the device (and the
+    # oracle's merge-join expects)
+    qx = np.sort(rng.permutation(present)[:nq * nt].reshape(nq, nt), axis=1).reshape(-1).astype(np.int32)
+    qi = np.arange(0, nq * nt + 1, nt, dtype=np.int32)
+    qv = rng.uniform(0.05, 0.35, nq * nt).astype(np.float32)
+    idx = _sparse_index(csr, gpu)
+    for k in (5, 40):
+        got = _run(idx, (qi, qx, qv), k, gpu)
+        _same(got, oracle_mod.sparse_topk(*csr, qi, qx, qv, k))
+        assert (got["count"] > 0).all()
