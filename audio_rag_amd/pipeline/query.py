@@ -27,7 +27,7 @@ from audio_rag_amd.embeddings import EmbeddingsRegistry
 from audio_rag_amd.pipeline.components import GeneratorRegistry, HyDEExpander, ResourceManager
 from audio_rag_amd.reranking import RerankerRegistry
 from audio_rag_amd.retrieval import RetrievalRegistry
-from audio_rag_amd.retrieval.mi355x import QueryBatch, sparse_arrays
+from audio_rag_amd.retrieval.mi355x import QueryBatch, query_sparse_arrays
 from audio_rag_amd.utils.decorators import timed
 
 logger = logging.getLogger(__name__)
@@ -218,7 +218,7 @@ class QueryPipeline:
             dense, lex = self.embedder.embed_queries(query_texts)
             batch = QueryBatch(dense=dense)
             if lex is not None and all(lex):
-                parts = [sparse_arrays(self.embedder._convert_sparse(x)) for x in lex]
+                parts = [query_sparse_arrays(self.embedder._convert_sparse(x)) for x in lex]
                 indptr = np.zeros(len(parts) + 1, dtype=np.int32)
                 np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
                 t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(retriever.device)

@@ -26,7 +26,7 @@ import torch
 
 from audio_rag_amd.core.base import EmbeddingResult, RetrievalResult
 from audio_rag_amd.core.exceptions import RetrievalError
-from audio_rag_amd.retrieval.mi355x import MI355XRetriever, QueryBatch, sparse_arrays
+from audio_rag_amd.retrieval.mi355x import MI355XRetriever, QueryBatch, query_sparse_arrays
 
 logger = logging.getLogger(__name__)
 
@@ -79,7 +79,7 @@ class QueryBatcher:
     def submit(self, query: EmbeddingResult, filter_metadata: dict | None = None) -> Future:
         """EmbeddingResult (BGEM3Embedder.embed_query output) -> Future[list[RetrievalResult]]."""
         return self.submit_arrays(np.asarray(query.dense, dtype=np.float32),
-                                  sparse_arrays(query.sparse), filter_metadata)
+                                  query_sparse_arrays(query.sparse), filter_metadata)
 
     def search(self, query: EmbeddingResult, filter_metadata: dict | None = None,
                timeout: float | None = None) -> list[RetrievalResult]:

@@ -58,6 +58,19 @@ def sparse_arrays(sv: SparseVector | None) -> tuple[np.ndarray, np.ndarray] | No
     return idx.astype(np.int32), val
 
 
+MAX_QUERY_TERMS = 256  # armi_sparse_topk's per-query term capacity (include/armi.h)
+
+
+def query_sparse_arrays(sv: SparseVector | None) -> tuple[np.ndarray, np.ndarray] | None:
+    """sparse_arrays for a query vector, refusing more terms than the device search scores (it
+    would silently use only the first 256; Qdrant uses every term)."""
+    arr = sparse_arrays(sv)
+    if arr is not None and arr[0].size > MAX_QUERY_TERMS:
+        raise ValueError(f"sparse query has {arr[0].size} terms; the MI355X sparse search takes at "
+                         f"most {MAX_QUERY_TERMS}")
+    return arr
+
+
 def fp16_rows(vectors: list[list[float]] | np.ndarray, dim: int) -> np.ndarray:
     a = np.asarray(vectors, dtype=np.float32)
     if a.ndim != 2 or a.shape[1] != dim:
@@ -241,7 +254,7 @@ class MI355XRetriever(BaseRetriever):
                                            self.embedding_dim)).to(self.device)
         if any(q.sparse is None for q in query_embeddings):
             return QueryBatch(dense=dense)
-        parts = [sparse_arrays(q.sparse) for q in query_embeddings]
+        parts = [query_sparse_arrays(q.sparse) for q in query_embeddings]
         indptr = np.zeros(len(parts) + 1, dtype=np.int32)
         np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
         idx = np.concatenate([p[0] for p in parts]).astype(np.int32)

@@ -141,7 +141,8 @@ int armi_sparse_index_destroy(armi_sparse_index* index);
 
 size_t armi_sparse_workspace_bytes(const armi_sparse_index* index, int n_queries, int k);
 /* Sparse dot-product top-k. Query CSR: q_indptr [n_queries+1] int32 (absolute offsets),
- * q_indices ascending int32 (at most 256 per query; more set flag bit 8), q_values float.
+ * q_indices ascending int32 (at most 256 per query: a longer query is scored on its first 256
+ * terms and gets flag bit 8; the Python layer refuses such queries before the call), q_values float.
  * out_flags: ARMI_FLAG_CERTIFIED (merged lists proved exact) or ARMI_FLAG_FALLBACK (answer from
  * the collecting rescan; bit 4 = more than 4096 rows tied at the threshold, answer truncated). score = sum over shared indices, ascending index order, of
  * fl32(q*d) accumulated in fp32 (mul and add rounded separately). Only rows that share at

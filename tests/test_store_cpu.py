@@ -138,3 +138,21 @@ def test_retriever_save_load_and_sparse_drop(tmp_path, drop):
     else:
         _same_sparse(coll.sparse_rows, sparse)
     assert coll.payloads[3]["metadata"] == {"lecture": 3, "tags": []}
+
+
+def test_query_sparse_vectors_are_sorted_and_capped():
+    """Query CSRs reach armi_sparse_topk ascending and unique; a query with more terms than the
+    device search scores (256) is refused instead of silently truncated."""
+    from audio_rag_amd.core import SparseVector
+    from audio_rag_amd.retrieval.mi355x import MAX_QUERY_TERMS, query_sparse_arrays
+
+    idx, val = query_sparse_arrays(SparseVector(indices=[9, 4, 7], values=[0.1, 0.2, 0.3]))
+    assert idx.tolist() == [4, 7, 9] and val.tolist() == pytest.approx([0.2, 0.3, 0.1])
+    assert query_sparse_arrays(None) is None
+    ok = SparseVector(indices=list(range(4, 4 + MAX_QUERY_TERMS)), values=[0.1] * MAX_QUERY_TERMS)
+    assert query_sparse_arrays(ok)[0].size == MAX_QUERY_TERMS
+    long = SparseVector(indices=list(range(4, 5 + MAX_QUERY_TERMS)), values=[0.1] * (MAX_QUERY_TERMS + 1))
+    with pytest.raises(ValueError, match="at most 256"):
+        query_sparse_arrays(long)
+    with pytest.raises(ValueError, match="unique"):
+        query_sparse_arrays(SparseVector(indices=[5, 5], values=[0.1, 0.2]))
