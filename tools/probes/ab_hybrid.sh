@@ -9,5 +9,5 @@ for v in new old new old; do
   python -c "import json;d=json.loads(open('gpurun_out/ab_$v.log').read().strip().splitlines()[-1]);print('$v', round(d['value']), d['ms_per_step'])"
 done
 cp $L/libarmi_new.so $L/libarmi.so
-timeout -k 10 300 python -u -m pytest tests/test_sparse_rrf_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_sparse_rrf_gpu.py tests/test_golden_pipeline_gpu.py tests/test_store_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1; rc=$?
 tail -2 gpurun_out/ab_tests.log; exit $rc
