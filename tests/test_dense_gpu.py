@@ -66,6 +66,27 @@ def test_dense_topk_matches_oracle(gpu, oracle_mod, n, dim, b, k):
         _assert_same(_run(idx, qs, k, gpu), ref, k)
 
 
+@pytest.mark.parametrize("b", [63, 64, 65, 128, 129, 256, 257])
+def test_batch_size_boundaries(gpu, oracle_mod, b):
+    """Query counts at the scan-form boundaries: one 64-query pass, the XCD-grouped multi-block
+    scan (65-128), the tiled scan with one / two 256-query blocks."""
+    rows = oracle_mod.unit_fp16(3000, 1024, seed=40 + b)
+    qs = oracle_mod.unit_fp16(b, 1024, seed=41 + b)
+    idx = _index(rows, gpu, base=5)
+    _assert_same(_run(idx, qs, 5, gpu), oracle_mod.dense_topk(rows, qs, 5, ordinal_base=5), 5)
+
+
+@pytest.mark.parametrize("n,b", [(20000, 32), (20000, 200)])
+def test_max_k(gpu, oracle_mod, n, b):
+    """k = 240 (MAX_K), on the 64-query scan and on the tiled scan."""
+    from audio_rag_amd.retrieval.device import MAX_K
+
+    rows = oracle_mod.unit_fp16(n, 1024, seed=50 + b)
+    qs = oracle_mod.unit_fp16(b, 1024, seed=51 + b)
+    idx = _index(rows, gpu)
+    _assert_same(_run(idx, qs, MAX_K, gpu), oracle_mod.dense_topk(rows, qs, MAX_K), MAX_K)
+
+
 def test_fast_path_certifies(gpu, oracle_mod):
     """The MFMA scan + exact rescore must certify random queries itself (the exact fallback
     would otherwise hide a broken fast path)."""

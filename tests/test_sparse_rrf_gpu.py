@@ -173,3 +173,13 @@ def test_sparse_pass_with_many_distinct_terms(gpu, oracle_mod):
         got = _run(idx, (qi, qx, qv), k, gpu)
         _same(got, oracle_mod.sparse_topk(*csr, qi, qx, qv, k))
         assert (got["count"] > 0).all()
+
+
+def test_sparse_max_k_and_several_passes(gpu, oracle_mod):
+    """k = 240 (MAX_K) over 150 queries: three 64-query passes, the last one partial."""
+    from audio_rag_amd.retrieval.device import MAX_K
+
+    csr = oracle_mod.sparse_corpus(8000, seed=61)
+    q = oracle_mod.sparse_queries(150, seed=62)
+    idx = _sparse_index(csr, gpu, base=3)
+    _same(_run(idx, q, MAX_K, gpu), oracle_mod.sparse_topk(*csr, *q, MAX_K, ordinal_base=3))
