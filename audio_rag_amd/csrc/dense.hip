@@ -92,7 +92,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
-    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
+    int guard) {
   constexpr int KSTEPS = DIM / 16;
   // workgroup -> (64-query block qb, tile range rp). With several blocks, the blocks of one range
   // get workgroup ids congruent mod 8, i.e. the same XCD: they stream the same rows at about the
@@ -203,33 +204,46 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
         const float4 v = *reinterpret_cast<const float4*>(inv_norm32 + row0 + 8 * q + 4 * h);
         inv[4 * q + 0] = v.x; inv[4 * q + 1] = v.y; inv[4 * q + 2] = v.z; inv[4 * q + 3] = v.w;
       }
-      uint32_t mbits = 0xffffffffu;
-      if (row_mask) mbits = (uint32_t)(row_mask[row0 >> 6] >> (row0 & 63));
+      // Invalid rows carry a NaN inverse norm, filtered rows get one here: a NaN score never
+      // enters a lane list (x > s is false) and fmaxf ignores it in the maxima and the bound,
+      // i.e. the lists and bounds of a -inf score without per-score tests.
+      if (row_mask) {
+        const uint32_t mbits = (uint32_t)(row_mask[row0 >> 6] >> (row0 & 63));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (!((mbits >> ((j & 3) + 8 * (j >> 2) + 4 * h)) & 1u)) inv[j] = __builtin_nanf("");
+      }
       float x0[16], x1[16];
       float mx0 = kNegInf, mx1 = kNegInf;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const int rt = (j & 3) + 8 * (j >> 2) + 4 * h;
-        const float a0 = acc0[j] * inv[j];
-        const float a1 = acc1[j] * inv[j];
-        const bool ok = ((mbits >> rt) & 1u) && (a0 == a0) && (a1 == a1);
-        x0[j] = ok ? a0 : kNegInf;
-        x1[j] = ok ? a1 : kNegInf;
+        x0[j] = acc0[j] * inv[j];
+        x1[j] = acc1[j] * inv[j];
         mx0 = fmaxf(mx0, x0[j]);
         mx1 = fmaxf(mx1, x1[j]);
       }
       const int32_t rbase = (int32_t)row0 + 4 * h;
       if (__any(mx0 > s0[kLaneList - 1])) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(x0[j] > s0[kLaneList - 1])) {
+            d0 = fmaxf(d0, x0[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
           topm_insert<kLaneList>(x0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+        }
       } else {
         d0 = fmaxf(d0, mx0);
       }
       if (__any(mx1 > s1[kLaneList - 1])) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(x1[j] > s1[kLaneList - 1])) {
+            d1 = fmaxf(d1, x1[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
           topm_insert<kLaneList>(x1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+        }
       } else {
         d1 = fmaxf(d1, mx1);
       }
@@ -313,7 +327,7 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
     int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
   constexpr int KT = DIM / 64;  // k-steps per row tile
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][kGStage]
@@ -436,15 +450,25 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
       }
       if (__any(mx0 > s0[kLaneList - 1])) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(y0[j] > s0[kLaneList - 1])) {
+            d0 = fmaxf(d0, y0[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
           topm_insert<kLaneList>(y0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+        }
       } else {
         d0 = fmaxf(d0, mx0);
       }
       if (__any(mx1 > s1[kLaneList - 1])) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(y1[j] > s1[kLaneList - 1])) {
+            d1 = fmaxf(d1, y1[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
           topm_insert<kLaneList>(y1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+        }
       } else {
         d1 = fmaxf(d1, mx1);
       }
@@ -526,6 +550,317 @@ constexpr size_t gemm_scan_lds_bytes() {
   constexpr size_t stages = (size_t)2 * kGStage * 2;
   constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
   return stages > lists ? stages : lists;
+}
+
+// LDS-DMA tiled scan (the default form of the multi-block scan; the register-staged
+// dense_gemm_scan_kernel above is kept for A/B, ARMI_GEMM_STAGE=reg). Same output layout.
+//   workgroup = (256-query block, row range); tile = 256 rows x 256 queries; 8 waves as
+//   2 (row groups of 128) x 4 (query groups of 64); per wave 4 x 2 v_mfma_f32_32x32x16_f16
+//   accumulators (128 VGPRs). The bigger tile halves the staged bytes per MFMA of the 128-row
+//   form: per 32-wide k-step a stage is 32 KB for 256 MFMAs per workgroup.
+//   Staging is global_load_lds_dwordx4 straight into four LDS stages ([256 rows][32] +
+//   [256 queries][32] fp16 images with 64-B rows, plus [8 waves][64] fp32 inverse norms), so
+//   three k-steps are in flight across each barrier (~100 KB per CU) and no VGPRs or ds_write
+//   pass are spent on staging. A wave-instruction writes 1 KB = 16 image rows lane-linearly;
+//   chunk c (16 B) of image row ir sits in slot c ^ ((ir >> 2) & 3): the swizzle is applied to
+//   the lanes' global source addresses and puts every ds_read_b128 lane group of the fragment
+//   reads on 16 distinct 16-B bank slots.
+//   Per k-step s (raw s_barrier, counted vmcnt, never vmcnt(0) in steady state): issue stage
+//   s+3 into buffer (s+3)%4 (last read in step s-1, before the previous barrier) -> MFMAs of
+//   stage s (+ the tile epilogue after its last k-step) -> vmcnt(10) retires this wave's stage
+//   s+1 -> barrier.
+constexpr int kG2Rows = 256;                                    // rows per tile
+constexpr int kG2Img = (kG2Rows + kGQB) * 64;                   // image bytes per stage
+constexpr int kG2StageBytes = kG2Img + kWaves * 64 * 4;         // + inverse norms
+constexpr int kG2Stages = 4;
+constexpr int kG2Pieces = (kG2Rows + kGQB) / 16 / kWaves;       // 1-KB pieces per wave (4)
+static_assert(kG2Pieces == 4, "vmcnt counts below assume 4 + 1 loads per wave and stage");
+
+template <int DIM>
+constexpr size_t gemm_glds_lds_bytes() {
+  constexpr size_t stages = (size_t)kG2Stages * kG2StageBytes;
+  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
+  return stages > lists ? stages : lists;
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int DIM>
+__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
+    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard, int ablate) {
+  constexpr int KT = DIM / 32;  // k-steps per row tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int id = blockIdx.x;
+  int qb, rp;
+  if (n_qb == 2) {
+    qb = (id >> 3) & 1;
+    rp = (id >> 4) * 8 + (id & 7);
+  } else {
+    qb = id % n_qb;
+    rp = id / n_qb;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int64_t lo = (int64_t)rp * rows_per_range;
+  const int64_t hi = min(lo + rows_per_range, n_rows);
+  const int q_base = qb * kGQB;
+
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int wq = wave & 3;   // query group: queries wq*64 + n*32 + r
+  const int wr = wave >> 2;  // row group: rows wr*128 + m*32 + ...
+  const int swz = (r >> 2) & 3;  // the swizzle of every image row this lane reads
+
+  float s0[kLaneList], s1[kLaneList];
+  int32_t i0[kLaneList], i1[kLaneList];
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
+  }
+  float d0 = kNegInf, d1 = kNegInf;
+
+  // Wave piece p covers image rows 16 * (p * 8 + wave) + lane / 4: pieces 0-15 are the tile's
+  // corpus rows, 16-31 the query block. Lane slot lane % 4 holds chunk (lane % 4) ^ swizzle.
+  const int pr = lane >> 2;
+  // piece p < 4 of stage st (16 image rows), p == 4: the stage's inverse norms (tile rows
+  // (wave & 3) * 64 + lane, one fp32 per lane)
+  auto issue_piece = [&](int64_t st, int p) {
+    const int64_t tn = st / KT;
+    const int t = (int)(st - tn * KT);
+    const int64_t row0 = lo + tn * kG2Rows;
+    unsigned char* base = smem + (int)(st & (kG2Stages - 1)) * kG2StageBytes;
+    if (p == kG2Pieces) {
+      const int64_t nr = min(row0 + (wave & 3) * 64 + lane, n_rows - 1);
+      __builtin_amdgcn_global_load_lds(inv_norm32 + nr, (lds_ptr_t)(base + kG2Img + wave * 256),
+                                       4, 0, 0);
+      return;
+    }
+    const int piece = p * kWaves + wave;
+    const int ir = piece * 16 + pr;
+    const int c = (lane & 3) ^ ((ir >> 2) & 3);
+    const uint16_t* src;
+    if (p < 2) {
+      const int64_t row = min(((ablate & 8) ? lo : row0) + ir, n_rows - 1);
+      src = rows + row * DIM + 32 * t + 8 * c;
+    } else {
+      const int q = min(q_base + ir - kG2Rows, nq - 1);
+      src = queries + (size_t)q * DIM + 32 * t + 8 * c;
+    }
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(base + piece * 1024), 16, 0, 0);
+  };
+  auto issue_stage = [&](int64_t st) {
+#pragma unroll
+    for (int p = 0; p <= kG2Pieces; ++p) issue_piece(st, p);
+  };
+
+  const int64_t n_tiles = (hi - lo + kG2Rows - 1) / kG2Rows;
+  const int64_t n_steps = n_tiles * KT;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) { acc[m][0] = f32x16{}; acc[m][1] = f32x16{}; }
+
+  auto epilogue = [&](int64_t tile, const unsigned char* base) {
+    const int64_t row0 = lo + tile * kG2Rows + wr * 128;
+    const bool full = lo + (tile + 1) * kG2Rows <= hi;  // workgroup-uniform
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      // Inverse norms by inline asm: for a plain LDS read hipcc cannot tell the in-flight
+      // LDS-DMA writes of the other stages apart and emits vmcnt(0), draining the pipeline once
+      // per tile. This stage was retired by the vmcnt + barrier before this step.
+      const uint32_t linv = (uint32_t)(uintptr_t)(lds_ptr_t)(
+          base + kG2Img + (wr * 2 + (m >> 1)) * 256 + ((m & 1) * 32 + 4 * h) * 4);
+      u32x4 invw[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int64_t rb = row0 + m * 32;
+      float inv[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        inv[4 * g + 0] = __uint_as_float(invw[g].x);
+        inv[4 * g + 1] = __uint_as_float(invw[g].y);
+        inv[4 * g + 2] = __uint_as_float(invw[g].z);
+        inv[4 * g + 3] = __uint_as_float(invw[g].w);
+      }
+      // Rows past the range and rows the filter drops get a NaN scale. A NaN score never enters
+      // a lane list (x > s is false), and fmaxf ignores it in the maxima and the bound: the
+      // same lists and bounds as a -inf score, without per-score tests on full tiles.
+      if (!full) {
+        const int lim = (int)max<int64_t>(0, min<int64_t>(32, hi - rb));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if ((j & 3) + 8 * (j >> 2) + 4 * h >= lim) inv[j] = __builtin_nanf("");
+      }
+      if (row_mask) {
+        const uint32_t mbits = rb < hi ? (uint32_t)(row_mask[rb >> 6] >> (rb & 63)) : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (!((mbits >> ((j & 3) + 8 * (j >> 2) + 4 * h)) & 1u)) inv[j] = __builtin_nanf("");
+      }
+      const int32_t rbase = (int32_t)rb + 4 * h;
+      float y0[16], y1[16];
+      float mx0 = kNegInf, mx1 = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        y0[j] = acc[m][0][j] * inv[j];
+        y1[j] = acc[m][1][j] * inv[j];
+        mx0 = fmaxf(mx0, y0[j]);
+        mx1 = fmaxf(mx1, y1[j]);
+      }
+      if (__any(mx0 > s0[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(y0[j] > s0[kLaneList - 1])) {
+            d0 = fmaxf(d0, y0[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
+          topm_insert<kLaneList>(y0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+        }
+      } else {
+        d0 = fmaxf(d0, mx0);
+      }
+      if (__any(mx1 > s1[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(y1[j] > s1[kLaneList - 1])) {
+            d1 = fmaxf(d1, y1[j]);
+            continue;
+          }
+          topm_insert<kLaneList>(y1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+        }
+      } else {
+        d1 = fmaxf(d1, mx1);
+      }
+      acc[m][0] = f32x16{};
+      acc[m][1] = f32x16{};
+    }
+  };
+
+  // MFMAs of stage st with the issue of stage st+3 (when `more`) spread between them: issuing
+  // the five LDS-DMA loads as one block after the barrier kept every wave's fragment reads and
+  // MFMAs waiting behind them.
+  auto compute = [&](int64_t st, bool more) {
+    const int64_t tile = st / KT;
+    const int t = (int)(st - tile * KT);
+    const unsigned char* base = smem + (int)(st & (kG2Stages - 1)) * kG2StageBytes;
+    const unsigned char* xs = base + (wr * 128 + r) * 64;
+    const unsigned char* qs = base + (kG2Rows + wq * 64 + r) * 64;
+    const int off0 = (h ^ swz) << 4, off1 = ((2 + h) ^ swz) << 4;
+    u32x4 a[4], b[2], a1[4], b1[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) b[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * 64 + off0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const u32x4*>(xs + m * 32 * 64 + off0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
+      if (more) issue_piece(st + 3, m);
+      if (m == 1) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          b1[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * 64 + off1);
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm)
+          a1[mm] = *reinterpret_cast<const u32x4*>(xs + mm * 32 * 64 + off1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) issue_piece(st + 3, kG2Pieces);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a1[m], b1[n], acc[m][n]);
+    if (t == KT - 1) epilogue(tile, base);
+  };
+
+  if (n_steps > 0) {
+    issue_stage(0);
+    if (n_steps > 1) issue_stage(1);
+    if (n_steps > 2) issue_stage(2);
+    if (n_steps > 2) {
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else if (n_steps > 1) {
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int64_t st = 0; st < n_steps; ++st) {
+      compute(st, st + 3 < n_steps);  // workgroup-uniform
+      // retire stage st+1: the stages issued after it may stay in flight
+      const int64_t later = min<int64_t>(n_steps - 1, st + 3) - (st + 1);
+      if (later >= 2) {
+        asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+      } else if (later == 1) {
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+
+  // workgroup lists: per query the 16 entries of (row group, lane half, 4), sorted (the layout
+  // of dense_gemm_scan_kernel)
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
+  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);      // [256][4]
+  {
+    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
+    const int slot = (wr * 2 + h) * kLaneList;
+#pragma unroll
+    for (int j = 0; j < kLaneList; ++j) {
+      lkey[qa * 16 + slot + j] = s0[j];
+      lrow[qa * 16 + slot + j] = i0[j];
+      lkey[qc * 16 + slot + j] = s1[j];
+      lrow[qc * 16 + slot + j] = i1[j];
+    }
+    ldisc[qa * 4 + wr * 2 + h] = d0;
+    ldisc[qc * 4 + wr * 2 + h] = d1;
+  }
+  __syncthreads();
+  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
+    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
+    float key = lkey[ql * 16 + (lane & 15)];
+    int32_t row = lrow[ql * 16 + (lane & 15)];
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const float ok = __shfl_xor(key, stride);
+        const int32_t orow = __shfl_xor(row, stride);
+        const bool lower = (lane & stride) == 0;
+        const bool desc = (lane & size) == 0;
+        const bool other_better = armi::approx_better(ok, orow, key, row);
+        const bool take_other = (lower == desc) ? other_better : !other_better;
+        if (take_other) { key = ok; row = orow; }
+      }
+    }
+    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
+    const int qg = q_base + ql;
+    if (qg < nq) {
+      const size_t base = (size_t)rp * nq + qg;
+      cand_key[base * kKW + rank] = key;
+      cand_row[base * kKW + rank] = row;
+      if (rank == 0) {
+        const float* dd = ldisc + ql * 4;
+        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
+      }
+    }
+  }
 }
 
 
@@ -1011,6 +1346,37 @@ bool use_gemm_scan(int nq) {
   return nq > 2 * kQB;
 }
 
+// Staging of the tiled scan: LDS-DMA (default) or registers. ARMI_GEMM_STAGE=reg|glds forces
+// one of them (A/B measurements).
+bool use_glds_staging() {
+  static const bool glds = [] {
+    const char* e = getenv("ARMI_GEMM_STAGE");
+    return !(e && e[0] == 'r');
+  }();
+  return glds;
+}
+
+// Lane-list epilogues skip (wave-uniformly) the insertion of a score no lane list takes, instead
+// of running the insertion network on all 16 scores of a tile; ARMI_INSERT_GUARD=0 disables it
+// (A/B). Both forms produce identical lists and bounds.
+int insert_guard() {
+  static const int g = [] {
+    const char* e = getenv("ARMI_INSERT_GUARD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return g;
+}
+
+// Diagnostic ablation of the LDS-DMA tiled scan (results are wrong when set): ARMI_GEMM_ABLATE=8
+// re-reads the range's first row tile instead of streaming the range (row loads hit L2).
+int gemm_ablate() {
+  static const int a = [] {
+    const char* e = getenv("ARMI_GEMM_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return a;
+}
+
 struct GemmPlan {
   int n_qb = 0;
   int n_ranges = 0;
@@ -1156,15 +1522,31 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   if (use_gemm_scan(nq)) {
     const GemmPlan gp = plan_gemm(idx, nq);
     n_wg = gp.n_ranges;
-    if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
+    const bool glds = use_glds_staging();
+    if (glds) {
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM>, gemm_glds_lds_bytes<DIM>()))
+        return rc;
+    } else {
+      if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
+    }
     std::pair<hipEvent_t, hipEvent_t> ev;
     const int timed = timing_begin(stream, &ev);
     if (timed < 0) return ARMI_ERR_HIP;
-    dense_gemm_scan_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads), gemm_scan_lds_bytes<DIM>(),
-                                  stream>>>(idx->rows, idx->inv_norm32, row_mask, idx->n_rows,
-                                            gp.rows_per_range, gp.n_ranges, gp.n_qb, queries, nq,
-                                            w.cand_key, w.cand_row, w.cand_bound);
-    ARMI_LAUNCHED("dense_gemm_scan_kernel");
+    if (glds) {
+      dense_gemm_scan_glds_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads),
+                                         gemm_glds_lds_bytes<DIM>(), stream>>>(
+          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
+          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
+          gemm_ablate());
+      ARMI_LAUNCHED("dense_gemm_scan_glds_kernel");
+    } else {
+      dense_gemm_scan_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads), gemm_scan_lds_bytes<DIM>(),
+                                    stream>>>(idx->rows, idx->inv_norm32, row_mask, idx->n_rows,
+                                              gp.rows_per_range, gp.n_ranges, gp.n_qb, queries,
+                                              nq, w.cand_key, w.cand_row, w.cand_bound,
+                                              insert_guard());
+      ARMI_LAUNCHED("dense_gemm_scan_kernel");
+    }
     if (timed == 1)
       if (int rc = timing_end(stream, ev)) return rc;
   } else {
@@ -1174,7 +1556,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (timed < 0) return ARMI_ERR_HIP;
     dense_scan_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
         idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
     ARMI_LAUNCHED("dense_scan_kernel");
     if (timed == 1)
       if (int rc = timing_end(stream, ev)) return rc;

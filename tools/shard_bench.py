@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--gs", default="1,2,4,8")
     args = ap.parse_args()
     from bench import make_queries, make_rows
+    from audio_rag_amd import _armi
     from audio_rag_amd.retrieval.device import DenseIndex
 
     dev = torch.device("cuda", 0)
@@ -36,15 +37,24 @@ def main():
             out = idx.topk(q, args.k, workspace=ws)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tot = _armi.ctypes.c_double()
+        launches = _armi.ctypes.c_int64()
+        _armi.call("armi_scan_timing_enable", 1)
+        _armi.call("armi_scan_timing_read", _armi.ctypes.byref(tot), _armi.ctypes.byref(launches))
         a.record()
         for _ in range(args.iters):
             out = idx.topk(q, args.k, workspace=ws)
         b.record()
         torch.cuda.synchronize()
+        _armi.call("armi_scan_timing_read", _armi.ctypes.byref(tot), _armi.ctypes.byref(launches))
+        _armi.call("armi_scan_timing_enable", 0)
         ms = a.elapsed_time(b) / args.iters
+        scan_ms = tot.value / max(launches.value, 1)
+        tflops = 2.0 * n * 1024 * 64 * g / (scan_ms * 1e-3) / 1e12
         cert = float((out.flags == 1).float().mean().item())
         print(f"G={g} shard_rows={n} queries={64 * g} k={args.k}: {ms * 1e3:.1f} us per call, "
-              f"{64 * g / (ms * 1e-3):.0f} q/s per GPU, certified {cert:.3f}", flush=True)
+              f"{64 * g / (ms * 1e-3):.0f} q/s per GPU, certified {cert:.3f}; scan kernel "
+              f"{scan_ms * 1e3:.1f} us ({tflops:.0f} TFLOP/s)", flush=True)
         del idx, rows, ws
 
 
