@@ -569,29 +569,40 @@ constexpr size_t gemm_scan_lds_bytes() {
 //   s+3 into buffer (s+3)%4 (last read in step s-1, before the previous barrier) -> MFMAs of
 //   stage s (+ the tile epilogue after its last k-step) -> vmcnt(10) retires this wave's stage
 //   s+1 -> barrier.
-constexpr int kG2Rows = 256;                                    // rows per tile
-constexpr int kG2Img = (kG2Rows + kGQB) * 64;                   // image bytes per stage
-constexpr int kG2StageBytes = kG2Img + kWaves * 64 * 4;         // + inverse norms
-constexpr int kG2Stages = 4;
-constexpr int kG2Pieces = (kG2Rows + kGQB) / 16 / kWaves;       // 1-KB pieces per wave (4)
-static_assert(kG2Pieces == 4, "vmcnt counts below assume 4 + 1 loads per wave and stage");
+constexpr int kG2Rows = 256;  // rows per tile
+// Geometry per k-step width KS (32: four stages, three in flight; 64: two stages of full 128-B
+// row segments, one in flight).
+template <int KS>
+struct G2 {
+  static constexpr int Img = (kG2Rows + kGQB) * KS * 2;           // image bytes per stage
+  static constexpr int StageBytes = Img + kWaves * 64 * 4;         // + inverse norms
+  static constexpr int Stages = KS == 32 ? 4 : 2;
+  static constexpr int Ahead = Stages - 1;                         // stages issued ahead
+  static constexpr int RowsPerPiece = 1024 / (KS * 2);             // image rows per 1-KB piece
+  static constexpr int Pieces = (kG2Rows + kGQB) / RowsPerPiece / kWaves;  // per wave: 4 / 8
+  static constexpr int Chunks = KS / 8;                            // 16-B chunks per image row
+  static constexpr int SwzShift = KS == 32 ? 2 : 1;
+  static constexpr int Subs = KS / 16;
+};
+static_assert(G2<32>::Pieces == 4 && G2<64>::Pieces == 8, "vmcnt counts below");
 
-template <int DIM>
+template <int DIM, int KS>
 constexpr size_t gemm_glds_lds_bytes() {
-  constexpr size_t stages = (size_t)kG2Stages * kG2StageBytes;
+  constexpr size_t stages = (size_t)G2<KS>::Stages * G2<KS>::StageBytes;
   constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
   return stages > lists ? stages : lists;
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int DIM>
+template <int DIM, int KS>
 __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
     int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
     int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard, int ablate) {
-  constexpr int KT = DIM / 32;  // k-steps per row tile
+  using GG = G2<KS>;
+  constexpr int KT = DIM / KS;  // k-steps per row tile
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int id = blockIdx.x;
@@ -615,7 +626,8 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
   const int h = lane >> 5;
   const int wq = wave & 3;   // query group: queries wq*64 + n*32 + r
   const int wr = wave >> 2;  // row group: rows wr*128 + m*32 + ...
-  const int swz = (r >> 2) & 3;  // the swizzle of every image row this lane reads
+  // the swizzle of every image row this lane reads (rows differ by multiples of 32)
+  const int swz = (r >> GG::SwzShift) & (GG::Chunks - 1);
 
   float s0[kLaneList], s1[kLaneList];
   int32_t i0[kLaneList], i1[kLaneList];
@@ -627,36 +639,36 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
 
   // Wave piece p covers image rows 16 * (p * 8 + wave) + lane / 4: pieces 0-15 are the tile's
   // corpus rows, 16-31 the query block. Lane slot lane % 4 holds chunk (lane % 4) ^ swizzle.
-  const int pr = lane >> 2;
+  const int pr = lane / GG::Chunks;
   // piece p < 4 of stage st (16 image rows), p == 4: the stage's inverse norms (tile rows
   // (wave & 3) * 64 + lane, one fp32 per lane)
   auto issue_piece = [&](int64_t st, int p) {
     const int64_t tn = st / KT;
     const int t = (int)(st - tn * KT);
     const int64_t row0 = lo + tn * kG2Rows;
-    unsigned char* base = smem + (int)(st & (kG2Stages - 1)) * kG2StageBytes;
-    if (p == kG2Pieces) {
+    unsigned char* base = smem + (int)(st & (GG::Stages - 1)) * GG::StageBytes;
+    if (p == GG::Pieces) {
       const int64_t nr = min(row0 + (wave & 3) * 64 + lane, n_rows - 1);
-      __builtin_amdgcn_global_load_lds(inv_norm32 + nr, (lds_ptr_t)(base + kG2Img + wave * 256),
+      __builtin_amdgcn_global_load_lds(inv_norm32 + nr, (lds_ptr_t)(base + GG::Img + wave * 256),
                                        4, 0, 0);
       return;
     }
     const int piece = p * kWaves + wave;
-    const int ir = piece * 16 + pr;
-    const int c = (lane & 3) ^ ((ir >> 2) & 3);
+    const int ir = piece * GG::RowsPerPiece + pr;
+    const int c = (lane & (GG::Chunks - 1)) ^ ((ir >> GG::SwzShift) & (GG::Chunks - 1));
     const uint16_t* src;
-    if (p < 2) {
+    if (ir < kG2Rows) {  // wave-uniform: pieces never straddle the row / query images
       const int64_t row = min(((ablate & 8) ? lo : row0) + ir, n_rows - 1);
-      src = rows + row * DIM + 32 * t + 8 * c;
+      src = rows + row * DIM + KS * t + 8 * c;
     } else {
       const int q = min(q_base + ir - kG2Rows, nq - 1);
-      src = queries + (size_t)q * DIM + 32 * t + 8 * c;
+      src = queries + (size_t)q * DIM + KS * t + 8 * c;
     }
     __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(base + piece * 1024), 16, 0, 0);
   };
   auto issue_stage = [&](int64_t st) {
 #pragma unroll
-    for (int p = 0; p <= kG2Pieces; ++p) issue_piece(st, p);
+    for (int p = 0; p <= GG::Pieces; ++p) issue_piece(st, p);
   };
 
   const int64_t n_tiles = (hi - lo + kG2Rows - 1) / kG2Rows;
@@ -674,7 +686,7 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
       // LDS-DMA writes of the other stages apart and emits vmcnt(0), draining the pipeline once
       // per tile. This stage was retired by the vmcnt + barrier before this step.
       const uint32_t linv = (uint32_t)(uintptr_t)(lds_ptr_t)(
-          base + kG2Img + (wr * 2 + (m >> 1)) * 256 + ((m & 1) * 32 + 4 * h) * 4);
+          base + GG::Img + (wr * 2 + (m >> 1)) * 256 + ((m & 1) * 32 + 4 * h) * 4);
       u32x4 invw[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -750,56 +762,45 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
   auto compute = [&](int64_t st, bool more) {
     const int64_t tile = st / KT;
     const int t = (int)(st - tile * KT);
-    const unsigned char* base = smem + (int)(st & (kG2Stages - 1)) * kG2StageBytes;
-    const unsigned char* xs = base + (wr * 128 + r) * 64;
-    const unsigned char* qs = base + (kG2Rows + wq * 64 + r) * 64;
-    const int off0 = (h ^ swz) << 4, off1 = ((2 + h) ^ swz) << 4;
-    u32x4 a[4], b[2], a1[4], b1[2];
+    const unsigned char* base = smem + (int)(st & (GG::Stages - 1)) * GG::StageBytes;
+    const unsigned char* xs = base + (wr * 128 + r) * (KS * 2);
+    const unsigned char* qs = base + (kG2Rows + wq * 64 + r) * (KS * 2);
+    u32x4 a[2][4], b[2][2];  // fragments of sub-steps sub (cur) and sub + 1 (nxt)
+    auto load_frags = [&](int sub, u32x4 (&fa)[4], u32x4 (&fb)[2]) {
+      const int off = ((2 * sub + h) ^ swz) << 4;
 #pragma unroll
-    for (int n = 0; n < 2; ++n) b[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * 64 + off0);
+      for (int n = 0; n < 2; ++n)
+        fb[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * (KS * 2) + off);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const u32x4*>(xs + m * 32 * 64 + off0);
+      for (int m = 0; m < 4; ++m)
+        fa[m] = *reinterpret_cast<const u32x4*>(xs + m * 32 * (KS * 2) + off);
+    };
+    load_frags(0, a[0], b[0]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int sub = 0; sub < GG::Subs; ++sub) {
+      const int cur = sub & 1;
 #pragma unroll
-      for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
-      if (more) issue_piece(st + 3, m);
-      if (m == 1) {
+      for (int m = 0; m < 4; ++m) {
+        if (ablate & 32) {
+          asm volatile("" :: "v"(a[cur][m]), "v"(b[cur][0]), "v"(b[cur][1]));
+        } else {
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          b1[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * 64 + off1);
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm)
-          a1[mm] = *reinterpret_cast<const u32x4*>(xs + mm * 32 * 64 + off1);
+          for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a[cur][m], b[cur][n], acc[m][n]);
+        }
+        const int p = sub * 4 + m;  // the next stage's loads, spread between the MFMAs
+        if (p <= GG::Pieces && more) issue_piece(st + GG::Ahead, p);
+        if (m == 1 && sub + 1 < GG::Subs) load_frags(sub + 1, a[cur ^ 1], b[cur ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
-    if (more) issue_piece(st + 3, kG2Pieces);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a1[m], b1[n], acc[m][n]);
+    if (GG::Subs * 4 <= GG::Pieces && more) issue_piece(st + GG::Ahead, GG::Pieces);
     if (t == KT - 1) epilogue(tile, base);
   };
 
-  if (n_steps > 0) {
-    issue_stage(0);
-    if (n_steps > 1) issue_stage(1);
-    if (n_steps > 2) issue_stage(2);
-    if (n_steps > 2) {
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    } else if (n_steps > 1) {
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    for (int64_t st = 0; st < n_steps; ++st) {
-      compute(st, st + 3 < n_steps);  // workgroup-uniform
-      // retire stage st+1: the stages issued after it may stay in flight
-      const int64_t later = min<int64_t>(n_steps - 1, st + 3) - (st + 1);
+  // vmcnt for "retire the oldest outstanding stage, leave `later` younger ones in flight"
+  auto wait_stage = [&](int64_t later) {
+    if constexpr (KS == 32) {
       if (later >= 2) {
         asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
       } else if (later == 1) {
@@ -807,7 +808,27 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
       } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
-      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+  };
+  if (n_steps > 0) {
+#pragma unroll
+    for (int j = 0; j < GG::Ahead; ++j)
+      if (j < n_steps) issue_stage(j);
+    wait_stage(min<int64_t>(n_steps, GG::Ahead) - 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int64_t st = 0; st < n_steps; ++st) {
+      compute(st, st + GG::Ahead < n_steps);  // workgroup-uniform
+      // retire stage st+1: the stages issued after it may stay in flight
+      const int64_t later = min<int64_t>(n_steps - 1, st + GG::Ahead) - (st + 1);
+      if (ablate & 16) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        wait_stage(later);
+      }
+      if (!(ablate & 64)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   }
@@ -1367,8 +1388,19 @@ int insert_guard() {
   return g;
 }
 
-// Diagnostic ablation of the LDS-DMA tiled scan (results are wrong when set): ARMI_GEMM_ABLATE=8
-// re-reads the range's first row tile instead of streaming the range (row loads hit L2).
+// k-step width of the LDS-DMA tiled scan: 32 (four stages) or 64 (two stages of full 128-B row
+// segments); ARMI_GEMM_KSTEP=32|64 (A/B).
+int gemm_kstep() {
+  static const int k = [] {
+    const char* e = getenv("ARMI_GEMM_KSTEP");
+    return (e && atoi(e) == 64) ? 64 : 32;
+  }();
+  return k;
+}
+
+// Diagnostic ablations of the LDS-DMA tiled scan (results are wrong when set), ARMI_GEMM_ABLATE
+// bits: 8 re-reads the range's first row tile (row loads hit L2), 16 skips the vmcnt waits,
+// 32 the MFMAs, 64 the per-step barrier.
 int gemm_ablate() {
   static const int a = [] {
     const char* e = getenv("ARMI_GEMM_ABLATE");
@@ -1524,7 +1556,9 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     n_wg = gp.n_ranges;
     const bool glds = use_glds_staging();
     if (glds) {
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM>, gemm_glds_lds_bytes<DIM>()))
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32>, gemm_glds_lds_bytes<DIM, 32>()))
+        return rc;
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 64>, gemm_glds_lds_bytes<DIM, 64>()))
         return rc;
     } else {
       if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
@@ -1533,8 +1567,11 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     const int timed = timing_begin(stream, &ev);
     if (timed < 0) return ARMI_ERR_HIP;
     if (glds) {
-      dense_gemm_scan_glds_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads),
-                                         gemm_glds_lds_bytes<DIM>(), stream>>>(
+      auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64>
+                                     : dense_gemm_scan_glds_kernel<DIM, 32>;
+      const size_t lds = gemm_kstep() == 64 ? gemm_glds_lds_bytes<DIM, 64>()
+                                            : gemm_glds_lds_bytes<DIM, 32>();
+      kern<<<dim3(gp.grid), dim3(kGThreads), lds, stream>>>(
           idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
           gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
           gemm_ablate());

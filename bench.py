@@ -408,7 +408,8 @@ def main() -> None:
         "certified_frac": certified,
         "roofline": ({
             "bound": "hbm",
-            "kernel": "dense_scan_kernel<1024>" if nq_scan <= 64 else "dense_gemm_scan_kernel<1024>",
+            "kernel": ("dense_scan_kernel<1024>" if nq_scan <= 128
+                       else "dense_gemm_scan_glds_kernel<1024>"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -419,7 +420,7 @@ def main() -> None:
             "launches_timed": launches.value,
         } if not mfma_bound else {
             "bound": "mfma",
-            "kernel": "dense_gemm_scan_kernel<1024>",
+            "kernel": "dense_gemm_scan_glds_kernel<1024>",
             "achieved": alg_flops / (scan_avg_ms * 1e-3) / 1e12,
             "peak": MFMA_PEAK_TFLOPS["fp16"],
             "unit": "TFLOP/s",
