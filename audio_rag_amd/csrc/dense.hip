@@ -595,7 +595,9 @@ constexpr size_t gemm_glds_lds_bytes() {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int DIM, int KS>
+// ABL: the diagnostic instantiation that honours `ablate`; the production one (ABL = false)
+// compiles the switches out, so no branch sits between the MFMAs.
+template <int DIM, int KS, bool ABL>
 __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
     const int c = (lane & (GG::Chunks - 1)) ^ ((ir >> GG::SwzShift) & (GG::Chunks - 1));
     const uint16_t* src;
     if (ir < kG2Rows) {  // wave-uniform: pieces never straddle the row / query images
-      const int64_t row = min(((ablate & 8) ? lo : row0) + ir, n_rows - 1);
+      const int64_t row = min(((ABL && (ablate & 8)) ? lo : row0) + ir, n_rows - 1);
       src = rows + row * DIM + KS * t + 8 * c;
     } else {
       const int q = min(q_base + ir - kG2Rows, nq - 1);
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
       const int cur = sub & 1;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        if (ablate & 32) {
+        if (ABL && (ablate & 32)) {
           asm volatile("" :: "v"(a[cur][m]), "v"(b[cur][0]), "v"(b[cur][1]));
         } else {
 #pragma unroll
@@ -812,29 +814,33 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
   };
+  // Stages past the last k-step are issued too: their rows / queries are clamped in-bounds and
+  // land in the buffer of the step before (read before the previous barrier), nobody reads them,
+  // and every wait keeps the same count, so the k-step loop carries no issue branches.
   if (n_steps > 0) {
 #pragma unroll
-    for (int j = 0; j < GG::Ahead; ++j)
-      if (j < n_steps) issue_stage(j);
-    wait_stage(min<int64_t>(n_steps, GG::Ahead) - 1);
+    for (int j = 0; j < GG::Ahead; ++j) issue_stage(j);
+    wait_stage(GG::Ahead - 1);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     for (int64_t st = 0; st < n_steps; ++st) {
-      compute(st, st + GG::Ahead < n_steps);  // workgroup-uniform
-      // retire stage st+1: the stages issued after it may stay in flight
-      const int64_t later = min<int64_t>(n_steps - 1, st + GG::Ahead) - (st + 1);
-      if (ablate & 16) {
+      compute(st, true);
+      // retire stage st+1: the stages issued after it stay in flight
+      const int64_t later = GG::Ahead - 1;
+      if (ABL && (ablate & 16)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
         wait_stage(later);
       }
-      if (!(ablate & 64)) __builtin_amdgcn_s_barrier();
+      if (!(ABL && (ablate & 64))) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   }
 
   // workgroup lists: per query the 16 entries of (row group, lane half, 4), sorted (the layout
-  // of dense_gemm_scan_kernel)
+  // of dense_gemm_scan_kernel). The tail stages' LDS-DMA writes must land before the stage
+  // buffers are reused.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
   int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
@@ -1556,9 +1562,14 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     n_wg = gp.n_ranges;
     const bool glds = use_glds_staging();
     if (glds) {
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32>, gemm_glds_lds_bytes<DIM, 32>()))
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32, false>,
+                             gemm_glds_lds_bytes<DIM, 32>()))
         return rc;
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 64>, gemm_glds_lds_bytes<DIM, 64>()))
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 64, false>,
+                             gemm_glds_lds_bytes<DIM, 64>()))
+        return rc;
+      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32, true>,
+                             gemm_glds_lds_bytes<DIM, 32>()))
         return rc;
     } else {
       if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
@@ -1567,8 +1578,9 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     const int timed = timing_begin(stream, &ev);
     if (timed < 0) return ARMI_ERR_HIP;
     if (glds) {
-      auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64>
-                                     : dense_gemm_scan_glds_kernel<DIM, 32>;
+      auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64, false>
+                  : gemm_ablate()    ? dense_gemm_scan_glds_kernel<DIM, 32, true>
+                                     : dense_gemm_scan_glds_kernel<DIM, 32, false>;
       const size_t lds = gemm_kstep() == 64 ? gemm_glds_lds_bytes<DIM, 64>()
                                             : gemm_glds_lds_bytes<DIM, 32>();
       kern<<<dim3(gp.grid), dim3(kGThreads), lds, stream>>>(
