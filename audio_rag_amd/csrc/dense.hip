@@ -1360,7 +1360,9 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
 // Multi-block calls (more than kQB queries): up to 2 blocks the XCD-grouped dense_scan_kernel
 // (HBM-bound, rows shared through L2), beyond that the LDS-tiled dense_gemm_scan_kernel (rows
 // read once per 256 queries). Measured per-GPU call times, 1M rows / G with G*64 queries:
-// G=2 366 vs 497 us, G=4 326 vs 272-318 us, G=8 308 vs 251-269 us (grouped vs tiled).
+// G=2 366 vs 497 us, G=4 326 vs 272-318 us, G=8 308 vs 251-269 us (grouped vs register-staged
+// tiled); with the LDS-DMA tiled scan G=2 377 vs 459 us, G=4 357 vs 281 us
+// (profiles/r01f_scan_form_ab.txt), so the switch stays above two blocks.
 // ARMI_DENSE_SCAN=grouped|tiled forces one of them (A/B measurements).
 bool use_gemm_scan(int nq) {
   static const int force = [] {
