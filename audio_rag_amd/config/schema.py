@@ -4,9 +4,16 @@ The sections and defaults the hot path reads are those of src/audio_rag/config/s
 (EmbeddingConfig 48-55, RetrievalConfig 58-69, RerankingConfig 72-79, ExpansionConfig 82-85,
 GenerationConfig 88-96). Differences, all additive:
   * RetrievalConfig.backend accepts "mi355x" (the device chunk store of this package) and
-    defaults to it; "qdrant" stays a legal value so reference config files still validate.
+    defaults to it. "qdrant" (what the reference's configs/base.yaml:39 names) resolves to the
+    same MI355X store, so reference config files build a working pipeline unchanged; the Qdrant
+    connection knobs (qdrant_host / qdrant_port / qdrant_in_memory) are accepted and ignored.
   * RetrievalConfig.device / rrf_k / reproduce_sparse_drop and RerankingConfig.max_length are new
-    knobs of the MI355X backend (rrf_k = 2 is Qdrant's RRF constant).
+    knobs of the MI355X backend (rrf_k = 2 is Qdrant's RRF constant, 1/(rrf_k + pos)).
+  * reproduce_sparse_drop defaults to True: add() then stores what the reference's add() leaves
+    in Qdrant (qdrant.py:183-220 upserts dense+sparse points, then re-upserts the same ids
+    dense-only, which replaces them), so a hybrid search over a corpus ingested through add()
+    returns the reference's results. False keeps the sparse vectors (an explicit opt-in bug
+    fix, not the reference's behaviour).
 Sections of the ingestion side (asr, diarization, alignment, chunking, contextual, tts,
 resources) are accepted as free-form dicts so reference YAML files load unchanged.
 """
@@ -44,8 +51,8 @@ class RetrievalConfig(BaseModel):
     sparse_weight: float = Field(default=0.3, ge=0.0, le=1.0)  # never read (as in the reference)
     # MI355X backend
     device: int = 0
-    rrf_k: int = Field(default=2, ge=0)
-    reproduce_sparse_drop: bool = False
+    rrf_k: int = Field(default=2, ge=1)
+    reproduce_sparse_drop: bool = True
 
 
 class RerankingConfig(BaseModel):

@@ -1408,13 +1408,19 @@ int gemm_kstep() {
 
 // Diagnostic ablations of the LDS-DMA tiled scan (results are wrong when set), ARMI_GEMM_ABLATE
 // bits: 8 re-reads the range's first row tile (row loads hit L2), 16 skips the vmcnt waits,
-// 32 the MFMAs, 64 the per-step barrier.
+// 32 the MFMAs, 64 the per-step barrier. Only a probe build (-DARMI_PROBE_BUILD) reads the
+// variable and carries the ablating instantiation; the shipped library ignores it, so a stray
+// environment variable can never produce wrong certified results.
 int gemm_ablate() {
+#ifdef ARMI_PROBE_BUILD
   static const int a = [] {
     const char* e = getenv("ARMI_GEMM_ABLATE");
     return e ? atoi(e) : 0;
   }();
   return a;
+#else
+  return 0;
+#endif
 }
 
 struct GemmPlan {
@@ -1570,9 +1576,11 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
       if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 64, false>,
                              gemm_glds_lds_bytes<DIM, 64>()))
         return rc;
+#ifdef ARMI_PROBE_BUILD
       if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32, true>,
                              gemm_glds_lds_bytes<DIM, 32>()))
         return rc;
+#endif
     } else {
       if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
     }
@@ -1581,8 +1589,10 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (timed < 0) return ARMI_ERR_HIP;
     if (glds) {
       auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64, false>
-                  : gemm_ablate()    ? dense_gemm_scan_glds_kernel<DIM, 32, true>
                                      : dense_gemm_scan_glds_kernel<DIM, 32, false>;
+#ifdef ARMI_PROBE_BUILD
+      if (gemm_ablate()) kern = dense_gemm_scan_glds_kernel<DIM, 32, true>;
+#endif
       const size_t lds = gemm_kstep() == 64 ? gemm_glds_lds_bytes<DIM, 64>()
                                             : gemm_glds_lds_bytes<DIM, 32>();
       kern<<<dim3(gp.grid), dim3(kGThreads), lds, stream>>>(

@@ -114,7 +114,7 @@ extern "C" int armi_rrf_fuse(const int64_t* a_ids, const int32_t* a_count, int k
   ARMI_REQUIRE(ka >= 1 && ka <= kMaxList && kb >= 1 && kb <= kMaxList,
                "armi_rrf_fuse: list widths must be in [1, 256]");
   ARMI_REQUIRE(limit >= 1, "armi_rrf_fuse: limit must be >= 1");
-  ARMI_REQUIRE(rrf_k >= 0, "armi_rrf_fuse: rrf_k must be >= 0");
+  ARMI_REQUIRE(rrf_k >= 1, "armi_rrf_fuse: rrf_k must be >= 1 (1/(rrf_k + pos) at pos 0)");
   if (n_queries <= 0) return ARMI_OK;
   ARMI_REQUIRE(a_ids && a_count && b_ids && b_count && out_ids && out_scores && out_count,
                "armi_rrf_fuse: null pointer argument");

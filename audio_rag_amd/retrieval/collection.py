@@ -7,7 +7,9 @@ Replaces one Qdrant collection as QdrantRetriever creates and fills it
   * payload {text, start, end, speaker, metadata}                  -> host list
 Points get consecutive ordinals in upsert order (the reference's uuid4 ids are never surfaced:
 RetrievalResult carries no id, core/base.py:56-61). The device indexes are rebuilt lazily on the
-first search after an add; a built collection is read-only, so concurrent searches are safe.
+first search after an add; a built index is read-only, so concurrent searches are safe, and a
+rebuild never frees an index a running search still holds (the old handles die with their last
+reference).
 """
 
 from __future__ import annotations
@@ -102,9 +104,10 @@ class ChunkCollection:
                 t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
                 self._sparse = SparseIndex(t(indptr), t(idx), t(val), vocab)
             self._built_rows = self.count
-            for old in (old_dense, old_sparse):
-                if old is not None:
-                    old.close()
+            # The superseded indexes are not closed here: a search that fetched them before
+            # this rebuild may still be using them. Dropping the reference frees each one (its
+            # __del__ closes it) once the last such search lets go of it.
+            del old_dense, old_sparse
 
     @property
     def dense_index(self) -> DenseIndex:

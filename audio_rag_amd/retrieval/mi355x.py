@@ -322,3 +322,10 @@ class MI355XRetriever(BaseRetriever):
             return results
         except Exception as e:
             raise RetrievalError(f"Search failed in '{resolved}': {e}")
+
+
+# The reference's own configs name the backend "qdrant" (configs/base.yaml:39,
+# config/schema.py:60); in this package that key builds the MI355X chunk store, so a reference
+# deployment's YAML runs unchanged (the qdrant_host / qdrant_port / qdrant_in_memory knobs are
+# accepted and ignored).
+RetrievalRegistry.register("qdrant")(MI355XRetriever)

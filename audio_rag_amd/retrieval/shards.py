@@ -7,13 +7,19 @@ cosine key; sparse: exact fp32 score; both tie-broken by the global ordinal), so
 is the top-k of the union of per-shard top-k lists.
 
 One search step for a process group of G ranks, each bringing B queries:
-  1. all-gather the queries (RCCL over xGMI): every rank holds all G*B queries
-  2. local top-k of all G*B queries on this rank's shard (libarmi kernels)
-  3. all-gather the per-shard lists, packed as int64 [G*B, 2k] (key bits, ordinal) and
-     int32 [G*B, k+1] (score bits, count): two small collectives
-  4. merge this rank's B queries over the G shard lists (armi_topk_merge_shards)
-Hybrid search gathers and merges the dense and sparse prefetch lists, then fuses them with RRF.
-Per-GPU work is fixed as G grows (shard rows x G*B queries = corpus x B): weak scaling.
+  1. all-gather the queries (RCCL over xGMI): every rank holds all G*B queries. Dense rows and,
+     for hybrid / sparse search, the sparse query terms travel in ONE collective: each query's
+     terms are padded to MAX_QUERY_TERMS fixed slots, so the message size is known on every rank
+     without a host round trip.
+  2. local top-k of all G*B queries on this rank's shard (libarmi kernels); for hybrid the dense
+     scan runs on the caller's stream and the sparse scan on a side stream, concurrently.
+  3. all-gather the per-shard lists (dense and sparse together for hybrid), packed into one byte
+     buffer per query: one collective.
+  4. merge this rank's B queries over the G shard lists (armi_topk_merge_shards), then RRF for
+     hybrid.
+Nothing in a step waits on the host: no .item() / .tolist(), so the whole step is enqueued
+asynchronously. Per-GPU work is fixed as G grows (shard rows x G*B queries = corpus x B): weak
+scaling.
 """
 
 from __future__ import annotations
@@ -24,6 +30,8 @@ import torch
 import torch.distributed as dist
 
 from audio_rag_amd.retrieval.device import TopK
+
+MAX_QUERY_TERMS = 256  # armi_sparse_topk's per-query term capacity (include/armi.h)
 
 LocalSearch = Callable[[torch.Tensor, int], TopK]
 Merge = Callable[[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, int], TopK]
@@ -42,6 +50,71 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group) -> None:
         dist.all_gather(list(out.unbind(0)), inp, group=group)
 
 
+def _bytes(t: torch.Tensor, n: int) -> torch.Tensor:
+    """[n, ...] tensor -> its bytes as uint8 [n, row_bytes]."""
+    return t.contiguous().reshape(n, -1).view(torch.uint8)
+
+
+def pack_rows(parts: list[torch.Tensor]) -> tuple[torch.Tensor, list[tuple[int, torch.dtype, tuple]]]:
+    """Concatenates per-query tensors (leading dim n) into one uint8 [n, bytes] buffer; returns it
+    with the layout unpack_rows needs."""
+    n = int(parts[0].shape[0])
+    layout = [(int(_bytes(p, n).shape[1]), p.dtype, tuple(p.shape[1:])) for p in parts]
+    return torch.cat([_bytes(p, n) for p in parts], dim=1), layout
+
+
+def unpack_rows(buf: torch.Tensor, layout) -> list[torch.Tensor]:
+    """Inverse of pack_rows on a buffer [..., bytes]: tensors [..., *shape] of the packed dtypes."""
+    out, off = [], 0
+    lead = tuple(buf.shape[:-1])
+    for nbytes, dtype, shape in layout:
+        out.append(buf[..., off:off + nbytes].contiguous().view(dtype).reshape(lead + shape))
+        off += nbytes
+    return out
+
+
+def pad_csr(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,
+            slots: int = MAX_QUERY_TERMS) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """CSR (indptr [n+1], indices, values) -> fixed slots (count int32 [n], indices int32 [n, slots],
+    values float32 [n, slots]), on the device and without a host synchronisation."""
+    n = int(indptr.numel()) - 1
+    dev = indptr.device
+    ip = indptr.to(torch.int64)
+    count = (ip[1:] - ip[:-1]).to(torch.int32)
+    pi = torch.zeros(n * slots + 1, dtype=torch.int32, device=dev)
+    pv = torch.zeros(n * slots + 1, dtype=torch.float32, device=dev)
+    nnz = int(idx.numel())  # the tensor's size, known on the host
+    if nnz:
+        e = torch.arange(nnz, dtype=torch.int64, device=dev)
+        q = torch.searchsorted(ip[1:], e, right=True)  # query owning element e
+        pos = q * slots + (e - ip[q])
+        pi.index_copy_(0, pos, idx.to(torch.int32))
+        pv.index_copy_(0, pos, val.to(torch.float32))
+    return count, pi[:-1].view(n, slots), pv[:-1].view(n, slots)
+
+
+def unpad_csr(count: torch.Tensor, pi: torch.Tensor, pv: torch.Tensor):
+    """Inverse of pad_csr: (indptr int32 [n+1], indices, values). The index / value arrays keep
+    their padded length; entries past indptr[-1] are unused (the CSR ends at indptr[-1])."""
+    n, slots = pi.shape
+    dev = pi.device
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(count.to(torch.int64), 0, out=indptr[1:])
+    j = torch.arange(slots, dtype=torch.int64, device=dev)
+    live = j[None, :] < count.to(torch.int64)[:, None]
+    # live slot (q, j) -> indptr[q] + j; dead slots -> a dump slot past the end
+    pos = torch.where(live, indptr[:-1, None] + j[None, :], torch.full_like(j[None, :], n * slots))
+    oi = torch.zeros(n * slots + 1, dtype=torch.int32, device=dev)
+    ov = torch.zeros(n * slots + 1, dtype=torch.float32, device=dev)
+    oi.index_copy_(0, pos.reshape(-1), pi.reshape(-1))
+    ov.index_copy_(0, pos.reshape(-1), pv.reshape(-1))
+    return indptr.to(torch.int32), oi[:-1], ov[:-1]
+
+
+def _topk_parts(t: TopK) -> list[torch.Tensor]:
+    return [t.rank.to(torch.float64), t.ids, t.scores, t.count.to(torch.int32).view(-1, 1)]
+
+
 class ShardedSearch:
     """Sharded top-k over a process group. `local_dense(q, k)` / `local_sparse(qcsr, k)` search
     this rank's shard and return global ordinals; `merge` combines [S, B, k] lists."""
@@ -55,71 +128,83 @@ class ShardedSearch:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self._side: torch.cuda.Stream | None = None
 
-    def _gather_lists(self, local: TopK, k: int, nb: int) -> TopK:
-        """All-gathers per-shard lists of all G*nb queries; merges this rank's nb queries."""
-        g = self.world
-        dev = local.ids.device
-        rank_bits = local.rank.contiguous().view(torch.int64)
-        pack_a = torch.cat([rank_bits, local.ids], dim=1).contiguous()                 # [G*nb, 2k]
-        pack_b = torch.cat([local.scores.contiguous().view(torch.int32),
-                            local.count.view(-1, 1).to(torch.int32)], dim=1).contiguous()  # [G*nb, k+1]
-        ga = torch.empty((g,) + tuple(pack_a.shape), dtype=pack_a.dtype, device=dev)
-        gb = torch.empty((g,) + tuple(pack_b.shape), dtype=pack_b.dtype, device=dev)
-        _all_gather(ga, pack_a, self.group)
-        _all_gather(gb, pack_b, self.group)
-        mine_a = ga[:, self.rank * nb:(self.rank + 1) * nb]
-        mine_b = gb[:, self.rank * nb:(self.rank + 1) * nb]
-        return self.merge(mine_a[..., :k].contiguous().view(torch.float64),
-                          mine_b[..., :k].contiguous().view(torch.float32),
-                          mine_a[..., k:].contiguous(), mine_b[..., k].contiguous(), k)
+    # ------------------------------------------------------------------ collectives
+
+    def _gather(self, buf: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+        _all_gather(out, buf, self.group)
+        return out
+
+    def _gather_queries(self, q_dense: torch.Tensor | None, q_csr=None):
+        """All queries of all ranks: (dense [G*nb, dim] or None, csr of G*nb queries or None)."""
+        parts = []
+        if q_dense is not None:
+            parts.append(q_dense)
+        if q_csr is not None:
+            parts.extend(pad_csr(*q_csr))
+        buf, layout = pack_rows(parts)
+        g = self._gather(buf)                              # [G, nb, bytes]
+        g = g.reshape((-1,) + tuple(g.shape[2:]))          # [G*nb, bytes]
+        vals = unpack_rows(g, layout)
+        dense = vals.pop(0) if q_dense is not None else None
+        csr = unpad_csr(*vals) if q_csr is not None else None
+        return dense, csr
+
+    def _exchange(self, lists: list[TopK], k: int, nb: int) -> list[TopK]:
+        """All-gathers per-shard lists of all G*nb queries (several searches in one message) and
+        merges this rank's nb queries over the G shards."""
+        parts = [p for t in lists for p in _topk_parts(t)]
+        buf, layout = pack_rows(parts)
+        g = self._gather(buf)                              # [G, G*nb, bytes]
+        mine = g[:, self.rank * nb:(self.rank + 1) * nb]   # [G, nb, bytes]
+        vals = unpack_rows(mine, layout)
+        out = []
+        for i in range(len(lists)):
+            rank, ids, scores, count = vals[4 * i:4 * i + 4]
+            out.append(self.merge(rank, scores, ids, count.reshape(count.shape[:2]), k))
+        return out
+
+    # ------------------------------------------------------------------------ search
 
     def gather_queries(self, q_local: torch.Tensor) -> torch.Tensor:
-        out = torch.empty((self.world,) + tuple(q_local.shape), dtype=q_local.dtype,
-                          device=q_local.device)
-        _all_gather(out, q_local.contiguous(), self.group)
-        return out.reshape((-1,) + tuple(q_local.shape[1:]))
+        return self._gather_queries(q_local)[0]
 
     def dense(self, q_local: torch.Tensor, k: int) -> TopK:
         nb = int(q_local.shape[0])
-        all_q = self.gather_queries(q_local)
-        return self._gather_lists(self.local_dense(all_q, k), k, nb)
+        all_q, _ = self._gather_queries(q_local)
+        return self._exchange([self.local_dense(all_q, k)], k, nb)[0]
 
     def sparse(self, q_local_csr: tuple[torch.Tensor, torch.Tensor, torch.Tensor], k: int) -> TopK:
         """q_local_csr: (indptr int32 [nb+1], indices int32, values float32) of this rank."""
-        indptr, idx, val = q_local_csr
-        nb = int(indptr.numel()) - 1
-        all_csr = self._gather_csr(indptr, idx, val)
-        return self._gather_lists(self.local_sparse(all_csr, k), k, nb)
+        nb = int(q_local_csr[0].numel()) - 1
+        _, all_csr = self._gather_queries(None, q_local_csr)
+        return self._exchange([self.local_sparse(all_csr, k)], k, nb)[0]
 
     def hybrid(self, q_local: torch.Tensor, q_local_csr, k: int) -> TopK:
-        """Prefetch dense and sparse 2k each on the global corpus, then RRF(limit=k)."""
-        d = self.dense(q_local, 2 * k)
-        s = self.sparse(q_local_csr, 2 * k)
+        """Prefetch dense and sparse 2k each on the global corpus, then RRF(limit=k). One
+        collective for the queries, the two local scans concurrent, one for the lists."""
+        nb = int(q_local.shape[0])
+        all_q, all_csr = self._gather_queries(q_local, q_local_csr)
+        d, s = self._local_pair(all_q, all_csr, 2 * k)
+        d, s = self._exchange([d, s], 2 * k, nb)
         return self.rrf(d, s, k)
 
-    def _gather_csr(self, indptr, idx, val):
-        """All-gathers ragged CSR blocks: lengths first, then padded payloads."""
-        dev = indptr.device
-        n_local = torch.tensor([idx.numel()], dtype=torch.int64, device=dev)
-        lens = torch.empty((self.world, 1), dtype=torch.int64, device=dev)
-        _all_gather(lens, n_local, self.group)
-        lens = lens.view(-1).tolist()
-        m = max(max(lens), 1)
-        pad_i = torch.zeros(m, dtype=torch.int32, device=dev)
-        pad_v = torch.zeros(m, dtype=torch.float32, device=dev)
-        pad_i[: idx.numel()] = idx
-        pad_v[: val.numel()] = val
-        gi = torch.empty((self.world, m), dtype=torch.int32, device=dev)
-        gv = torch.empty((self.world, m), dtype=torch.float32, device=dev)
-        gp = torch.empty((self.world, indptr.numel()), dtype=torch.int32, device=dev)
-        _all_gather(gi, pad_i, self.group)
-        _all_gather(gv, pad_v, self.group)
-        _all_gather(gp, indptr.to(torch.int32).contiguous(), self.group)
-        ptrs, idxs, vals, base = [torch.zeros(1, dtype=torch.int32, device=dev)], [], [], 0
-        for r in range(self.world):
-            ptrs.append(gp[r, 1:] + base)
-            idxs.append(gi[r, : lens[r]])
-            vals.append(gv[r, : lens[r]])
-            base += lens[r]
-        return torch.cat(ptrs), torch.cat(idxs), torch.cat(vals)
+    def _local_pair(self, all_q, all_csr, k: int) -> tuple[TopK, TopK]:
+        if not all_q.is_cuda:
+            return self.local_dense(all_q, k), self.local_sparse(all_csr, k)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=all_q.device)
+        main = torch.cuda.current_stream()
+        self._side.wait_stream(main)
+        for t in all_csr:
+            t.record_stream(self._side)
+        with torch.cuda.stream(self._side):
+            s = self.local_sparse(all_csr, k)
+        d = self.local_dense(all_q, k)
+        main.wait_stream(self._side)
+        for t in (s.scores, s.ids, s.rank, s.count, s.flags):
+            if t is not None:
+                t.record_stream(main)
+        return d, s

@@ -32,103 +32,14 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from audio_rag_amd.synthetic import (VOCAB, doc_tokens, make_queries, make_rows,  # noqa: E402
+                                     make_sparse_queries, make_sparse_rows)
+
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # dense (non-sparse) matrix peaks, MI355X_MICROARCH.md: bf16/f16 ~2.5 PF; fp32-input MFMA runs at
 # 1/16 of the bf16 rate (cdna_hip_programming.md §3 'FP32-input MFMA')
 MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.0}
-CHUNK_ROWS = 65536
-
-
-def make_rows(first: int, count: int, dim: int, device, seed: int = 0) -> torch.Tensor:
-    """Rows [first, first+count) of the global synthetic corpus: each 64k-row chunk has its own
-    seed, so a shard's rows are identical whatever the shard count."""
-    out = torch.empty((count, dim), dtype=torch.float16, device=device)
-    c0 = first // CHUNK_ROWS
-    c1 = (first + count + CHUNK_ROWS - 1) // CHUNK_ROWS
-    for c in range(c0, c1):
-        a, b = c * CHUNK_ROWS, (c + 1) * CHUNK_ROWS
-        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
-        x = torch.randn((CHUNK_ROWS, dim), generator=g, device=device)
-        x = (x / x.norm(dim=1, keepdim=True)).half()
-        lo, hi = max(a, first), min(b, first + count)
-        if lo < hi:
-            out[lo - first:hi - first] = x[lo - a:hi - a]
-    return out
-
-
-def make_queries(n_batches: int, batch: int, dim: int, device, seed: int) -> torch.Tensor:
-    g = torch.Generator(device=device).manual_seed(seed)
-    x = torch.randn((n_batches, batch, dim), generator=g, device=device)
-    return (x / x.norm(dim=2, keepdim=True)).half().contiguous()
-
-
-VOCAB = 250002
-
-
-def _zipf_cdf(device, a: float = 1.1) -> torch.Tensor:
-    r = torch.arange(1, VOCAB - 4 + 1, dtype=torch.float64, device=device)
-    p = r.pow(-a)
-    return torch.cumsum(p / p.sum(), 0)
-
-
-def _sparse_rows(n: int, mean_nnz: float, lo: int, hi: int, wlo: float, whi: float,
-                 g: torch.Generator, cdf: torch.Tensor, cap: int):
-    """SURVEY §8(d) law on the device: nnz ~ clip(Poisson(mean), lo, hi), unique Zipf(1.1) token
-    ids in [4, VOCAB) (sorted per row), weights U(wlo, whi). Returns (counts, indices, values)."""
-    dev = cdf.device
-    nnz = torch.poisson(torch.full((n,), mean_nnz, device=dev), generator=g).clamp_(lo, hi)
-    u = torch.rand((n, cap), generator=g, device=dev, dtype=torch.float64)
-    ids = torch.searchsorted(cdf, u).clamp_(max=VOCAB - 5).to(torch.int32) + 4
-    ids, _ = torch.sort(ids, dim=1)
-    fresh = torch.ones_like(ids, dtype=torch.bool)
-    fresh[:, 1:] = ids[:, 1:] != ids[:, :-1]
-    rank = torch.cumsum(fresh.to(torch.int32), dim=1)
-    keep = fresh & (rank <= nnz[:, None].to(torch.int32))
-    counts = keep.sum(dim=1)
-    idx = ids[keep]
-    vals = torch.empty(idx.numel(), device=dev).uniform_(wlo, whi, generator=g)
-    return counts, idx.contiguous(), vals.contiguous()
-
-
-def make_sparse_rows(first: int, count: int, device, seed: int = 2):
-    """CSR rows [first, first+count) of the global synthetic sparse corpus (64k-row chunks with
-    their own seeds, as make_rows)."""
-    cdf = _zipf_cdf(device)
-    cnts, idxs, vals = [], [], []
-    c0 = first // CHUNK_ROWS
-    c1 = (first + count + CHUNK_ROWS - 1) // CHUNK_ROWS
-    for c in range(c0, c1):
-        a = c * CHUNK_ROWS
-        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
-        cnt, idx, val = _sparse_rows(CHUNK_ROWS, 96.0, 16, 256, 0.01, 0.40, g, cdf, cap=320)
-        off = torch.zeros(CHUNK_ROWS + 1, dtype=torch.int64, device=device)
-        off[1:] = torch.cumsum(cnt, 0)
-        lo, hi = max(a, first) - a, min(a + CHUNK_ROWS, first + count) - a
-        if lo < hi:
-            cnts.append(cnt[lo:hi])
-            idxs.append(idx[off[lo]:off[hi]])
-            vals.append(val[off[lo]:off[hi]])
-    counts = torch.cat(cnts)
-    indptr = torch.zeros(count + 1, dtype=torch.int64, device=device)
-    indptr[1:] = torch.cumsum(counts, 0)
-    return indptr, torch.cat(idxs).contiguous(), torch.cat(vals).contiguous()
-
-
-def make_sparse_queries(n: int, device, seed: int):
-    g = torch.Generator(device=device).manual_seed(seed)
-    cnt, idx, val = _sparse_rows(n, 12.0, 1, 32, 0.05, 0.35, g, _zipf_cdf(device), cap=48)
-    indptr = torch.zeros(n + 1, dtype=torch.int32, device=device)
-    indptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
-    return indptr, idx, val
-
-
-def doc_tokens(ordinals: torch.Tensor, length: int) -> torch.Tensor:
-    """Synthetic token ids of a chunk (240 tokens, ids in [4, VOCAB)), a pure
-    function of the chunk ordinal so every rank can build rerank pairs without a payload table."""
-    pos = torch.arange(length, device=ordinals.device, dtype=torch.int64)
-    h = ordinals[..., None].to(torch.int64) * 2654435761 + pos * 40503 + 12345
-    return (h % (VOCAB - 4) + 4).to(torch.int32)
 
 
 def cpu_baseline(n_full: int, dim: int, batch: int, k: int, budget_s: float = 12.0) -> dict:

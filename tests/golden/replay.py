@@ -13,6 +13,15 @@ FIXTURE = Path(__file__).resolve().parent / "reference_query_path.json"
 COLLECTION_HYBRID = {"ingested": True, "hybrid_real": True, "legacy": False, "empty": False}
 
 
+CONFIG_FIXTURE = Path(__file__).resolve().parent / "reference_config_development.json"
+
+
+def reference_config() -> dict:
+    """The configuration the reference's loader builds from its own config files
+    (make_config_fixture.py), as a plain dict."""
+    return json.loads(CONFIG_FIXTURE.read_text())["config"]
+
+
 def load():
     golden = json.loads(FIXTURE.read_text())
     s = scenario.build()

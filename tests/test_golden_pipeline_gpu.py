@@ -20,7 +20,7 @@ def _build(golden_s):
     import torch
 
     from audio_rag_amd import AudioRAG
-    from audio_rag_amd.config import AudioRAGConfig, GenerationConfig, RetrievalConfig
+    from audio_rag_amd.config import AudioRAGConfig, RetrievalConfig
     from audio_rag_amd.core import AudioChunk, BaseEmbedder, EmbeddingResult, SparseVector
     from audio_rag_amd.reranking.bge import BGEReranker
 
@@ -56,8 +56,12 @@ def _build(golden_s):
                 raise RuntimeError("simulated cross-encoder failure")
             return [float(s["rerank"][q, text2c[t]]) for t in texts]
 
-    cfg = AudioRAGConfig(retrieval=RetrievalConfig(backend="mi355x", reproduce_sparse_drop=True),
-                         generation=GenerationConfig(backend="none"))
+    # the configuration a reference deployment loads (its own loader on its own config files,
+    # tests/golden/reference_config_development.json): backend "qdrant", every MI355X knob at its
+    # default (reproduce_sparse_drop included)
+    cfg = AudioRAGConfig(**replay.reference_config())
+    assert cfg.retrieval.backend == "qdrant" and cfg.retrieval == RetrievalConfig(
+        **replay.reference_config()["retrieval"])
     rag = AudioRAG(cfg)
     rag._embedder = TableEmbedder()
     retriever = rag.retriever

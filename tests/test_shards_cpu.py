@@ -134,3 +134,27 @@ def test_two_rank_sharded_search_equals_global(tmp_path, oracle_mod):
             assert z["h_cnt"][q] == len(want)
             assert [int(x) for x in z["h_ids"][q, :len(want)]] == [p for p, _ in want]
             assert [float(x) for x in z["h_sc"][q, :len(want)]] == [v for _, v in want]
+
+
+def test_pad_unpad_csr_roundtrip():
+    """The fixed-slot query layout of the one-collective query exchange: ragged, empty and
+    full (MAX_QUERY_TERMS) queries survive pad -> unpad with the CSR order intact."""
+    from audio_rag_amd.retrieval.shards import MAX_QUERY_TERMS, pack_rows, pad_csr, unpack_rows, unpad_csr
+
+    rng = np.random.default_rng(0)
+    lens = [0, 3, MAX_QUERY_TERMS, 1, 0, 17]
+    indptr = np.zeros(len(lens) + 1, np.int32)
+    indptr[1:] = np.cumsum(lens)
+    idx = rng.integers(0, 250002, indptr[-1]).astype(np.int32)
+    val = rng.random(indptr[-1]).astype(np.float32)
+    t = lambda a: torch.from_numpy(a)
+    cnt, pi, pv = pad_csr(t(indptr), t(idx), t(val))
+    assert cnt.tolist() == lens and pi.shape == (len(lens), MAX_QUERY_TERMS)
+    dense = torch.randn(len(lens), 8, dtype=torch.float64)
+    buf, layout = pack_rows([dense, cnt, pi, pv])
+    d2, c2, i2, v2 = unpack_rows(buf, layout)
+    assert torch.equal(d2, dense)
+    ip2, ix2, vx2 = unpad_csr(c2, i2, v2)
+    assert ip2.tolist() == indptr.tolist()
+    n = int(indptr[-1])
+    assert ix2[:n].tolist() == idx.tolist() and vx2[:n].tolist() == val.tolist()
