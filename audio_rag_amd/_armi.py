@@ -18,6 +18,7 @@ LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libarmi.so"
 ARMI_OK = 0
 ARMI_FLAG_CERTIFIED = 1
 ARMI_FLAG_FALLBACK = 2
+TIMING_DENSE_SCAN, TIMING_SPARSE_SCAN, TIMING_ENCODER_GEMM = 0, 1, 2
 ABI_VERSION = 1
 
 c_void_p = ctypes.c_void_p
@@ -47,6 +48,7 @@ SIGNATURES: dict[str, tuple] = {
                                        c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "armi_scan_timing_enable": (c_int, [c_int]),
     "armi_scan_timing_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
+    "armi_kernel_timing_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_sparse_index_create": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                          c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_sparse_index_destroy": (c_int, [c_void_p]),

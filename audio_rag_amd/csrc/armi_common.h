@@ -34,6 +34,16 @@ int hip_fail(hipError_t e, const char* what);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Live kernel timing (armi_scan_timing_enable / armi_kernel_timing_read): TimedLaunch brackets
+// one launch on `stream` with a HIP event pair when timing is enabled, else costs nothing.
+struct TimedLaunch {
+  int slot = -1;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipStream_t stream = nullptr;
+  int begin(int slot, hipStream_t stream);  // 0 = not timed, 1 = timed, <0 = error (set)
+  int end();
+};
+
 // Carves consecutive 256-B aligned sub-buffers out of one caller workspace.
 struct Carver {
   char* base;

@@ -1521,43 +1521,6 @@ int launch_exact(const armi_index* idx, const uint16_t* queries, int nq, int k,
   return ARMI_OK;
 }
 
-// Optional live timing of the scan kernel (bench.py's roofline): a HIP event pair around every
-// dense_scan launch while enabled; read back (synchronising) by armi_scan_timing_read.
-struct ScanTiming {
-  bool enabled = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> spare;
-  std::mutex mu;
-};
-ScanTiming& scan_timing() {
-  static ScanTiming t;
-  return t;
-}
-
-int timing_begin(hipStream_t stream, std::pair<hipEvent_t, hipEvent_t>* ev) {
-  ScanTiming& st = scan_timing();
-  std::lock_guard<std::mutex> g(st.mu);
-  if (!st.enabled) return 0;
-  if (st.spare.empty()) {
-    hipEvent_t a, b;
-    ARMI_HIP(hipEventCreate(&a));
-    ARMI_HIP(hipEventCreate(&b));
-    st.spare.emplace_back(a, b);
-  }
-  *ev = st.spare.back();
-  st.spare.pop_back();
-  ARMI_HIP(hipEventRecord(ev->first, stream));
-  return 1;
-}
-
-int timing_end(hipStream_t stream, const std::pair<hipEvent_t, hipEvent_t>& ev) {
-  ScanTiming& st = scan_timing();
-  std::lock_guard<std::mutex> g(st.mu);
-  ARMI_HIP(hipEventRecord(ev.second, stream));
-  st.pending.push_back(ev);
-  return ARMI_OK;
-}
-
 template <int DIM>
 int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int k,
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
@@ -1584,9 +1547,8 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     } else {
       if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
     }
-    std::pair<hipEvent_t, hipEvent_t> ev;
-    const int timed = timing_begin(stream, &ev);
-    if (timed < 0) return ARMI_ERR_HIP;
+    armi::TimedLaunch tl;
+    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     if (glds) {
       auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64, false>
                                      : dense_gemm_scan_glds_kernel<DIM, 32, false>;
@@ -1608,19 +1570,16 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                                               insert_guard());
       ARMI_LAUNCHED("dense_gemm_scan_kernel");
     }
-    if (timed == 1)
-      if (int rc = timing_end(stream, ev)) return rc;
+    if (int rc = tl.end()) return rc;
   } else {
     if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
-    std::pair<hipEvent_t, hipEvent_t> ev;
-    const int timed = timing_begin(stream, &ev);
-    if (timed < 0) return ARMI_ERR_HIP;
+    armi::TimedLaunch tl;
+    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     dense_scan_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
         idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
     ARMI_LAUNCHED("dense_scan_kernel");
-    if (timed == 1)
-      if (int rc = timing_end(stream, ev)) return rc;
+    if (int rc = tl.end()) return rc;
   }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
@@ -1726,31 +1685,6 @@ int armi_dense_exact_topk(const armi_index* idx, const uint16_t* queries, int n_
     return launch_exact<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
                              out_count, flags, 0, w, stream);
   });
-}
-
-int armi_scan_timing_enable(int enable) {
-  ScanTiming& st = scan_timing();
-  std::lock_guard<std::mutex> g(st.mu);
-  st.enabled = enable != 0;
-  return ARMI_OK;
-}
-
-int armi_scan_timing_read(double* total_ms, int64_t* launches) {
-  ARMI_REQUIRE(total_ms && launches, "armi_scan_timing_read: null pointer argument");
-  ScanTiming& st = scan_timing();
-  std::lock_guard<std::mutex> g(st.mu);
-  double sum = 0.0;
-  for (auto& ev : st.pending) {
-    ARMI_HIP(hipEventSynchronize(ev.second));
-    float ms = 0.f;
-    ARMI_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
-    sum += ms;
-    st.spare.push_back(ev);
-  }
-  *total_ms = sum;
-  *launches = (int64_t)st.pending.size();
-  st.pending.clear();
-  return ARMI_OK;
 }
 
 int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const int64_t* in_ids,

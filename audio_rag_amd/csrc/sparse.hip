@@ -1122,11 +1122,14 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.wl,
         w.wl_count, w.qof, pflags);
     ARMI_LAUNCHED("pass_terms_kernel");
+    armi::TimedLaunch tl;
+    if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
+    if (int rc = tl.end()) return rc;
 #ifdef ARMI_SPARSE_PROFILE
     if (dbg & 8) {
       std::vector<unsigned long long> h((size_t)kMaxRanges * kWaves * 8);

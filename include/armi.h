@@ -120,11 +120,20 @@ int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const 
                            int k_out, double* out_rank, float* out_scores, int64_t* out_ids,
                            int32_t* out_count, hipStream_t stream);
 
-/* Live timing of the dense scan kernel for roofline reporting: while enabled, every
- * dense_scan launch is bracketed by a HIP event pair on its stream. _read synchronises on the
- * recorded events, returns the summed kernel time and launch count, and clears them. */
+/* Live timing of the dominant kernels for roofline reporting (bench.py): while enabled, every
+ * launch of a timed kernel is bracketed by a HIP event pair on the stream it is launched on.
+ * _read synchronises on the recorded events of one slot, returns the summed kernel time and the
+ * launch count, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
+ * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (sparse_scan_kernel of armi_sparse_topk),
+ * ARMI_TIMING_ENCODER_GEMM (the cross-encoder GEMMs of armi_enc_gemm_f16).
+ * armi_scan_timing_read = armi_kernel_timing_read(ARMI_TIMING_DENSE_SCAN, ...). */
+#define ARMI_TIMING_DENSE_SCAN 0
+#define ARMI_TIMING_SPARSE_SCAN 1
+#define ARMI_TIMING_ENCODER_GEMM 2
+#define ARMI_TIMING_SLOTS 3
 int armi_scan_timing_enable(int enable);
 int armi_scan_timing_read(double* total_ms, int64_t* launches);
+int armi_kernel_timing_read(int slot, double* total_ms, int64_t* launches);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Sparse (lexical-weight) store                                                              */
