@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <limits>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -68,6 +69,12 @@ __device__ __forceinline__ void topm_insert(float x, int32_t id, float (&s)[M], 
     ix[j] = ti;
   }
   disc = fmaxf(disc, x);
+}
+
+// The same MFMA with the accumulator pinned to AGPRs (inline asm: hipcc otherwise keeps it in
+// ArchVGPRs when the kernel fits in 256 of them).
+__device__ __forceinline__ void mfma16_acc(f32x16& c, u32x4 a, u32x4 b) {
+  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 __device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
@@ -891,6 +898,416 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
 }
 
 
+// Phase-pipelined tiled scan (ARMI_GEMM_FORM=p8; measured slower than the four-stage kernel
+// above, which stays the default: see DESIGN.md §7 and profiles/r02_p8_scan_ab.txt). Same tile (256 rows x 256 queries), same wave geometry
+// (2 row groups of 128 x 4 query groups of 64, waves w and w + 4 on one SIMD) and the same
+// candidate output as dense_gemm_scan_glds_kernel, a different schedule:
+//   * a K-tile is 64 deep; the wave's 128 x 64 output is cut into four QUADRANTS, visited in
+//     snake order q = (rows 0-63, queries 0-31), (0-63, 32-63), (64-127, 32-63), (64-127, 0-31),
+//     so consecutive quadrants share one operand (kept in registers); one PHASE = one quadrant x
+//     the K-tile = 8 v_mfma_f32_32x32x16_f16 (2 row tiles x 4 k-steps);
+//   * each phase of a wave is LOAD (LDS-DMA issue of one 16-KB piece of a later K-tile, the
+//     quadrant's new fragments: 12 / 4 / 8 / 4 ds_read_b128, lgkmcnt(0)) -> s_barrier -> MATH ->
+//     s_barrier, and waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MATH
+//     runs while its partner's LOAD runs;
+//   * the LDS holds two K-tiles of four 16-KB pieces, 128 image rows x 128 B (k 0-63: every
+//     LDS-DMA instruction moves 8 whole 128-B lines): PA0 = the rows 0-63 of both row groups,
+//     PB0 = the queries 0-31 of every query group, PA1 = rows 64-127, PB1 = queries 32-63; 16-B
+//     chunk c of image row ir sits in slot c ^ ((ir >> 1) & 7) (conflict-free ds_read_b128). A
+//     piece is last read in phase 0 (PA0), 1 (PB1), 2 (PA1) or 3 (PB0) of its K-tile, and the
+//     same piece of the K-tile two ahead is issued in the next phase (7, 7, 7 and 4 phases
+//     before its first reader); a constant vmcnt(6) per phase retires it in time;
+//   * the epilogue of each quadrant (inverse norms from an LDS copy, NaN masking, lane-list
+//     insertion) runs in the LOAD segment after the quadrant's last MFMAs, beside the partner's
+//     MATH.
+constexpr int kP8Piece = 16384;            // bytes per piece (128 image rows x 128 B)
+constexpr int kP8Buf = 4 * kP8Piece;       // one K-tile
+constexpr int kP8Lds = 2 * kP8Buf;         // two K-tiles (128 KB)
+
+template <int DIM>
+constexpr size_t gemm_p8_lds_bytes() {
+  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
+  return kP8Lds + 2048 > lists ? (size_t)kP8Lds + 2048 : lists;
+}
+
+// ABL: diagnostic ablations, compiled only into a probe build (-DARMI_PROBE_BUILD, results
+// wrong): 1 no vmcnt wait, 2 every row piece re-reads the range's first row tile (L2 hits),
+// 4 no MFMAs, 8 no barriers in the phase loop. The shipped instantiation is ABL = 0.
+template <int DIM, int ABL>
+__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_p8_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
+    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
+  constexpr int KT = DIM / 64;  // K-tiles per row tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int id = blockIdx.x;
+  int qb, rp;
+  if (n_qb == 2) {
+    qb = (id >> 3) & 1;
+    rp = (id >> 4) * 8 + (id & 7);
+  } else {
+    qb = id % n_qb;
+    rp = id / n_qb;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int64_t lo = (int64_t)rp * rows_per_range;
+  const int64_t hi = min(lo + rows_per_range, n_rows);
+  const int q_base = qb * kGQB;
+  // 32-bit row offsets from here on: the range's rows, its pointers and its limits
+  const int n_here = (int)(hi - lo);                  // rows of this range
+  const int last_row = (int)(n_rows - 1 - lo);        // last valid row offset (clamp target)
+  const uint16_t* __restrict__ rows_r = rows + lo * DIM;
+  const float* __restrict__ inv_r = inv_norm32 + lo;
+  const int last4 = (int)(((n_rows + 31) / 32) * 32 - 4 - lo);  // last 16-B group of the norms
+
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int wq = wave & 3;   // query group: queries wq*64 + n*32 + r
+  const int wr = wave >> 2;  // row group: rows wr*128 + m*32 + ...
+
+  float s0[kLaneList], s1[kLaneList];
+  int32_t i0[kLaneList], i1[kLaneList];
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
+  }
+  float d0 = kNegInf, d1 = kNegInf;
+
+  const int n_tiles = (n_here + kG2Rows - 1) / kG2Rows;
+
+  // Piece x in {PA0, PB0, PA1, PB1} of K-tile (tile, kt), into buffer `buf`. This wave's two
+  // 1-KB instructions cover image rows 16 * wave + [0, 16): lane slot lane % 8 of image row
+  // ir holds chunk (lane % 8) ^ ((ir >> 1) & 7). The per-lane source offsets are fixed per piece
+  // type and instruction (8 VGPRs, bytes from a wave-uniform base), so an issue is one
+  // LDS-DMA and a scalar base; the last row tile of the range (and the clamped tiles past it,
+  // issued into the free buffer and never read) clamps its rows to the store instead.
+  uint32_t off_a[2][2], off_b[2][2];  // [x >> 1][instruction]
+  int tr_a[2][2];
+#pragma unroll
+  for (int hx = 0; hx < 2; ++hx)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ir = 16 * wave + 8 * i + (lane >> 3);
+      const int c = (lane & 7) ^ ((ir >> 1) & 7);
+      tr_a[hx][i] = (ir >> 6) * 128 + hx * 64 + (ir & 63);  // row of the tile
+      off_a[hx][i] = (uint32_t)(tr_a[hx][i] * DIM * 2 + c * 16);
+      const int q = min(q_base + (ir >> 5) * 64 + hx * 32 + (ir & 31), nq - 1);
+      off_b[hx][i] = (uint32_t)((q - q_base) * DIM * 2 + c * 16);
+    }
+  const unsigned char* __restrict__ qsrc =
+      reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
+  const unsigned char* __restrict__ rsrc = reinterpret_cast<const unsigned char*>(rows_r);
+  const int full_tiles = n_here / kG2Rows;  // tiles whose 256 rows are all inside the store
+  auto issue_piece = [&](int tile, int kt, int buf, auto X) {
+    constexpr int x = decltype(X)::value;
+    constexpr int hx = x >> 1;
+    unsigned char* base = smem + buf * kP8Buf + x * kP8Piece + wave * 2048;
+    if constexpr ((x & 1) == 0) {
+      if (tile < full_tiles && tile * kG2Rows + kG2Rows - 1 <= last_row) {
+        const unsigned char* tb = rsrc + ((size_t)tile * kG2Rows * DIM + kt * 64) * 2;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_global_load_lds(tb + off_a[hx][i], (lds_ptr_t)(base + i * 1024), 16, 0,
+                                           0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = min(tile * kG2Rows + tr_a[hx][i], last_row);
+          const uint32_t c16 = off_a[hx][i] & 127u;
+          __builtin_amdgcn_global_load_lds(rsrc + ((size_t)row * DIM + kt * 64) * 2 + c16,
+                                           (lds_ptr_t)(base + i * 1024), 16, 0, 0);
+        }
+      }
+    } else {
+      const unsigned char* tb = qsrc + kt * 64 * 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds(tb + off_b[hx][i], (lds_ptr_t)(base + i * 1024), 16, 0, 0);
+    }
+  };
+  // Inverse norms of row tile `tile` -> LDS [kP8Lds + (tile & 1) KB]: one 1-KB LDS-DMA by wave 0
+  // (its later vmcnt waits then cover one instruction more: a slightly earlier retire, never a
+  // missed one). Clamped to the padded norm array; rows past the range are masked anyway.
+  auto issue_norms = [&](int tile) {
+    if (wave == 0) {
+      const int rr = min(tile * kG2Rows + 4 * lane, last4);
+      __builtin_amdgcn_global_load_lds(inv_r + rr,
+                                       (lds_ptr_t)(smem + kP8Lds + (tile & 1) * 1024), 16, 0, 0);
+    }
+  };
+
+  if constexpr (ABL & 1024) {
+    // an AGPR operand anywhere in the kernel makes hipcc select the AGPR form of the MFMAs
+    // (accumulators in AccVGPRs) instead of the ArchVGPR form it picks for <= 256 registers
+    int zero = 0;
+    asm volatile("; agpr-form hint %0" ::"a"(zero));
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) { acc[m][0] = f32x16{}; acc[m][1] = f32x16{}; }
+
+  // Epilogue of quadrant Q (row tiles 2 mh, 2 mh + 1 x query tile nh of the wave) of `tile`.
+  auto epilogue = [&](int tile, auto Q) {
+    constexpr int q = decltype(Q)::value;
+    constexpr int mh = q >> 1;
+    constexpr int nh = (q == 1 || q == 2) ? 1 : 0;
+#pragma unroll
+    for (int mm = 0; mm < 2; ++mm) {
+      const int m = 2 * mh + mm;
+      const int ro = tile * kG2Rows + wr * 128 + m * 32;  // row offset of the 32-row block
+      const int64_t rb = lo + ro;
+      // inverse norms of rows ro + (j & 3) + 8 (j >> 2) + 4 h from the tile's LDS copy; by inline
+      // asm, else hipcc cannot tell them from the in-flight LDS-DMA and drains it (vmcnt(0))
+      const uint32_t linv = (uint32_t)(uintptr_t)(lds_ptr_t)(
+          smem + kP8Lds + (tile & 1) * 1024 + (wr * 128 + m * 32 + 4 * h) * 4);
+      u32x4 invw[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
+      // valid rows of the block (wave-uniform bits): inside the range and kept by the filter
+      uint32_t valid = ro + 32 <= n_here ? 0xffffffffu
+                                         : (ro >= n_here ? 0u : (1u << (n_here - ro)) - 1u);
+      if (row_mask) valid &= (uint32_t)(row_mask[rb >> 6] >> (rb & 63));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      float inv[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        inv[4 * g + 0] = __uint_as_float(invw[g].x);
+        inv[4 * g + 1] = __uint_as_float(invw[g].y);
+        inv[4 * g + 2] = __uint_as_float(invw[g].z);
+        inv[4 * g + 3] = __uint_as_float(invw[g].w);
+      }
+      // invalid rows get a NaN scale: a NaN score never enters a lane list and fmaxf ignores it
+      if (valid != 0xffffffffu) {
+        const uint32_t vb = valid >> (4 * h);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (!((vb >> ((j & 3) + 8 * (j >> 2))) & 1u)) inv[j] = __builtin_nanf("");
+      }
+      // opaque: keeps hipcc from hoisting the 16 row ids of every block out of the phase loop
+      // (they would stay live across all K-tiles and spill)
+      int32_t rbase = (int32_t)rb + 4 * h;
+      asm volatile("" : "+v"(rbase));
+      f32x16& c = mm ? acc[2 * mh + 1][nh] : acc[2 * mh][nh];
+      float* sl = nh ? s1 : s0;
+      int32_t* il = nh ? i1 : i0;
+      float& dl = nh ? d1 : d0;
+      float y[16];
+      float mx = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        y[j] = c[j] * inv[j];
+        mx = fmaxf(mx, y[j]);
+      }
+      if (__any(mx > sl[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(y[j] > sl[kLaneList - 1])) {
+            dl = fmaxf(dl, y[j]);  // = topm_insert of a value no lane list takes
+            continue;
+          }
+          float v = y[j];
+          int32_t id2 = rbase + (j & 3) + 8 * (j >> 2);
+#pragma unroll
+          for (int e = 0; e < kLaneList; ++e) {
+            const bool cbt = v > sl[e];
+            const float ts = cbt ? v : sl[e];
+            const int32_t ti = cbt ? id2 : il[e];
+            v = cbt ? sl[e] : v;
+            id2 = cbt ? il[e] : id2;
+            sl[e] = ts;
+            il[e] = ti;
+          }
+          dl = fmaxf(dl, v);
+        }
+      } else {
+        dl = fmaxf(dl, mx);
+      }
+      c = f32x16{};
+    }
+  };
+
+  // Per-lane LDS addresses: image row (wr*64 + r) of an A piece / (wq*32 + r) of a B piece, and
+  // the swizzled chunk of k-step ks: 2*ks + h.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  const uint32_t a_lane = lds0 + (uint32_t)(wr * 64 + r) * 128;
+  const uint32_t b_lane = lds0 + (uint32_t)(wq * 32 + r) * 128;
+  const int swz = (r >> 1) & 7;
+  uint32_t co[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) co[ks] = (uint32_t)(((2 * ks + h) ^ swz) << 4);
+
+  u32x4 fa[2][4], fb[4];  // A: [row tile of the half][k-step], B: [k-step]
+  auto read_a = [&](uint32_t piece) {
+    const uint32_t b = a_lane + piece;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[0][ks]) : "v"(b + co[ks]));
+      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fa[1][ks]) : "v"(b + co[ks]));
+    }
+  };
+  auto read_b = [&](uint32_t piece) {
+    const uint32_t b = b_lane + piece;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fb[ks]) : "v"(b + co[ks]));
+  };
+
+  auto advance = [&](int& t, int& k) {
+    if (++k == KT) { k = 0; ++t; }
+  };
+  // One phase (quadrant j of K-tile T = (tile, kt)): LOAD -> barrier -> MATH -> barrier.
+  auto phase = [&](int T, int tile, int kt, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int mh = j >> 1;
+    constexpr int nh = (j == 1 || j == 2) ? 1 : 0;
+    // ---- LOAD: epilogue of the quadrant whose last MFMAs ran in the previous phase
+    if constexpr (j == 0) {
+      if (kt == 0 && tile > 0) epilogue(tile - 1, std::integral_constant<int, 3>{});
+    } else {
+      if (kt == KT - 1) epilogue(tile, std::integral_constant<int, j - 1>{});
+    }
+    {  // the piece freed by the previous phase, of the K-tile two ahead of it
+      constexpr int x = j == 0 ? 1 : (j == 1 ? 0 : (j == 2 ? 3 : 2));  // PB0, PA0, PB1, PA1
+      int t1 = tile;
+      int k1 = kt;
+      if constexpr (j != 0) advance(t1, k1);
+      advance(t1, k1);
+      if constexpr (!(ABL & 128))
+        issue_piece(t1, k1, (j == 0 ? T + 1 : T) & 1, std::integral_constant<int, x>{});
+      if constexpr (j == 1) {
+        if (kt == 0) issue_norms(tile);
+      }
+    }
+    const uint32_t buf = (uint32_t)((T & 1) * kP8Buf);
+    if constexpr (!(ABL & 256)) {
+      if constexpr (j == 0) { read_a(buf + 0 * kP8Piece); read_b(buf + 1 * kP8Piece); }
+      if constexpr (j == 1) read_b(buf + 3 * kP8Piece);
+      if constexpr (j == 2) read_a(buf + 2 * kP8Piece);
+      if constexpr (j == 3) read_b(buf + 1 * kP8Piece);
+    }
+    // retire this wave's pieces older than the 3 youngest phases and the fragment reads (so the
+    // next phase's DMA may overwrite what was read here)
+    if constexpr (ABL & 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
+    // ---- MATH: 2 row tiles x 1 query tile x 4 k-steps
+    if constexpr (!(ABL & 16)) __builtin_amdgcn_s_setprio(1);
+    f32x16& c0 = acc[2 * mh][nh];
+    f32x16& c1 = acc[2 * mh + 1][nh];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if constexpr (ABL & 4) {
+        asm volatile("" :: "v"(fa[0][ks]), "v"(fa[1][ks]), "v"(fb[ks]));
+      } else if constexpr (ABL & 512) {
+        mfma16_acc(c0, fa[0][ks], fb[ks]);
+        mfma16_acc(c1, fa[1][ks], fb[ks]);
+      } else {
+        c0 = mfma16(fa[0][ks], fb[ks], c0);
+        c1 = mfma16(fa[1][ks], fb[ks], c1);
+      }
+    }
+    if constexpr (!(ABL & 16)) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if (n_tiles > 0) {
+    {  // prologue: K-tile 0 whole, K-tile 1's PA0, PB1, PA1 (phase 0 issues its PB0)
+      int t1 = 0;
+      int k1 = 0;
+      advance(t1, k1);
+      issue_piece(0, 0, 0, std::integral_constant<int, 0>{});
+      issue_piece(0, 0, 0, std::integral_constant<int, 1>{});
+      issue_piece(0, 0, 0, std::integral_constant<int, 3>{});
+      issue_piece(0, 0, 0, std::integral_constant<int, 2>{});
+      issue_piece(t1, k1, 1, std::integral_constant<int, 0>{});
+      issue_piece(t1, k1, 1, std::integral_constant<int, 3>{});
+      issue_piece(t1, k1, 1, std::integral_constant<int, 2>{});
+    }
+    // K-tile 0's PA0 and PB0 retired: the 5 youngest pieces stay in flight
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // waves 4-7 run one barrier behind (ABL 32: the odd waves instead; ABL 64: no stagger)
+    const bool late = (ABL & 32) ? (wave & 1) : ((ABL & 64) ? false : wr != 0);
+    if (!(ABL & 8) && late) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    int T = 0;
+    for (int tile = 0; tile < n_tiles; ++tile) {
+      for (int kt = 0; kt < KT; ++kt, ++T) {
+        phase(T, tile, kt, std::integral_constant<int, 0>{});
+        phase(T, tile, kt, std::integral_constant<int, 1>{});
+        phase(T, tile, kt, std::integral_constant<int, 2>{});
+        phase(T, tile, kt, std::integral_constant<int, 3>{});
+      }
+    }
+    if (!(ABL & 8) && !(ABL & 64) && !late) __builtin_amdgcn_s_barrier();  // balance the count
+    epilogue(n_tiles - 1, std::integral_constant<int, 3>{});
+  }
+
+  // workgroup lists (as dense_gemm_scan_glds_kernel); the DMA of the clamped tail pieces must
+  // land before the stage buffers are reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
+  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);      // [256][4]
+  {
+    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
+    const int slot = (wr * 2 + h) * kLaneList;
+#pragma unroll
+    for (int j = 0; j < kLaneList; ++j) {
+      lkey[qa * 16 + slot + j] = s0[j];
+      lrow[qa * 16 + slot + j] = i0[j];
+      lkey[qc * 16 + slot + j] = s1[j];
+      lrow[qc * 16 + slot + j] = i1[j];
+    }
+    ldisc[qa * 4 + wr * 2 + h] = d0;
+    ldisc[qc * 4 + wr * 2 + h] = d1;
+  }
+  __syncthreads();
+  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
+    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
+    float key = lkey[ql * 16 + (lane & 15)];
+    int32_t row = lrow[ql * 16 + (lane & 15)];
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const float ok = __shfl_xor(key, stride);
+        const int32_t orow = __shfl_xor(row, stride);
+        const bool lower = (lane & stride) == 0;
+        const bool desc = (lane & size) == 0;
+        const bool other_better = armi::approx_better(ok, orow, key, row);
+        const bool take_other = (lower == desc) ? other_better : !other_better;
+        if (take_other) { key = ok; row = orow; }
+      }
+    }
+    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
+    const int qg = q_base + ql;
+    if (qg < nq) {
+      const size_t base = (size_t)rp * nq + qg;
+      cand_key[base * kKW + rank] = key;
+      cand_row[base * kKW + rank] = row;
+      if (rank == 0) {
+        const float* dd = ldisc + ql * 4;
+        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
+      }
+    }
+  }
+}
+
 // This lane's DIM/64 contiguous fp16 elements of a vector, as raw 8-byte words.
 template <int DIM>
 __device__ __forceinline__ void load_raw(const uint16_t* __restrict__ v, int lane,
@@ -1423,6 +1840,17 @@ int gemm_ablate() {
 #endif
 }
 
+// Schedule of the tiled scan: the four-stage kernel (default) or the phase-pipelined one
+// (ARMI_GEMM_FORM=p8, A/B measurements; measured 2.00 vs 1.67-1.73 ms at the 10M / 8-way
+// per-rank shape, profiles/r02_p8_scan_ab.txt).
+bool use_p8_form() {
+  static const bool p8 = [] {
+    const char* e = getenv("ARMI_GEMM_FORM");
+    return e && e[0] == 'p';
+  }();
+  return p8;
+}
+
 struct GemmPlan {
   int n_qb = 0;
   int n_ranges = 0;
@@ -1549,7 +1977,39 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     }
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    if (glds) {
+    if (glds && use_p8_form()) {
+      auto kern = dense_gemm_scan_p8_kernel<DIM, 0>;
+#ifdef ARMI_PROBE_BUILD
+      switch (gemm_ablate()) {
+        case 1: kern = dense_gemm_scan_p8_kernel<DIM, 1>; break;
+        case 2: kern = dense_gemm_scan_p8_kernel<DIM, 2>; break;
+        case 3: kern = dense_gemm_scan_p8_kernel<DIM, 3>; break;
+        case 4: kern = dense_gemm_scan_p8_kernel<DIM, 4>; break;
+        case 8: kern = dense_gemm_scan_p8_kernel<DIM, 8>; break;
+        case 12: kern = dense_gemm_scan_p8_kernel<DIM, 12>; break;
+        case 13: kern = dense_gemm_scan_p8_kernel<DIM, 13>; break;
+        case 16: kern = dense_gemm_scan_p8_kernel<DIM, 16>; break;
+        case 32: kern = dense_gemm_scan_p8_kernel<DIM, 32>; break;
+        case 64: kern = dense_gemm_scan_p8_kernel<DIM, 64>; break;
+        case 68: kern = dense_gemm_scan_p8_kernel<DIM, 68>; break;
+        case 196: kern = dense_gemm_scan_p8_kernel<DIM, 196>; break;
+        case 324: kern = dense_gemm_scan_p8_kernel<DIM, 324>; break;
+        case 452: kern = dense_gemm_scan_p8_kernel<DIM, 452>; break;
+        case 192: kern = dense_gemm_scan_p8_kernel<DIM, 192>; break;
+        case 320: kern = dense_gemm_scan_p8_kernel<DIM, 320>; break;
+        case 512: kern = dense_gemm_scan_p8_kernel<DIM, 512>; break;
+        case 576: kern = dense_gemm_scan_p8_kernel<DIM, 576>; break;
+        case 1024: kern = dense_gemm_scan_p8_kernel<DIM, 1024>; break;
+        case 1088: kern = dense_gemm_scan_p8_kernel<DIM, 1088>; break;
+        default: break;
+      }
+#endif
+      if (int rc = allow_lds(kern, gemm_p8_lds_bytes<DIM>())) return rc;
+      kern<<<dim3(gp.grid), dim3(kGThreads), gemm_p8_lds_bytes<DIM>(), stream>>>(
+          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
+          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
+      ARMI_LAUNCHED("dense_gemm_scan_p8_kernel");
+    } else if (glds) {
       auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64, false>
                                      : dense_gemm_scan_glds_kernel<DIM, 32, false>;
 #ifdef ARMI_PROBE_BUILD
