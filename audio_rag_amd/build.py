@@ -23,7 +23,7 @@ LIB = OUT_DIR / "libarmi.so"
 OBJ_DIR = ROOT / "build" / "armi_obj"
 
 SOURCES = ["armi_common.cpp", "index.hip", "dense.hip", "sparse.hip", "rrf.hip", "encoder.hip",
-           "attention.hip"]
+           "attention.hip", "stream.cpp"]
 ARCH = os.environ.get("ARMI_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-ffp-contract=off",
@@ -64,7 +64,7 @@ def build(verbose: bool = False) -> Path:
         objs = list(ex.map(lambda s: _compile(s, headers), SOURCES))
     tmp = LIB.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
-           "-Wl,-rpath,/opt/rocm/lib", "-Wl,-z,defs", "-lamdhip64"]
+           "-Wl,-rpath,/opt/rocm/lib", "-Wl,-z,defs", "-lamdhip64", "-lpthread"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")

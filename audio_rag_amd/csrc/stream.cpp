@@ -1,0 +1,395 @@
+// Native streaming query server (BASELINE configs[4] "streaming query at fixed QPS"): single
+// dense queries from any number of caller threads coalesced into device batches.
+//
+// The reference answers one request at a time: the REST route calls pipeline.query() per
+// request (src/audio_rag/api/v1/query.py:90-115) in each of 4 uvicorn processes
+// (Dockerfile.api:85-86), so Qdrant sees batch-1 searches. On the MI355X a batch-1 scan costs the
+// same HBM pass over the chunk store as a batch-64 scan, so the serving layer batches across
+// requests. This is that layer without an interpreter in the request path:
+//   submit (any thread): copy the query into the collecting batch (pinned host memory), take a
+//     ticket; the first query of a batch starts its max_wait clock.
+//   dispatcher thread: when the batch is full or its first query has waited max_wait, hand it
+//     to one of kSlots in-flight slots: H2D copy, armi_dense_topk, D2H copy of the results, an
+//     event -- all on the server's HIP stream -- and start collecting the next batch while the
+//     GPU runs (slots recycle in order).
+//   completion thread: per slot in order, wait for its event, copy every query's top-k into the
+//     result ring, stamp the completion time, wake the waiters.
+//   wait (caller): block until its ticket's ring entry is complete, copy the results out.
+// Per-query semantics are armi_dense_topk's (exact cosine ranking, certified fast scan, exact
+// fallback inside the call); only the grouping is new.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "armi_index.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch())
+      .count();
+}
+
+constexpr int kSlots = 3;           // batches in flight (GPU running / collected / collecting)
+constexpr int64_t kRing = 1 << 20;  // result ring entries (tickets alive at once)
+
+struct Slot {
+  int n = 0;                         // queries in the batch
+  int64_t first_ticket = 0;
+  uint16_t* h_queries = nullptr;     // pinned [max_batch][dim]
+  uint16_t* d_queries = nullptr;
+  float* d_scores = nullptr;
+  int64_t* d_ids = nullptr;
+  double* d_rank = nullptr;
+  int32_t* d_count = nullptr;
+  uint32_t* d_flags = nullptr;
+  void* d_ws = nullptr;
+  float* h_scores = nullptr;         // pinned results
+  int64_t* h_ids = nullptr;
+  double* h_rank = nullptr;
+  int32_t* h_count = nullptr;
+  hipEvent_t done = nullptr;
+  int status = ARMI_OK;
+};
+
+struct Entry {
+  std::atomic<int64_t> ticket{-1};   // ticket whose result this entry holds (complete when set)
+  int64_t t_submit = 0;
+  int64_t t_done = 0;
+  int32_t count = 0;
+  int status = ARMI_OK;
+};
+
+}  // namespace
+
+struct armi_stream {
+  const armi_index* idx = nullptr;
+  int k = 0, max_batch = 0, dim = 0;
+  int64_t max_wait_ns = 0;
+  size_t ws_bytes = 0;
+  hipStream_t stream = nullptr;
+  Slot slots[kSlots];
+  // result ring: entries + their payload arrays
+  std::vector<Entry> ring;
+  std::vector<float> r_scores;
+  std::vector<int64_t> r_ids;
+  std::vector<double> r_rank;
+  // collection state (mu)
+  std::mutex mu;
+  std::condition_variable cv_dispatch;   // dispatcher: batch ready / stop
+  std::condition_variable cv_space;      // submitters: a collecting slot is free
+  std::condition_variable cv_complete;   // completion thread: a launched slot to finish
+  std::condition_variable cv_done;       // waiters: results published
+  int collect = 0;                       // slot being filled
+  int64_t first_submit_ns = 0;           // submit time of its first query
+  std::deque<int> launched;              // slots on the GPU, in order
+  int free_slots = kSlots - 1;           // slots neither collecting nor launched
+  int64_t next_ticket = 0;
+  bool stop = false;
+  std::atomic<int64_t> batches{0}, queries{0};
+  std::thread dispatcher, completer;
+  int device = 0;
+};
+
+namespace {
+
+int launch_slot(armi_stream* s, Slot& sl) {
+  const size_t qbytes = (size_t)sl.n * s->dim * sizeof(uint16_t);
+  ARMI_HIP(hipMemcpyAsync(sl.d_queries, sl.h_queries, qbytes, hipMemcpyHostToDevice, s->stream));
+  int rc = armi_dense_topk(s->idx, sl.d_queries, sl.n, s->k, nullptr, sl.d_scores, sl.d_ids,
+                           sl.d_rank, sl.d_count, sl.d_flags, sl.d_ws, s->ws_bytes, s->stream);
+  if (rc != ARMI_OK) return rc;
+  const size_t nk = (size_t)sl.n * s->k;
+  ARMI_HIP(hipMemcpyAsync(sl.h_scores, sl.d_scores, nk * sizeof(float), hipMemcpyDeviceToHost,
+                          s->stream));
+  ARMI_HIP(hipMemcpyAsync(sl.h_ids, sl.d_ids, nk * sizeof(int64_t), hipMemcpyDeviceToHost,
+                          s->stream));
+  ARMI_HIP(hipMemcpyAsync(sl.h_rank, sl.d_rank, nk * sizeof(double), hipMemcpyDeviceToHost,
+                          s->stream));
+  ARMI_HIP(hipMemcpyAsync(sl.h_count, sl.d_count, (size_t)sl.n * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, s->stream));
+  ARMI_HIP(hipEventRecord(sl.done, s->stream));
+  return ARMI_OK;
+}
+
+void dispatcher_main(armi_stream* s) {
+  (void)hipSetDevice(s->device);
+  std::unique_lock<std::mutex> lk(s->mu);
+  for (;;) {
+    // a batch is due when full, or when its first query has waited max_wait
+    for (;;) {
+      if (s->stop) return;
+      Slot& c = s->slots[s->collect];
+      if (c.n == s->max_batch) break;
+      if (c.n > 0) {
+        const int64_t due = s->first_submit_ns + s->max_wait_ns;
+        const int64_t t = now_ns();
+        if (t >= due) break;
+        s->cv_dispatch.wait_for(lk, std::chrono::nanoseconds(due - t));
+      } else {
+        s->cv_dispatch.wait(lk);
+      }
+    }
+    // hand the batch over, and open the next collecting slot (wait for one if all are busy)
+    while (s->free_slots == 0 && !s->stop) s->cv_dispatch.wait(lk);
+    if (s->stop) return;
+    const int cur = s->collect;
+    int nxt = (cur + 1) % kSlots;
+    s->collect = nxt;
+    --s->free_slots;
+    Slot& sl = s->slots[cur];
+    lk.unlock();
+    s->cv_space.notify_all();
+    sl.status = launch_slot(s, sl);
+    lk.lock();
+    s->launched.push_back(cur);
+    s->cv_complete.notify_one();
+  }
+}
+
+void completer_main(armi_stream* s) {
+  (void)hipSetDevice(s->device);
+  std::unique_lock<std::mutex> lk(s->mu);
+  for (;;) {
+    while (s->launched.empty() && !s->stop) s->cv_complete.wait(lk);
+    if (s->launched.empty() && s->stop) return;
+    const int cur = s->launched.front();
+    lk.unlock();
+    Slot& sl = s->slots[cur];
+    int status = sl.status;
+    if (status == ARMI_OK && hipEventSynchronize(sl.done) != hipSuccess) status = ARMI_ERR_HIP;
+    const int64_t t = now_ns();
+    for (int i = 0; i < sl.n; ++i) {
+      const int64_t tk = sl.first_ticket + i;
+      Entry& e = s->ring[tk % kRing];
+      const size_t o = (size_t)(tk % kRing) * s->k;
+      if (status == ARMI_OK) {
+        std::memcpy(&s->r_scores[o], sl.h_scores + (size_t)i * s->k, s->k * sizeof(float));
+        std::memcpy(&s->r_ids[o], sl.h_ids + (size_t)i * s->k, s->k * sizeof(int64_t));
+        std::memcpy(&s->r_rank[o], sl.h_rank + (size_t)i * s->k, s->k * sizeof(double));
+        e.count = sl.h_count[i];
+      } else {
+        e.count = 0;
+      }
+      e.status = status;
+      e.t_done = t;
+      e.ticket.store(tk, std::memory_order_release);
+    }
+    s->batches.fetch_add(1);
+    s->queries.fetch_add(sl.n);
+    lk.lock();
+    sl.n = 0;
+    s->launched.pop_front();
+    ++s->free_slots;
+    s->cv_done.notify_all();
+    s->cv_dispatch.notify_one();
+  }
+}
+
+void free_slot(Slot& sl) {
+  if (sl.h_queries) (void)hipHostFree(sl.h_queries);
+  if (sl.h_scores) (void)hipHostFree(sl.h_scores);
+  if (sl.h_ids) (void)hipHostFree(sl.h_ids);
+  if (sl.h_rank) (void)hipHostFree(sl.h_rank);
+  if (sl.h_count) (void)hipHostFree(sl.h_count);
+  for (void* p : {(void*)sl.d_queries, (void*)sl.d_scores, (void*)sl.d_ids, (void*)sl.d_rank,
+                  (void*)sl.d_count, (void*)sl.d_flags, sl.d_ws})
+    if (p) (void)hipFree(p);
+  if (sl.done) (void)hipEventDestroy(sl.done);
+  sl = Slot{};
+}
+
+void shutdown(armi_stream* s) {
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->stop = true;
+  }
+  s->cv_dispatch.notify_all();
+  s->cv_complete.notify_all();
+  s->cv_space.notify_all();
+  if (s->dispatcher.joinable()) s->dispatcher.join();
+  if (s->completer.joinable()) s->completer.join();
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->cv_done.notify_all();
+  }
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (auto& sl : s->slots) free_slot(sl);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  s->stream = nullptr;
+}
+
+int alloc_slot(armi_stream* s, Slot& sl) {
+  const size_t nq = (size_t)s->max_batch, nk = nq * s->k;
+  ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_queries), nq * s->dim * 2));
+  ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_scores), nk * sizeof(float)));
+  ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_ids), nk * sizeof(int64_t)));
+  ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_rank), nk * sizeof(double)));
+  ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_count), nq * sizeof(int32_t)));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_queries), nq * s->dim * 2));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_scores), nk * sizeof(float)));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_ids), nk * sizeof(int64_t)));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_rank), nk * sizeof(double)));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_count), nq * sizeof(int32_t)));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_flags), nq * sizeof(uint32_t)));
+  ARMI_HIP(hipMalloc(&sl.d_ws, s->ws_bytes));
+  ARMI_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  return ARMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int armi_stream_create(const armi_index* idx, int k, int max_batch, double max_wait_us,
+                       armi_stream** out) {
+  ARMI_REQUIRE(idx && out, "armi_stream_create: null pointer argument");
+  ARMI_REQUIRE(k >= 1 && k <= 240, "armi_stream_create: k must be in [1, 240]");
+  ARMI_REQUIRE(max_batch >= 1 && max_batch <= 4096, "armi_stream_create: max_batch in [1, 4096]");
+  ARMI_REQUIRE(max_wait_us >= 0.0, "armi_stream_create: max_wait_us < 0");
+  *out = nullptr;
+  auto* s = new armi_stream();
+  s->idx = idx;
+  s->k = k;
+  s->max_batch = max_batch;
+  s->dim = armi_index_dim(idx);
+  s->max_wait_ns = (int64_t)(max_wait_us * 1e3);
+  s->device = idx->device;
+  s->ws_bytes = armi_dense_workspace_bytes(idx, max_batch, k);
+  s->ring = std::vector<Entry>(kRing);
+  s->r_scores.assign((size_t)kRing * k, 0.f);
+  s->r_ids.assign((size_t)kRing * k, -1);
+  s->r_rank.assign((size_t)kRing * k, 0.0);
+  int rc = ARMI_OK;
+  if (hipSetDevice(s->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    rc = armi::fail(ARMI_ERR_HIP, "armi_stream_create: stream");
+  }
+  for (int i = 0; i < kSlots && rc == ARMI_OK; ++i) rc = alloc_slot(s, s->slots[i]);
+  if (rc != ARMI_OK) {
+    shutdown(s);
+    delete s;
+    return rc;
+  }
+  s->dispatcher = std::thread(dispatcher_main, s);
+  s->completer = std::thread(completer_main, s);
+  *out = s;
+  return ARMI_OK;
+}
+
+int armi_stream_destroy(armi_stream* s) {
+  if (!s) return ARMI_OK;
+  shutdown(s);
+  delete s;
+  return ARMI_OK;
+}
+
+int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
+  ARMI_REQUIRE(s && query && ticket, "armi_stream_submit: null pointer argument");
+  std::unique_lock<std::mutex> lk(s->mu);
+  for (;;) {
+    if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_submit: server stopped");
+    if (s->slots[s->collect].n < s->max_batch) break;
+    s->cv_space.wait(lk);  // collecting batch full and not yet handed over
+  }
+  Slot& c = s->slots[s->collect];
+  const int64_t tk = s->next_ticket++;
+  if (c.n == 0) {
+    c.first_ticket = tk;
+    s->first_submit_ns = now_ns();
+  }
+  std::memcpy(c.h_queries + (size_t)c.n * s->dim, query, (size_t)s->dim * sizeof(uint16_t));
+  Entry& e = s->ring[tk % kRing];
+  e.t_submit = now_ns();
+  ++c.n;
+  const bool wake = c.n == 1 || c.n == s->max_batch;
+  lk.unlock();
+  if (wake) s->cv_dispatch.notify_one();
+  *ticket = tk;
+  return ARMI_OK;
+}
+
+int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids, double* rank,
+                     int32_t* count, double timeout_us) {
+  ARMI_REQUIRE(s && count, "armi_stream_wait: null pointer argument");
+  ARMI_REQUIRE(ticket >= 0, "armi_stream_wait: bad ticket");
+  Entry& e = s->ring[ticket % kRing];
+  if (e.ticket.load(std::memory_order_acquire) != ticket) {
+    std::unique_lock<std::mutex> lk(s->mu);
+    const auto until = Clock::now() + std::chrono::nanoseconds((int64_t)(timeout_us * 1e3));
+    while (e.ticket.load(std::memory_order_acquire) != ticket) {
+      if (ticket >= s->next_ticket) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: unknown ticket");
+      if (e.ticket.load(std::memory_order_acquire) > ticket)
+        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: result overwritten (ring wrapped)");
+      if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: server stopped");
+      if (s->cv_done.wait_until(lk, until) == std::cv_status::timeout &&
+          e.ticket.load(std::memory_order_acquire) != ticket)
+        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: timeout");
+    }
+  }
+  if (e.status != ARMI_OK) return armi::fail(e.status, "armi_stream_wait: the batch failed");
+  const size_t o = (size_t)(ticket % kRing) * s->k;
+  if (scores) std::memcpy(scores, &s->r_scores[o], s->k * sizeof(float));
+  if (ids) std::memcpy(ids, &s->r_ids[o], s->k * sizeof(int64_t));
+  if (rank) std::memcpy(rank, &s->r_rank[o], s->k * sizeof(double));
+  *count = e.count;
+  return ARMI_OK;
+}
+
+int armi_stream_stats(armi_stream* s, int64_t* batches, int64_t* queries) {
+  ARMI_REQUIRE(s && batches && queries, "armi_stream_stats: null pointer argument");
+  *batches = s->batches.load();
+  *queries = s->queries.load();
+  return ARMI_OK;
+}
+
+int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, int64_t n_vectors,
+                        int64_t n_queries, double qps, uint64_t seed, double* latency_us,
+                        double* elapsed_s, int64_t* completed) {
+  ARMI_REQUIRE(s && queries && latency_us && elapsed_s && completed,
+               "armi_stream_loadgen: null pointer argument");
+  ARMI_REQUIRE(n_vectors >= 1, "armi_stream_loadgen: n_vectors < 1");
+  ARMI_REQUIRE(n_queries >= 1 && n_queries <= kRing / 2, "armi_stream_loadgen: n_queries range");
+  ARMI_REQUIRE(qps > 0.0, "armi_stream_loadgen: qps must be > 0");
+  std::mt19937_64 rng(seed);
+  std::exponential_distribution<double> gap(qps);
+  std::vector<int64_t> tickets((size_t)n_queries);
+  const int64_t t0 = now_ns();
+  double due = 0.0;  // seconds since t0
+  for (int64_t i = 0; i < n_queries; ++i) {
+    due += gap(rng);
+    const int64_t due_ns = t0 + (int64_t)(due * 1e9);
+    for (;;) {  // open-loop arrivals: sleep to ~50 us before the due time, then spin
+      const int64_t t = now_ns();
+      if (t >= due_ns) break;
+      if (due_ns - t > 100000) std::this_thread::sleep_for(std::chrono::nanoseconds(due_ns - t - 50000));
+    }
+    if (int rc = armi_stream_submit(s, queries + (size_t)(i % n_vectors) * s->dim,
+                                    &tickets[(size_t)i]))
+      return rc;
+  }
+  int64_t t_last = t0, t_first = -1;
+  int32_t cnt = 0;
+  for (int64_t i = 0; i < n_queries; ++i) {
+    if (int rc = armi_stream_wait(s, tickets[(size_t)i], nullptr, nullptr, nullptr, &cnt, 60e6))
+      return rc;
+    const Entry& e = s->ring[tickets[(size_t)i] % kRing];
+    latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;
+    t_last = std::max(t_last, e.t_done);
+    if (t_first < 0) t_first = e.t_submit;
+  }
+  *elapsed_s = (double)(t_last - t_first) * 1e-9;
+  *completed = n_queries;
+  return ARMI_OK;
+}
+
+}  // extern "C"

@@ -169,3 +169,100 @@ class QueryBatcher:
             for q in reqs:
                 if not q.future.done():
                     q.future.set_exception(err)
+
+
+class StreamServer:
+    """The native streaming server (libarmi armi_stream_*, include/armi.h) over one collection's
+    dense index: no Python thread in the request path. Callers submit single dense queries from
+    any thread (ctypes releases the GIL) and collect reference-shaped results; the batching,
+    the device work and the completion run in libarmi's own threads on the server's HIP stream.
+    Dense search only (the search_type="dense" path of qdrant.py:316-323, the configs[4] stream
+    workload); hybrid and filtered queries go through QueryBatcher."""
+
+    def __init__(self, retriever: MI355XRetriever, collection_name: str | None = None,
+                 top_k: int | None = None, max_batch: int = 64, max_wait_ms: float = 2.0):
+        from audio_rag_amd import _armi
+
+        self._armi = _armi
+        self.retriever = retriever
+        self.resolved = retriever._resolve_collection(collection_name)
+        self.collection = retriever._collections[self.resolved]
+        self.index = self.collection.dense_index  # kept alive for the server's lifetime
+        self.k = top_k or retriever.config.top_k
+        self.dim = retriever.embedding_dim
+        self._handle = _armi.ctypes.c_void_p()
+        _armi.call("armi_stream_create", self.index.handle, self.k, max_batch,
+                   float(max_wait_ms) * 1e3, _armi.ctypes.byref(self._handle))
+
+    def submit_arrays(self, dense: np.ndarray) -> int:
+        q = np.ascontiguousarray(dense, dtype=np.float16).reshape(-1)
+        if q.size != self.dim:
+            raise RetrievalError(f"query has {q.size} components, the store {self.dim}")
+        ticket = self._armi.ctypes.c_int64()
+        self._armi.call("armi_stream_submit", self._handle, q.ctypes.data,
+                        self._armi.ctypes.byref(ticket))
+        return ticket.value
+
+    def submit(self, query: EmbeddingResult) -> int:
+        return self.submit_arrays(np.asarray(query.dense, dtype=np.float32))
+
+    def raw_result(self, ticket: int, timeout: float = 60.0):
+        """(scores float32 [k], ids int64 [k], count) of a ticket."""
+        scores = np.empty(self.k, dtype=np.float32)
+        ids = np.empty(self.k, dtype=np.int64)
+        count = self._armi.ctypes.c_int32()
+        self._armi.call("armi_stream_wait", self._handle, ticket, scores.ctypes.data,
+                        ids.ctypes.data, None, self._armi.ctypes.byref(count), timeout * 1e6)
+        return scores, ids, count.value
+
+    def result(self, ticket: int, timeout: float = 60.0) -> list[RetrievalResult]:
+        """The ticket's list[RetrievalResult] (as MI355XRetriever.search builds it)."""
+        from audio_rag_amd.core.base import AudioChunk
+
+        scores, ids, c = self.raw_result(ticket, timeout)
+        out = []
+        for pid, score in zip(ids[:c].tolist(), scores[:c].tolist()):
+            p = self.collection.payloads[pid]
+            chunk = AudioChunk(text=p.get("text", ""), start=p.get("start", 0.0),
+                               end=p.get("end", 0.0), speaker=p.get("speaker"),
+                               metadata=p.get("metadata"))
+            out.append(RetrievalResult(chunk=chunk, score=float(score), source=self.resolved))
+        return out
+
+    def search(self, query: EmbeddingResult) -> list[RetrievalResult]:
+        return self.result(self.submit(query))
+
+    def stats(self) -> tuple[int, int]:
+        b, q = self._armi.ctypes.c_int64(), self._armi.ctypes.c_int64()
+        self._armi.call("armi_stream_stats", self._handle, self._armi.ctypes.byref(b),
+                        self._armi.ctypes.byref(q))
+        return b.value, q.value
+
+    def loadgen(self, queries: np.ndarray, n_queries: int, qps: float, seed: int = 0):
+        """Native open-loop Poisson load at `qps` (armi_stream_loadgen): per-query latency in
+        seconds and the elapsed time from the first submit to the last completion."""
+        q = np.ascontiguousarray(queries, dtype=np.float16).reshape(-1, self.dim)
+        lat = np.empty(n_queries, dtype=np.float64)
+        el = self._armi.ctypes.c_double()
+        done = self._armi.ctypes.c_int64()
+        self._armi.call("armi_stream_loadgen", self._handle, q.ctypes.data, q.shape[0], n_queries,
+                        float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
+                        self._armi.ctypes.byref(done))
+        return lat * 1e-6, el.value
+
+    def close(self) -> None:
+        if self._handle and self._handle.value:
+            self._armi.call("armi_stream_destroy", self._handle)
+            self._handle = self._armi.ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -241,6 +241,10 @@ def main() -> None:
     ap.add_argument("--queries", type=int, default=200, help="pipeline: timed queries")
     ap.add_argument("--qps", type=float, default=20000.0, help="stream: offered queries/s")
     ap.add_argument("--duration", type=float, default=4.0, help="stream: seconds of arrivals")
+    ap.add_argument("--stream-front", choices=["native", "python"], default="native",
+                    help="stream: native StreamServer + native load generator, or a Python "
+                         "client through QueryBatcher")
+    ap.add_argument("--max-wait-ms", type=float, default=2.0, help="stream: batching window")
     ap.add_argument("--initial-k", type=int, default=20)
     ap.add_argument("--rerank-dtype", choices=["fp32", "bf16", "fp16"], default="fp16",
                     help="cross-encoder GEMM dtype (fp16: fp16 GEMMs + fused fp16 attention, "
@@ -645,83 +649,97 @@ def pipeline_main(args) -> None:
 
 
 def stream_main(args) -> None:
-    """configs[4]'s query side on one GPU: single queries arrive as a Poisson process at
-    --qps from a client thread, QueryBatcher coalesces them (<= 64 per batch, <= 2 ms wait) into
-    MI355XRetriever.search_batch over the 1M-chunk store, and each caller gets its
-    list[RetrievalResult]. value = completed queries / s; latency = submit -> result."""
+    """configs[4]'s query side on one GPU: single dense queries arrive as an open-loop Poisson
+    process at --qps over the 1M-chunk store. Default front end: the native StreamServer
+    (libarmi armi_stream_*: coalescing into batches of <= 64, <= --max-wait-ms after a batch's
+    first query, up to three batches in flight on the server's stream) driven by libarmi's own
+    load generator thread, so no interpreter sits in the request path. --stream-front python:
+    the same arrivals from a Python client thread through QueryBatcher (futures +
+    list[RetrievalResult] per caller). value = completed queries / s; latency = submit -> result."""
     from audio_rag_amd.config import RetrievalConfig
-    from audio_rag_amd.retrieval.batcher import QueryBatcher
+    from audio_rag_amd.retrieval.batcher import QueryBatcher, StreamServer
     from audio_rag_amd.retrieval.collection import ChunkCollection
     from audio_rag_amd.retrieval.device import DenseIndex
     from audio_rag_amd.retrieval.mi355x import MI355XRetriever
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    # the client thread and the batcher thread share one interpreter: hand the GIL over at
-    # 0.2 ms instead of the 5 ms default, or a batch waits for the client's time slice
-    sys.setswitchinterval(2e-4)
     n, dim, k = args.chunks, args.dim, args.top_k
     rows = make_rows(0, n, dim, dev)
     payloads = [{"text": "", "start": 0.0, "end": 0.0, "speaker": None, "metadata": {}}] * n
     ret = MI355XRetriever(RetrievalConfig(top_k=k, search_type="dense"), dim)
     ret.attach_collection(ChunkCollection.from_indexes("audio_rag", DenseIndex(rows), payloads))
     qs = make_queries(1, 4096, dim, dev, seed=1)[0].cpu().numpy()
-    rng = np.random.default_rng(7)
-    lat, done = [], []
-    lock = __import__("threading").Lock()
+    n_q = int(args.qps * args.duration)
+    if args.stream_front == "native":
+        with StreamServer(ret, max_batch=64, max_wait_ms=args.max_wait_ms) as srv:
+            srv.loadgen(qs, 4096, qps=args.qps, seed=6)  # warm-up
+            b0, q0 = srv.stats()
+            lat, elapsed = srv.loadgen(qs, n_q, qps=args.qps, seed=7)
+            b1, q1 = srv.stats()
+        batches, served = b1 - b0, q1 - q0
+        value = n_q / elapsed
+        front = "native StreamServer + native open-loop load generator"
+    else:
+        # the client thread and the batcher thread share one interpreter: hand the GIL over at
+        # 0.2 ms instead of the 5 ms default, or a batch waits for the client's time slice
+        sys.setswitchinterval(2e-4)
+        rng = np.random.default_rng(7)
+        lat_l, done = [], []
+        lock = __import__("threading").Lock()
 
-    def on_done(t_sub):
-        def cb(f):
-            t = time.perf_counter()
-            f.result()
-            with lock:
-                lat.append(t - t_sub)
-                done.append(t)
-        return cb
+        def on_done(t_sub):
+            def cb(f):
+                t = time.perf_counter()
+                f.result()
+                with lock:
+                    lat_l.append(t - t_sub)
+                    done.append(t)
+            return cb
 
-    with QueryBatcher(ret, max_batch=64, max_wait_ms=2.0) as qb:
-        for i in range(256):  # warm-up
-            qb.submit_arrays(qs[i % 4096]).result()
-        lat.clear()
-        done.clear()
-        n_q = int(args.qps * args.duration)
-        gaps = rng.exponential(1.0 / args.qps, size=n_q)
-        t0 = time.perf_counter()
-        t_next = t0
-        futs = []
-        for i in range(n_q):
-            t_next += gaps[i]
-            delay = t_next - time.perf_counter()
-            if delay > 0:
-                time.sleep(delay)  # releases the GIL to the batcher thread (never spin here)
-            f = qb.submit_arrays(qs[i % 4096])
-            f.add_done_callback(on_done(time.perf_counter()))
-            futs.append(f)
-        for f in futs:
-            f.result()
-        batches, served = qb.batches, qb.queries
-    t_end = max(done)
-    value = len(done) / (t_end - t0)
-    lat_ms = np.array(lat) * 1e3
+        with QueryBatcher(ret, max_batch=64, max_wait_ms=args.max_wait_ms) as qb:
+            for i in range(256):  # warm-up
+                qb.submit_arrays(qs[i % 4096]).result()
+            gaps = rng.exponential(1.0 / args.qps, size=n_q)
+            t0 = time.perf_counter()
+            t_next = t0
+            futs = []
+            for i in range(n_q):
+                t_next += gaps[i]
+                delay = t_next - time.perf_counter()
+                if delay > 0:
+                    time.sleep(delay)  # releases the GIL to the batcher thread (never spin here)
+                f = qb.submit_arrays(qs[i % 4096])
+                f.add_done_callback(on_done(time.perf_counter()))
+                futs.append(f)
+            for f in futs:
+                f.result()
+            batches, served = qb.batches - 0, qb.queries
+        lat = np.array(lat_l)
+        elapsed = max(done) - t0
+        value = len(done) / elapsed
+        front = "Python client thread + QueryBatcher (futures, list[RetrievalResult])"
+    lat_ms = np.asarray(lat) * 1e3
     print(json.dumps({
         "metric": METRIC,
         "value": value,
         "unit": "queries/sec",
         "n_gpus": 1,
-        "steps": batches,
-        "warmup": 256,
-        "ms_per_step": (t_end - t0) / max(batches, 1) * 1e3,
+        "steps": int(batches),
+        "warmup": 4096 if args.stream_front == "native" else 256,
+        "ms_per_step": elapsed / max(batches, 1) * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic: N(0,1) rows and queries L2-normalised then cast to fp16, resident in HBM",
-        "config": {"workload": (f"streaming dense top-{k}: Poisson arrivals at {args.qps:.0f} q/s "
-                                f"for {args.duration:.1f} s, QueryBatcher (<=64, <=2 ms) -> "
-                                f"MI355XRetriever.search_batch over {n} x {dim} fp16 chunks -> "
-                                f"list[RetrievalResult] per caller"),
+        "config": {"workload": (f"streaming dense top-{k}: open-loop Poisson arrivals at "
+                                f"{args.qps:.0f} q/s for {args.duration:.1f} s, {front}, batches "
+                                f"<= 64 / <= {args.max_wait_ms} ms -> exact cosine top-{k} over "
+                                f"{n} x {dim} fp16 chunks"),
                    "n_chunks": n, "dim": dim, "top_k": k, "offered_qps": args.qps,
-                   "parallelism": "single GPU, one batcher thread"},
+                   "front_end": args.stream_front,
+                   "parallelism": "single GPU, batching server"},
         "p50_ms": float(np.percentile(lat_ms, 50)),
         "p99_ms": float(np.percentile(lat_ms, 99)),
         "mean_batch": served / max(batches, 1),

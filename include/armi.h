@@ -136,6 +136,36 @@ int armi_scan_timing_read(double* total_ms, int64_t* launches);
 int armi_kernel_timing_read(int slot, double* total_ms, int64_t* launches);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Streaming query server (BASELINE configs[4] "streaming query at fixed QPS")                 */
+/* ------------------------------------------------------------------------------------------ */
+/* Replaces the reference's per-request search (src/audio_rag/api/v1/query.py:90-115 calling
+ * QdrantRetriever.search, src/audio_rag/retrieval/qdrant.py:227-352, one query per request):
+ * single dense queries submitted from any thread are coalesced into batches of up to max_batch
+ * (a batch leaves when full or max_wait_us after its first query) and answered by
+ * armi_dense_topk on the server's own HIP stream, with up to three batches in flight. Results are
+ * those of armi_dense_topk for that query alone (exact ranking). Thread-safe; the index must
+ * outlive the server. */
+typedef struct armi_stream armi_stream;
+int armi_stream_create(const armi_index* index, int k, int max_batch, double max_wait_us,
+                       armi_stream** out);
+int armi_stream_destroy(armi_stream* server);
+/* query: host fp16 [dim], copied before return; *ticket identifies its result. */
+int armi_stream_submit(armi_stream* server, const uint16_t* query, int64_t* ticket);
+/* Blocks until the ticket's result is published (at most timeout_us), then copies its k
+ * scores / ids / rank keys (each nullable) and the valid count. Results stay readable until
+ * 2^20 later tickets have been submitted. */
+int armi_stream_wait(armi_stream* server, int64_t ticket, float* scores, int64_t* ids,
+                     double* rank, int32_t* count, double timeout_us);
+int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);
+/* Native open-loop load generator (bench.py --workload stream): n_queries arrivals as a
+ * Poisson process at `qps` from one thread, query i = row (i % n_vectors) of `queries` (host
+ * fp16 [n_vectors][dim]); latency_us[i] = completion - submit of query i; elapsed_s = last
+ * completion - first submit. n_queries <= 2^19. */
+int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, int64_t n_vectors,
+                        int64_t n_queries, double qps, uint64_t seed, double* latency_us,
+                        double* elapsed_s, int64_t* completed);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Sparse (lexical-weight) store                                                              */
 /* ------------------------------------------------------------------------------------------ */
 

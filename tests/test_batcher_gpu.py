@@ -1,6 +1,9 @@
-"""QueryBatcher on the GPU: answers coalesced from concurrent callers equal what
-MI355XRetriever.search returns for each query alone (dense, sparse and hybrid, with and
-without a metadata filter)."""
+"""Streaming front ends on the GPU, checked against the CPU oracle (oracle/): answers that
+QueryBatcher coalesces from concurrent callers (dense, sparse and hybrid, with and without a
+metadata filter), and the native StreamServer (libarmi armi_stream_*: dense, concurrent callers,
+its open-loop load generator). Expected results follow QdrantRetriever.search
+(src/audio_rag/retrieval/qdrant.py:227-352): strategy choice, prefetch 2*top_k, RRF 1/(2+pos)
+dense list first, metadata filter on both prefetches."""
 
 import threading
 
@@ -9,34 +12,77 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+N, NQ, K = 4000, 90, 7
 
-def test_batched_answers_equal_single_searches(gpu, oracle_mod):
+
+def _mask(n: int, keep) -> np.ndarray:
+    m = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in range(n):
+        if keep(r):
+            m[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    return m
+
+
+@pytest.fixture(scope="module")
+def store(oracle_mod):
+    rows = oracle_mod.unit_fp16(N, 1024, seed=51)
+    csr = oracle_mod.sparse_corpus(N, seed=52)
+    qi, qx, qv = oracle_mod.sparse_queries(NQ, seed=53)
+    qd = oracle_mod.unit_fp16(NQ, 1024, seed=54)
+    return rows, csr, (qi, qx, qv), qd
+
+
+def _expected(o, store, i: int, st: str, flt) -> list[tuple[str, float]]:
+    """(payload text, score) list the reference path returns for query i."""
+    rows, (ip, ix, iv), (qi, qx, qv), qd = store
+    mask = None if flt is None else _mask(N, lambda r: r % 3 == flt["lecture"])
+    has_sparse = bool(i % 4)
+    mode = o.search_mode(st, True, has_sparse)
+    q1 = qd[i:i + 1]
+    s_ptr = np.array([0, qi[i + 1] - qi[i]], dtype=np.int32)
+    s_idx, s_val = qx[qi[i]:qi[i + 1]], qv[qi[i]:qi[i + 1]]
+    if mode == "dense":
+        d = o.dense_topk(rows, q1, K, row_mask=mask)
+        return [(f"c{d.ids[0, j]}", float(d.scores[0, j])) for j in range(d.count[0])]
+    if mode == "sparse":
+        s = o.sparse_topk(ip, ix, iv, s_ptr, s_idx, s_val, K, row_mask=mask)
+        return [(f"c{s.ids[0, j]}", float(s.scores[0, j])) for j in range(s.count[0])]
+    d = o.dense_topk(rows, q1, 2 * K, row_mask=mask)
+    s = o.sparse_topk(ip, ix, iv, s_ptr, s_idx, s_val, 2 * K, row_mask=mask)
+    fused = o.rrf([d.ids[0, :d.count[0]].tolist(), s.ids[0, :s.count[0]].tolist()], K)
+    return [(f"c{pid}", float(score)) for pid, score in fused]
+
+
+def _retriever(store):
     from audio_rag_amd.config import RetrievalConfig
-    from audio_rag_amd.core import EmbeddingResult, SparseVector
-    from audio_rag_amd.retrieval.batcher import QueryBatcher
     from audio_rag_amd.retrieval.mi355x import MI355XRetriever
 
-    n = 4000
-    rows = oracle_mod.unit_fp16(n, 1024, seed=51).view(np.float16)
-    csr = oracle_mod.sparse_corpus(n, seed=52)
-    sparse = [(csr[1][csr[0][i]:csr[0][i + 1]], csr[2][csr[0][i]:csr[0][i + 1]]) for i in range(n)]
-    payloads = [{"text": f"c{i}", "start": i, "end": i + 1, "speaker": None,
-                 "metadata": {"lecture": i % 3}} for i in range(n)]
-    ret = MI355XRetriever(RetrievalConfig(top_k=7), 1024)
-    ret.add_arrays(rows, payloads, sparse=sparse)
-    qi, qx, qv = oracle_mod.sparse_queries(90, seed=53)
-    qd = oracle_mod.unit_fp16(90, 1024, seed=54).view(np.float16).astype(np.float32)
-    queries = [EmbeddingResult(dense=qd[i].tolist(),
+    rows, (ip, ix, iv), _, _ = store
+    sparse = [(ix[ip[r]:ip[r + 1]], iv[ip[r]:ip[r + 1]]) for r in range(N)]
+    payloads = [{"text": f"c{r}", "start": r, "end": r + 1, "speaker": None,
+                 "metadata": {"lecture": r % 3}} for r in range(N)]
+    ret = MI355XRetriever(RetrievalConfig(top_k=K), 1024)
+    ret.add_arrays(rows.view(np.float16), payloads, sparse=sparse)
+    return ret
+
+
+def test_batched_answers_match_oracle(gpu, oracle_mod, store):
+    from audio_rag_amd.core import EmbeddingResult, SparseVector
+    from audio_rag_amd.retrieval.batcher import QueryBatcher
+
+    ret = _retriever(store)
+    _, _, (qi, qx, qv), qd = store
+    qf = qd.view(np.float16).astype(np.float32)
+    queries = [EmbeddingResult(dense=qf[i].tolist(),
                                sparse=SparseVector(qx[qi[i]:qi[i + 1]].tolist(),
                                                    qv[qi[i]:qi[i + 1]].tolist()) if i % 4 else None)
-               for i in range(90)]
-    filters = [None if i % 5 else {"lecture": i % 3} for i in range(90)]
+               for i in range(NQ)]
+    filters = [None if i % 5 else {"lecture": i % 3} for i in range(NQ)]
     for st in ("hybrid", "dense", "sparse"):
-        want = [ret.search(q, filter_metadata=f, search_type=st) for q, f in zip(queries, filters)]
-        got = [None] * 90
+        got = [None] * NQ
         with QueryBatcher(ret, search_type=st, max_batch=32, max_wait_ms=5.0) as qb:
             def client(lo):
-                for i in range(lo, 90, 3):
+                for i in range(lo, NQ, 3):
                     got[i] = qb.submit(queries[i], filters[i])
             ts = [threading.Thread(target=client, args=(c,)) for c in range(3)]
             for t in ts:
@@ -44,7 +90,58 @@ def test_batched_answers_equal_single_searches(gpu, oracle_mod):
             for t in ts:
                 t.join()
             got = [f.result(timeout=60) for f in got]
-            assert qb.batches < 90
-        for i in range(90):
-            assert [(r.chunk.text, r.score, r.source) for r in got[i]] == \
-                   [(r.chunk.text, r.score, r.source) for r in want[i]], (st, i)
+            assert qb.batches < NQ
+        for i in range(NQ):
+            want = _expected(oracle_mod, store, i, st, filters[i])
+            assert [(r.chunk.text, r.score) for r in got[i]] == want, (st, i)
+            assert all(r.source == "audio_rag" for r in got[i])
+
+
+def test_stream_server_matches_oracle(gpu, oracle_mod, store):
+    """Native server: 4 caller threads submit single queries concurrently; every ticket's
+    answer equals the oracle's dense top-k; the batches coalesce."""
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    rows, _, _, qd = store
+    want = oracle_mod.dense_topk(rows, qd, K)
+    got = [None] * NQ
+    with StreamServer(ret, max_batch=16, max_wait_ms=3.0) as srv:
+        def client(lo):
+            tickets = [(i, srv.submit_arrays(qd[i].view(np.float16))) for i in range(lo, NQ, 4)]
+            for i, t in tickets:
+                got[i] = srv.result(t)
+        ts = [threading.Thread(target=client, args=(c,)) for c in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        batches, served = srv.stats()
+        assert served == NQ and batches < NQ, (batches, served)
+    for i in range(NQ):
+        assert [r.chunk.text for r in got[i]] == [f"c{p}" for p in want.ids[i, :want.count[i]]], i
+        assert [r.score for r in got[i]] == [float(s) for s in want.scores[i, :want.count[i]]], i
+
+
+def test_stream_server_loadgen_and_filtered_edge(gpu, oracle_mod, store):
+    """The native load generator completes every arrival with positive latencies; a server over
+    a tiny store returns fewer than k results where the store has fewer rows."""
+    from audio_rag_amd.config import RetrievalConfig
+    from audio_rag_amd.retrieval.batcher import StreamServer
+    from audio_rag_amd.retrieval.mi355x import MI355XRetriever
+
+    ret = _retriever(store)
+    _, _, _, qd = store
+    with StreamServer(ret, max_batch=64, max_wait_ms=1.0) as srv:
+        lat, elapsed = srv.loadgen(qd.view(np.float16), 3000, qps=20000.0, seed=3)
+        assert lat.shape == (3000,) and (lat > 0).all() and elapsed > 0
+        batches, served = srv.stats()
+        assert served == 3000 and batches <= 3000
+    small = MI355XRetriever(RetrievalConfig(top_k=K), 1024)
+    rows3 = oracle_mod.unit_fp16(3, 1024, seed=61)
+    small.add_arrays(rows3.view(np.float16), [{"text": f"s{r}", "metadata": {}} for r in range(3)])
+    with StreamServer(small, max_batch=8, max_wait_ms=0.5) as srv:
+        res = srv.result(srv.submit_arrays(qd[0].view(np.float16)))
+    want = oracle_mod.dense_topk(rows3, qd[:1], K)
+    assert want.count[0] == 3
+    assert [r.chunk.text for r in res] == [f"s{p}" for p in want.ids[0, :3]]
