@@ -228,7 +228,8 @@ def main() -> None:
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=30)
-    ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline"],
+    ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
+                                           "ingest"],
                     default="dense",
                     help="dense: BASELINE metric (default); hybrid: dense+sparse prefetch 2k + RRF "
                          "(configs[2] without rerank); hybrid_rerank: configs[2]: top-20 fused -> "
@@ -245,6 +246,9 @@ def main() -> None:
                     help="stream: native StreamServer + native load generator, or a Python "
                          "client through QueryBatcher")
     ap.add_argument("--max-wait-ms", type=float, default=2.0, help="stream: batching window")
+    ap.add_argument("--ingest-chunks", type=int, default=20000, help="ingest: chunks embedded")
+    ap.add_argument("--max-batch", type=int, default=64,
+                    help="stream (native): largest batch the server coalesces")
     ap.add_argument("--initial-k", type=int, default=20)
     ap.add_argument("--rerank-dtype", choices=["fp32", "bf16", "fp16"], default="fp16",
                     help="cross-encoder GEMM dtype (fp16: fp16 GEMMs + fused fp16 attention, "
@@ -255,6 +259,8 @@ def main() -> None:
         return stream_main(args)
     if args.workload == "pipeline":
         return pipeline_main(args)
+    if args.workload == "ingest":
+        return ingest_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -648,6 +654,89 @@ def pipeline_main(args) -> None:
     }), flush=True)
 
 
+def ingest_main(args) -> None:
+    """configs[4] after ASR (faster-whisper is not installed; the reference's ingest stages up to
+    the transcript stay out of scope): --ingest-chunks synthetic transcript chunks (40-100 words)
+    -> BGEM3Embedder.embed (24-layer XLM-R large fp16, batch_size 32, dense + lexical weights,
+    embeddings/bge.py:104-135) -> MI355XRetriever.add (qdrant.py:140-225, reference sparse-drop
+    by default) -> the native StreamServer over the new collection under open-loop Poisson load
+    at --qps (dense top-k). value = completed streaming queries / s; the embed and index rates
+    ride along. Weights are seeded (no checkpoints offline)."""
+    import logging
+
+    from audio_rag_amd.config.schema import AudioRAGConfig
+    from audio_rag_amd.core.base import AudioChunk
+    from audio_rag_amd.embeddings.bge_m3 import BGEM3Embedder
+    from audio_rag_amd.retrieval.batcher import StreamServer
+    from audio_rag_amd.retrieval.mi355x import MI355XRetriever
+
+    logging.disable(logging.INFO)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = AudioRAGConfig()
+    rng = np.random.default_rng(13)
+    n = args.ingest_chunks
+    texts = [" ".join(rng.choice(WORDS, size=int(rng.integers(40, 100)))) for _ in range(n)]
+    chunks = [AudioChunk(text=t, start=30.0 * i, end=30.0 * i + 30.0, speaker=f"SPEAKER_{i % 2}",
+                         metadata={"lecture": i % 7}) for i, t in enumerate(texts)]
+    emb = BGEM3Embedder(cfg.embedding, device=dev)
+    emb.load()
+    emb.embed(texts[:64])  # warm-up (kernel selection)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    embeddings = emb.embed(texts)
+    torch.cuda.synchronize()
+    t_embed = time.perf_counter() - t0
+    ret = MI355XRetriever(cfg.retrieval, emb.dimension)
+    t0 = time.perf_counter()
+    ret.add(chunks, embeddings)
+    ret._collections[ret._resolve_collection(None)].dense_index  # build the device index
+    torch.cuda.synchronize()
+    t_index = time.perf_counter() - t0
+    q_texts = [" ".join(rng.choice(WORDS, size=int(rng.integers(6, 16)))) for _ in range(256)]
+    qd, _ = emb.embed_queries(q_texts)
+    qs = qd.cpu().numpy()
+    n_q = int(args.qps * args.duration)
+    k = cfg.retrieval.top_k
+    with StreamServer(ret, top_k=k, max_batch=64, max_wait_ms=args.max_wait_ms) as srv:
+        srv.loadgen(qs, min(n_q, 4096), qps=args.qps, seed=6)  # warm-up
+        b0, q0 = srv.stats()
+        lat, elapsed = srv.loadgen(qs, n_q, qps=args.qps, seed=7)
+        b1, q1 = srv.stats()
+    batches, served = b1 - b0, q1 - q0
+    lat_ms = lat * 1e3
+    print(json.dumps({
+        "metric": METRIC,
+        "value": n_q / elapsed,
+        "unit": "queries/sec",
+        "n_gpus": 1,
+        "steps": int(batches),
+        "warmup": min(n_q, 4096),
+        "ms_per_step": elapsed / max(batches, 1) * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": ("synthetic transcript chunks (lecture vocabulary), seeded BGE-M3 weights, "
+                 "queries embedded by the same model"),
+        "config": {"workload": (f"configs[4] after ASR: {n} chunks -> BGE-M3 embed (24 layers "
+                                f"fp16, batch {cfg.embedding.batch_size}) -> MI355XRetriever.add "
+                                f"-> native StreamServer, open-loop Poisson queries at "
+                                f"{args.qps:.0f} q/s for {args.duration:.1f} s, dense top-{k}"),
+                   "n_chunks": n, "dim": emb.dimension, "top_k": k, "offered_qps": args.qps,
+                   "parallelism": "single GPU"},
+        "embed_chunks_per_s": n / t_embed,
+        "embed_s": t_embed,
+        "index_chunks_per_s": n / t_index,
+        "index_s": t_index,
+        "p50_ms": float(np.percentile(lat_ms, 50)),
+        "p99_ms": float(np.percentile(lat_ms, 99)),
+        "mean_batch": served / max(batches, 1),
+        "roofline": None,
+        "cpu_baseline": None,
+    }), flush=True)
+
+
 def stream_main(args) -> None:
     """configs[4]'s query side on one GPU: single dense queries arrive as an open-loop Poisson
     process at --qps over the 1M-chunk store. Default front end: the native StreamServer
@@ -672,7 +761,7 @@ def stream_main(args) -> None:
     qs = make_queries(1, 4096, dim, dev, seed=1)[0].cpu().numpy()
     n_q = int(args.qps * args.duration)
     if args.stream_front == "native":
-        with StreamServer(ret, max_batch=64, max_wait_ms=args.max_wait_ms) as srv:
+        with StreamServer(ret, max_batch=args.max_batch, max_wait_ms=args.max_wait_ms) as srv:
             srv.loadgen(qs, 4096, qps=args.qps, seed=6)  # warm-up
             b0, q0 = srv.stats()
             lat, elapsed = srv.loadgen(qs, n_q, qps=args.qps, seed=7)
@@ -735,7 +824,8 @@ def stream_main(args) -> None:
         "data": "synthetic: N(0,1) rows and queries L2-normalised then cast to fp16, resident in HBM",
         "config": {"workload": (f"streaming dense top-{k}: open-loop Poisson arrivals at "
                                 f"{args.qps:.0f} q/s for {args.duration:.1f} s, {front}, batches "
-                                f"<= 64 / <= {args.max_wait_ms} ms -> exact cosine top-{k} over "
+                                f"<= {args.max_batch} / <= {args.max_wait_ms} ms -> exact cosine "
+                                f"top-{k} over "
                                 f"{n} x {dim} fp16 chunks"),
                    "n_chunks": n, "dim": dim, "top_k": k, "offered_qps": args.qps,
                    "front_end": args.stream_front,
