@@ -25,6 +25,24 @@ from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex
 BGE_M3_VOCAB = 250002
 
 
+_NO_MATCH = object()
+
+
+def _canon(x):
+    """The equivalence class _match_value compares a scalar in: bools only equal bools,
+    integral numbers compare by value, non-integral floats never match, strings by value.
+    None when the value needs the general comparison."""
+    if isinstance(x, bool):
+        return ("bool", x)
+    if isinstance(x, int):
+        return ("num", x)
+    if isinstance(x, float):
+        return ("num", int(x)) if x.is_integer() else _NO_MATCH
+    if isinstance(x, str):
+        return ("str", x)
+    return None
+
+
 def _match_value(field_value, wanted) -> bool:
     """Qdrant MatchValue: equality on keyword / integer / bool payload values; an array field
     matches when any element does."""
@@ -52,6 +70,7 @@ class ChunkCollection:
     _sparse: SparseIndex | None = None
     _built_rows: int = -1
     _mask_cache: dict = field(default_factory=dict)
+    _key_index: dict = field(default_factory=dict)   # metadata key -> (count, {canon: ordinals})
     _lock: threading.Lock = field(default_factory=threading.Lock)
     _frozen: bool = False
 
@@ -79,6 +98,7 @@ class ChunkCollection:
             self.sparse_rows.extend(sparse)
             self.payloads.extend(payloads)
             self._mask_cache.clear()
+            self._key_index.clear()
 
     # ------------------------------------------------------------------------------- build
 
@@ -132,16 +152,52 @@ class ChunkCollection:
         if cached is not None and cached[0] == self.count:
             return cached[1]
         n = self.count
-        ok = np.zeros(n, dtype=bool)
-        for i, p in enumerate(self.payloads):
-            md = p.get("metadata") or {}
-            ok[i] = all(k in md and _match_value(md[k], v) for k, v in filter_metadata.items())
+        ok = np.ones(n, dtype=bool)
+        for k, v in filter_metadata.items():
+            ok &= self._key_matches(k, v, n)
         words = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
         idx = np.nonzero(ok)[0]
         np.bitwise_or.at(words, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
         mask = torch.from_numpy(words.view(np.int64)).to(self.device)
         self._mask_cache[key] = (n, mask)
         return mask
+
+    def _key_matches(self, key: str, wanted, n: int) -> np.ndarray:
+        """bool [n]: points whose metadata[key] matches `wanted` (_match_value). One pass over
+        the payloads per metadata key (cached until the next upsert) builds an inverted map
+        value-class -> ordinals, so a new filter value costs O(matches), not O(points)."""
+        cached = self._key_index.get(key)
+        if cached is None or cached[0] != n:
+            inv: dict = {}
+            general: list[int] = []  # points whose value needs the general comparison
+            for i, p in enumerate(self.payloads[:n]):
+                md = p.get("metadata") or {}
+                if key not in md:
+                    continue
+                fv = md[key]
+                for x in (fv if isinstance(fv, list) else (fv,)):
+                    c = _canon(x)
+                    if c is None:
+                        general.append(i)
+                    elif c is not _NO_MATCH:
+                        inv.setdefault(c, []).append(i)
+            cached = (n, {c: np.unique(np.asarray(v, dtype=np.int64)) for c, v in inv.items()},
+                      general)
+            self._key_index[key] = cached
+        _, inv, general = cached
+        ok = np.zeros(n, dtype=bool)
+        c = _canon(wanted)
+        if c is not None and c is not _NO_MATCH and c in inv:
+            ok[inv[c]] = True
+        for i in general:  # rare value types (None, dicts): the reference comparison
+            if not ok[i] and _match_value(self.payloads[i]["metadata"][key], wanted):
+                ok[i] = True
+        if c is None:  # an unusual wanted value: compare every point that has the key
+            for i, p in enumerate(self.payloads[:n]):
+                md = p.get("metadata") or {}
+                if key in md and _match_value(md[key], wanted):
+                    ok[i] = True
+        return ok
 
     @classmethod
     def from_indexes(cls, name: str, dense: DenseIndex, payloads: list[dict],
