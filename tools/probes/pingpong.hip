@@ -28,10 +28,24 @@ __global__ __launch_bounds__(512) void pingpong(long long* out, int iters, float
   u32x4 fr[12];
   for (int j = 0; j < 12; ++j) fr[j] = u32x4{(uint32_t)j, 1u, 2u, 3u};
   f32x16 c0 = {}, c1 = {};
+  u32x4 stage0 = {0u, 0u, 0u, 0u}, stage1 = {0u, 0u, 0u, 0u};
   if (STAGGER && wave >= 4) __builtin_amdgcn_s_barrier();
   const long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
-    if (GLDS) {
+    if (GLDS == 2) {
+      // register staging of the same 2 KB: 2 x global_load_dwordx4 (16 B / lane) -> 2 x
+      // ds_write_b128 into the upper 64 KB, the loads issued one phase ahead of their write
+      const long long e = ((((long long)blockIdx.x * iters + it) * 16 + wave * 2) * 512 + lane * 8) &
+                          (src_elems - 1);
+      u32x4 x0 = *reinterpret_cast<const u32x4*>(src + e);
+      u32x4 x1 = *reinterpret_cast<const u32x4*>(src + ((e + 512) & (src_elems - 1)));
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      const uint32_t wa = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(smem + 65536 + ((it & 3) * 16 + wave * 2) * 1024) + lane * 16;
+      asm volatile("ds_write_b128 %0, %1" :: "v"(wa), "v"(stage0) : "memory");
+      asm volatile("ds_write_b128 %0, %1 offset:1024" :: "v"(wa), "v"(stage1) : "memory");
+      stage0 = x0;
+      stage1 = x1;
+    } else if (GLDS) {
       // 2 x 1 KB LDS-DMA per wave into the upper 64 KB (8 rows x 128 B each, like the scan's
       // pieces), streaming through `src`; then keep 3 phases (6 instructions) in flight
 #pragma unroll
@@ -79,6 +93,7 @@ __global__ __launch_bounds__(512) void pingpong(long long* out, int iters, float
   float s = 0.f;
   for (int j = 0; j < 16; ++j) s += c0[j] + c1[j];
   for (int j = 0; j < 12; ++j) s += __uint_as_float(fr[j].x);
+  s += __uint_as_float(stage0.x) + __uint_as_float(stage1.y);
   if (s == 123.456f) sink[threadIdx.x] = s;
   if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
 }
@@ -118,13 +133,12 @@ void run(const char* name, int iters, long long src_elems = 1 << 20) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 4000;
-  run<0, 8, 1, 1, 1, 3>("nread=8 glds L2 inflight=3", iters, 1 << 20);
-  run<0, 8, 1, 1, 1, 5>("nread=8 glds L2 inflight=5", iters, 1 << 20);
-  run<0, 8, 1, 1, 1, 7>("nread=8 glds L2 inflight=7", iters, 1 << 20);
-  run<0, 8, 1, 1, 1, 11>("nread=8 glds L2 inflight=11", iters, 1 << 20);
-  run<0, 8, 1, 0, 1, 7>("nread=8 glds L2 inflight=7 mfma=0", iters, 1 << 20);
-  run<0, 0, 1, 0, 1, 11>("nread=0 glds L2 inflight=11 mfma=0", iters, 1 << 20);
-  run<0, 8, 1, 1, 1, 7>("nread=8 glds 64MB inflight=7", iters, 1LL << 25);
-  run<0, 8, 1, 1, 1, 7>("nread=8 glds HBM inflight=7", iters, 1LL << 30);
+  run<0, 8, 1, 1>("nread=8 no staging", iters);
+  run<0, 8, 1, 1, 1, 3>("nread=8 glds L2", iters, 1 << 20);
+  run<0, 8, 1, 1, 2, 3>("nread=8 regstage L2", iters, 1 << 20);
+  run<0, 8, 1, 1, 1, 3>("nread=8 glds HBM", iters, 1LL << 30);
+  run<0, 8, 1, 1, 2, 3>("nread=8 regstage HBM", iters, 1LL << 30);
+  run<0, 8, 1, 0, 2, 3>("nread=8 regstage L2 mfma=0", iters, 1 << 20);
+  run<0, 8, 0, 1, 2, 3>("nread=8 regstage L2 stagger=0", iters, 1 << 20);
   return 0;
 }
