@@ -50,12 +50,18 @@ SIGNATURES: dict[str, tuple] = {
     "armi_scan_timing_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_kernel_timing_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_stream_create": (c_int, [c_void_p, c_int, c_int, ctypes.c_double, ctypes.POINTER(c_void_p)]),
+    "armi_stream_create_hybrid": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_double,
+                                          ctypes.POINTER(c_void_p)]),
     "armi_stream_destroy": (c_int, [c_void_p]),
     "armi_stream_submit": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int64)]),
-    "armi_stream_wait": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_double]),
+    "armi_stream_submit_hybrid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                          ctypes.POINTER(c_int64)]),
+    "armi_stream_wait": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 ctypes.c_double]),
     "armi_stream_stats": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
-    "armi_stream_loadgen": (c_int, [c_void_p, c_void_p, c_int64, c_int64, ctypes.c_double, ctypes.c_uint64,
-                                    c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
+    "armi_stream_loadgen": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                    ctypes.c_double, ctypes.c_uint64, c_void_p,
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_sparse_index_create": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                          c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_sparse_index_destroy": (c_int, [c_void_p]),

@@ -16,7 +16,10 @@
 //     result ring, stamp the completion time, wake the waiters.
 //   wait (caller): block until its ticket's ring entry is complete, copy the results out.
 // Per-query semantics are armi_dense_topk's (exact cosine ranking, certified fast scan, exact
-// fallback inside the call); only the grouping is new.
+// fallback inside the call); only the grouping is new. A hybrid server (armi_stream_create_hybrid)
+// answers each query as QdrantRetriever.search's hybrid branch does (qdrant.py:272-298): dense and
+// sparse prefetches of 2k, RRF 1/(rrf_k + pos) with the dense list first, limit k; a query
+// submitted without sparse terms takes the dense branch (qdrant.py:316-323: its dense top-k).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -40,6 +43,7 @@ inline int64_t now_ns() {
 }
 
 constexpr int kSlots = 3;           // batches in flight (GPU running / collected / collecting)
+constexpr int kMaxTerms = 256;      // sparse terms per query (armi_sparse_topk's limit)
 constexpr int64_t kRing = 1 << 20;  // result ring entries (tickets alive at once)
 
 struct Slot {
@@ -59,6 +63,25 @@ struct Slot {
   int32_t* h_count = nullptr;
   hipEvent_t done = nullptr;
   int status = ARMI_OK;
+  // hybrid servers: the batch's sparse query CSR (pinned + device), prefetch lists, fusion
+  int nnz = 0;
+  int32_t* h_sp_ptr = nullptr;       // [max_batch + 1]
+  int32_t* h_sp_idx = nullptr;       // [max_batch * kMaxTerms]
+  float* h_sp_val = nullptr;
+  int32_t* d_sp_ptr = nullptr;
+  int32_t* d_sp_idx = nullptr;
+  float* d_sp_val = nullptr;
+  float* d_sp_scores = nullptr;      // [max_batch][2k]
+  int64_t* d_sp_ids = nullptr;
+  int32_t* d_sp_count = nullptr;
+  uint32_t* d_sp_flags = nullptr;
+  void* d_sp_ws = nullptr;
+  int64_t* d_f_ids = nullptr;        // fused [max_batch][k]
+  double* d_f_score = nullptr;
+  int32_t* d_f_count = nullptr;
+  int64_t* h_f_ids = nullptr;
+  double* h_f_score = nullptr;
+  int32_t* h_f_count = nullptr;
 };
 
 struct Entry {
@@ -66,6 +89,7 @@ struct Entry {
   int64_t t_submit = 0;
   int64_t t_done = 0;
   int32_t count = 0;
+  int32_t mode = 0;                  // 0 dense branch, 1 hybrid (RRF scores in rank)
   int status = ARMI_OK;
 };
 
@@ -73,6 +97,11 @@ struct Entry {
 
 struct armi_stream {
   const armi_index* idx = nullptr;
+  const armi_sparse_index* sidx = nullptr;  // non-null: hybrid server
+  int rrf_k = 2;
+  int kp = 0;                               // dense prefetch limit (2k hybrid, k dense)
+  size_t sws_bytes = 0;
+  std::vector<int32_t> nnz_of;              // per ring entry: sparse terms of the query
   int k = 0, max_batch = 0, dim = 0;
   int64_t max_wait_ns = 0;
   size_t ws_bytes = 0;
@@ -105,10 +134,34 @@ namespace {
 int launch_slot(armi_stream* s, Slot& sl) {
   const size_t qbytes = (size_t)sl.n * s->dim * sizeof(uint16_t);
   ARMI_HIP(hipMemcpyAsync(sl.d_queries, sl.h_queries, qbytes, hipMemcpyHostToDevice, s->stream));
-  int rc = armi_dense_topk(s->idx, sl.d_queries, sl.n, s->k, nullptr, sl.d_scores, sl.d_ids,
+  int rc = armi_dense_topk(s->idx, sl.d_queries, sl.n, s->kp, nullptr, sl.d_scores, sl.d_ids,
                            sl.d_rank, sl.d_count, sl.d_flags, sl.d_ws, s->ws_bytes, s->stream);
   if (rc != ARMI_OK) return rc;
-  const size_t nk = (size_t)sl.n * s->k;
+  if (s->sidx) {
+    ARMI_HIP(hipMemcpyAsync(sl.d_sp_ptr, sl.h_sp_ptr, (size_t)(sl.n + 1) * sizeof(int32_t),
+                            hipMemcpyHostToDevice, s->stream));
+    if (sl.nnz > 0) {
+      ARMI_HIP(hipMemcpyAsync(sl.d_sp_idx, sl.h_sp_idx, (size_t)sl.nnz * sizeof(int32_t),
+                              hipMemcpyHostToDevice, s->stream));
+      ARMI_HIP(hipMemcpyAsync(sl.d_sp_val, sl.h_sp_val, (size_t)sl.nnz * sizeof(float),
+                              hipMemcpyHostToDevice, s->stream));
+    }
+    rc = armi_sparse_topk(s->sidx, sl.d_sp_ptr, sl.d_sp_idx, sl.d_sp_val, sl.n, s->kp, nullptr,
+                          sl.d_sp_scores, sl.d_sp_ids, sl.d_sp_count, sl.d_sp_flags, sl.d_sp_ws,
+                          s->sws_bytes, s->stream);
+    if (rc != ARMI_OK) return rc;
+    rc = armi_rrf_fuse(sl.d_ids, sl.d_count, s->kp, sl.d_sp_ids, sl.d_sp_count, s->kp, sl.n,
+                       s->rrf_k, s->k, sl.d_f_ids, sl.d_f_score, sl.d_f_count, s->stream);
+    if (rc != ARMI_OK) return rc;
+    const size_t nf = (size_t)sl.n * s->k;
+    ARMI_HIP(hipMemcpyAsync(sl.h_f_ids, sl.d_f_ids, nf * sizeof(int64_t), hipMemcpyDeviceToHost,
+                            s->stream));
+    ARMI_HIP(hipMemcpyAsync(sl.h_f_score, sl.d_f_score, nf * sizeof(double),
+                            hipMemcpyDeviceToHost, s->stream));
+    ARMI_HIP(hipMemcpyAsync(sl.h_f_count, sl.d_f_count, (size_t)sl.n * sizeof(int32_t),
+                            hipMemcpyDeviceToHost, s->stream));
+  }
+  const size_t nk = (size_t)sl.n * s->kp;
   ARMI_HIP(hipMemcpyAsync(sl.h_scores, sl.d_scores, nk * sizeof(float), hipMemcpyDeviceToHost,
                           s->stream));
   ARMI_HIP(hipMemcpyAsync(sl.h_ids, sl.d_ids, nk * sizeof(int64_t), hipMemcpyDeviceToHost,
@@ -172,11 +225,24 @@ void completer_main(armi_stream* s) {
       const int64_t tk = sl.first_ticket + i;
       Entry& e = s->ring[tk % kRing];
       const size_t o = (size_t)(tk % kRing) * s->k;
-      if (status == ARMI_OK) {
-        std::memcpy(&s->r_scores[o], sl.h_scores + (size_t)i * s->k, s->k * sizeof(float));
-        std::memcpy(&s->r_ids[o], sl.h_ids + (size_t)i * s->k, s->k * sizeof(int64_t));
-        std::memcpy(&s->r_rank[o], sl.h_rank + (size_t)i * s->k, s->k * sizeof(double));
-        e.count = sl.h_count[i];
+      if (status == ARMI_OK && s->sidx && s->nnz_of[tk % kRing] > 0) {
+        // hybrid branch: the fused list, hit.score = the RRF score (rank holds it in fp64)
+        const size_t f = (size_t)i * s->k;
+        e.count = sl.h_f_count[i];
+        for (int j = 0; j < s->k; ++j) {
+          s->r_ids[o + j] = sl.h_f_ids[f + j];
+          s->r_rank[o + j] = sl.h_f_score[f + j];
+          s->r_scores[o + j] = (float)sl.h_f_score[f + j];
+        }
+        e.mode = 1;
+      } else if (status == ARMI_OK) {
+        // dense branch: the first k of the dense list (prefetch 2k on a hybrid server)
+        const size_t d = (size_t)i * s->kp;
+        std::memcpy(&s->r_scores[o], sl.h_scores + d, s->k * sizeof(float));
+        std::memcpy(&s->r_ids[o], sl.h_ids + d, s->k * sizeof(int64_t));
+        std::memcpy(&s->r_rank[o], sl.h_rank + d, s->k * sizeof(double));
+        e.count = std::min(sl.h_count[i], s->k);
+        e.mode = 0;
       } else {
         e.count = 0;
       }
@@ -188,6 +254,7 @@ void completer_main(armi_stream* s) {
     s->queries.fetch_add(sl.n);
     lk.lock();
     sl.n = 0;
+    sl.nnz = 0;
     s->launched.pop_front();
     ++s->free_slots;
     s->cv_done.notify_all();
@@ -201,8 +268,14 @@ void free_slot(Slot& sl) {
   if (sl.h_ids) (void)hipHostFree(sl.h_ids);
   if (sl.h_rank) (void)hipHostFree(sl.h_rank);
   if (sl.h_count) (void)hipHostFree(sl.h_count);
+  for (void* p : {(void*)sl.h_sp_ptr, (void*)sl.h_sp_idx, (void*)sl.h_sp_val, (void*)sl.h_f_ids,
+                  (void*)sl.h_f_score, (void*)sl.h_f_count})
+    if (p) (void)hipHostFree(p);
   for (void* p : {(void*)sl.d_queries, (void*)sl.d_scores, (void*)sl.d_ids, (void*)sl.d_rank,
-                  (void*)sl.d_count, (void*)sl.d_flags, sl.d_ws})
+                  (void*)sl.d_count, (void*)sl.d_flags, sl.d_ws, (void*)sl.d_sp_ptr,
+                  (void*)sl.d_sp_idx, (void*)sl.d_sp_val, (void*)sl.d_sp_scores,
+                  (void*)sl.d_sp_ids, (void*)sl.d_sp_count, (void*)sl.d_sp_flags, sl.d_sp_ws,
+                  (void*)sl.d_f_ids, (void*)sl.d_f_score, (void*)sl.d_f_count})
     if (p) (void)hipFree(p);
   if (sl.done) (void)hipEventDestroy(sl.done);
   sl = Slot{};
@@ -229,7 +302,7 @@ void shutdown(armi_stream* s) {
 }
 
 int alloc_slot(armi_stream* s, Slot& sl) {
-  const size_t nq = (size_t)s->max_batch, nk = nq * s->k;
+  const size_t nq = (size_t)s->max_batch, nk = nq * s->kp;
   ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_queries), nq * s->dim * 2));
   ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_scores), nk * sizeof(float)));
   ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_ids), nk * sizeof(int64_t)));
@@ -243,29 +316,56 @@ int alloc_slot(armi_stream* s, Slot& sl) {
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_flags), nq * sizeof(uint32_t)));
   ARMI_HIP(hipMalloc(&sl.d_ws, s->ws_bytes));
   ARMI_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  if (s->sidx) {
+    const size_t nt = nq * kMaxTerms, nf = nq * s->k;
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_ptr), (nq + 1) * sizeof(int32_t)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_idx), nt * sizeof(int32_t)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_val), nt * sizeof(float)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_ids), nf * sizeof(int64_t)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_score), nf * sizeof(double)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_count), nq * sizeof(int32_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_ptr), (nq + 1) * sizeof(int32_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_idx), nt * sizeof(int32_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_val), nt * sizeof(float)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_scores), nk * sizeof(float)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_ids), nk * sizeof(int64_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_count), nq * sizeof(int32_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_flags), nq * sizeof(uint32_t)));
+    ARMI_HIP(hipMalloc(&sl.d_sp_ws, s->sws_bytes));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_f_ids), nf * sizeof(int64_t)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_f_score), nf * sizeof(double)));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_f_count), nq * sizeof(int32_t)));
+    sl.h_sp_ptr[0] = 0;
+  }
   return ARMI_OK;
 }
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int armi_stream_create(const armi_index* idx, int k, int max_batch, double max_wait_us,
-                       armi_stream** out) {
+int create_impl(const armi_index* idx, const armi_sparse_index* sidx, int k, int rrf_k,
+                int max_batch, double max_wait_us, armi_stream** out) {
   ARMI_REQUIRE(idx && out, "armi_stream_create: null pointer argument");
-  ARMI_REQUIRE(k >= 1 && k <= 240, "armi_stream_create: k must be in [1, 240]");
+  ARMI_REQUIRE(k >= 1 && k <= (sidx ? 120 : 240), "armi_stream_create: k out of range");
   ARMI_REQUIRE(max_batch >= 1 && max_batch <= 4096, "armi_stream_create: max_batch in [1, 4096]");
   ARMI_REQUIRE(max_wait_us >= 0.0, "armi_stream_create: max_wait_us < 0");
+  ARMI_REQUIRE(rrf_k >= 1, "armi_stream_create: rrf_k must be >= 1");
   *out = nullptr;
   auto* s = new armi_stream();
   s->idx = idx;
+  s->sidx = sidx;
+  s->rrf_k = rrf_k;
   s->k = k;
+  s->kp = sidx ? 2 * k : k;
   s->max_batch = max_batch;
   s->dim = armi_index_dim(idx);
   s->max_wait_ns = (int64_t)(max_wait_us * 1e3);
   s->device = idx->device;
-  s->ws_bytes = armi_dense_workspace_bytes(idx, max_batch, k);
+  s->ws_bytes = armi_dense_workspace_bytes(idx, max_batch, s->kp);
+  if (sidx) s->sws_bytes = armi_sparse_workspace_bytes(sidx, max_batch, s->kp);
   s->ring = std::vector<Entry>(kRing);
+  s->nnz_of.assign(kRing, 0);
   s->r_scores.assign((size_t)kRing * k, 0.f);
   s->r_ids.assign((size_t)kRing * k, -1);
   s->r_rank.assign((size_t)kRing * k, 0.0);
@@ -286,15 +386,12 @@ int armi_stream_create(const armi_index* idx, int k, int max_batch, double max_w
   return ARMI_OK;
 }
 
-int armi_stream_destroy(armi_stream* s) {
-  if (!s) return ARMI_OK;
-  shutdown(s);
-  delete s;
-  return ARMI_OK;
-}
-
-int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
+int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
+                const float* sp_val, int nnz, int64_t* ticket) {
   ARMI_REQUIRE(s && query && ticket, "armi_stream_submit: null pointer argument");
+  ARMI_REQUIRE(nnz >= 0 && nnz <= kMaxTerms, "armi_stream_submit: nnz must be in [0, 256]");
+  ARMI_REQUIRE(nnz == 0 || (s->sidx && sp_idx && sp_val),
+               "armi_stream_submit: sparse terms need a hybrid server and both arrays");
   std::unique_lock<std::mutex> lk(s->mu);
   for (;;) {
     if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_submit: server stopped");
@@ -308,6 +405,15 @@ int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
     s->first_submit_ns = now_ns();
   }
   std::memcpy(c.h_queries + (size_t)c.n * s->dim, query, (size_t)s->dim * sizeof(uint16_t));
+  if (s->sidx) {
+    if (nnz > 0) {
+      std::memcpy(c.h_sp_idx + c.nnz, sp_idx, (size_t)nnz * sizeof(int32_t));
+      std::memcpy(c.h_sp_val + c.nnz, sp_val, (size_t)nnz * sizeof(float));
+    }
+    c.nnz += nnz;
+    c.h_sp_ptr[c.n + 1] = c.nnz;
+    s->nnz_of[tk % kRing] = nnz;
+  }
   Entry& e = s->ring[tk % kRing];
   e.t_submit = now_ns();
   ++c.n;
@@ -318,8 +424,39 @@ int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
   return ARMI_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int armi_stream_create(const armi_index* idx, int k, int max_batch, double max_wait_us,
+                       armi_stream** out) {
+  return create_impl(idx, nullptr, k, 2, max_batch, max_wait_us, out);
+}
+
+int armi_stream_create_hybrid(const armi_index* idx, const armi_sparse_index* sidx, int k,
+                              int rrf_k, int max_batch, double max_wait_us, armi_stream** out) {
+  ARMI_REQUIRE(sidx, "armi_stream_create_hybrid: sparse index is null");
+  return create_impl(idx, sidx, k, rrf_k, max_batch, max_wait_us, out);
+}
+
+int armi_stream_destroy(armi_stream* s) {
+  if (!s) return ARMI_OK;
+  shutdown(s);
+  delete s;
+  return ARMI_OK;
+}
+
+int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
+  return submit_impl(s, query, nullptr, nullptr, 0, ticket);
+}
+
+int armi_stream_submit_hybrid(armi_stream* s, const uint16_t* query, const int32_t* sp_indices,
+                              const float* sp_values, int nnz, int64_t* ticket) {
+  return submit_impl(s, query, sp_indices, sp_values, nnz, ticket);
+}
+
 int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids, double* rank,
-                     int32_t* count, double timeout_us) {
+                     int32_t* count, int32_t* mode, double timeout_us) {
   ARMI_REQUIRE(s && count, "armi_stream_wait: null pointer argument");
   ARMI_REQUIRE(ticket >= 0, "armi_stream_wait: bad ticket");
   Entry& e = s->ring[ticket % kRing];
@@ -341,6 +478,7 @@ int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids
   if (scores) std::memcpy(scores, &s->r_scores[o], s->k * sizeof(float));
   if (ids) std::memcpy(ids, &s->r_ids[o], s->k * sizeof(int64_t));
   if (rank) std::memcpy(rank, &s->r_rank[o], s->k * sizeof(double));
+  if (mode) *mode = e.mode;
   *count = e.count;
   return ARMI_OK;
 }
@@ -352,7 +490,8 @@ int armi_stream_stats(armi_stream* s, int64_t* batches, int64_t* queries) {
   return ARMI_OK;
 }
 
-int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, int64_t n_vectors,
+int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* q_indptr,
+                        const int32_t* q_indices, const float* q_values, int64_t n_vectors,
                         int64_t n_queries, double qps, uint64_t seed, double* latency_us,
                         double* elapsed_s, int64_t* completed) {
   ARMI_REQUIRE(s && queries && latency_us && elapsed_s && completed,
@@ -373,14 +512,19 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, int64_t n_vecto
       if (t >= due_ns) break;
       if (due_ns - t > 100000) std::this_thread::sleep_for(std::chrono::nanoseconds(due_ns - t - 50000));
     }
-    if (int rc = armi_stream_submit(s, queries + (size_t)(i % n_vectors) * s->dim,
-                                    &tickets[(size_t)i]))
+    const int64_t v = i % n_vectors;
+    const int nnz = q_indptr ? q_indptr[v + 1] - q_indptr[v] : 0;
+    if (int rc = submit_impl(s, queries + (size_t)v * s->dim,
+                             q_indptr ? q_indices + q_indptr[v] : nullptr,
+                             q_indptr ? q_values + q_indptr[v] : nullptr, nnz,
+                             &tickets[(size_t)i]))
       return rc;
   }
   int64_t t_last = t0, t_first = -1;
   int32_t cnt = 0;
   for (int64_t i = 0; i < n_queries; ++i) {
-    if (int rc = armi_stream_wait(s, tickets[(size_t)i], nullptr, nullptr, nullptr, &cnt, 60e6))
+    if (int rc = armi_stream_wait(s, tickets[(size_t)i], nullptr, nullptr, nullptr, &cnt, nullptr,
+                                  60e6))
       return rc;
     const Entry& e = s->ring[tickets[(size_t)i] % kRing];
     latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;

@@ -173,47 +173,76 @@ class QueryBatcher:
 
 class StreamServer:
     """The native streaming server (libarmi armi_stream_*, include/armi.h) over one collection's
-    dense index: no Python thread in the request path. Callers submit single dense queries from
-    any thread (ctypes releases the GIL) and collect reference-shaped results; the batching,
-    the device work and the completion run in libarmi's own threads on the server's HIP stream.
-    Dense search only (the search_type="dense" path of qdrant.py:316-323, the configs[4] stream
-    workload); hybrid and filtered queries go through QueryBatcher."""
+    indexes: no Python thread in the request path. Callers submit single queries from any
+    thread (ctypes releases the GIL) and collect reference-shaped results; the batching, the
+    device work and the completion run in libarmi's own threads on the server's HIP stream.
+    search_type "dense" answers every query by the dense branch of QdrantRetriever.search
+    (qdrant.py:316-323); "hybrid" (a hybrid collection) answers a query that carries sparse
+    terms by the hybrid branch (qdrant.py:272-298: prefetch 2k + 2k, RRF, hit.score = the RRF
+    score) and one without by the dense branch, as search() chooses. Filters and the sparse-only
+    mode go through QueryBatcher."""
 
     def __init__(self, retriever: MI355XRetriever, collection_name: str | None = None,
-                 top_k: int | None = None, max_batch: int = 64, max_wait_ms: float = 2.0):
+                 top_k: int | None = None, max_batch: int = 64, max_wait_ms: float = 2.0,
+                 search_type: str = "dense"):
         from audio_rag_amd import _armi
 
+        if search_type not in ("dense", "hybrid"):
+            raise ValueError("StreamServer search_type must be 'dense' or 'hybrid'")
         self._armi = _armi
         self.retriever = retriever
         self.resolved = retriever._resolve_collection(collection_name)
         self.collection = retriever._collections[self.resolved]
         self.index = self.collection.dense_index  # kept alive for the server's lifetime
+        self.sparse_index = self.collection.sparse_index if search_type == "hybrid" else None
+        self.hybrid = self.sparse_index is not None
         self.k = top_k or retriever.config.top_k
         self.dim = retriever.embedding_dim
         self._handle = _armi.ctypes.c_void_p()
-        _armi.call("armi_stream_create", self.index.handle, self.k, max_batch,
-                   float(max_wait_ms) * 1e3, _armi.ctypes.byref(self._handle))
+        if self.hybrid:
+            _armi.call("armi_stream_create_hybrid", self.index.handle, self.sparse_index.handle,
+                       self.k, retriever.config.rrf_k, max_batch, float(max_wait_ms) * 1e3,
+                       _armi.ctypes.byref(self._handle))
+        else:
+            _armi.call("armi_stream_create", self.index.handle, self.k, max_batch,
+                       float(max_wait_ms) * 1e3, _armi.ctypes.byref(self._handle))
 
-    def submit_arrays(self, dense: np.ndarray) -> int:
+    def submit_arrays(self, dense: np.ndarray,
+                      sparse: tuple[np.ndarray, np.ndarray] | None = None) -> int:
+        """dense: [dim] query; sparse: (ascending indices, values) or None. Returns a ticket."""
         q = np.ascontiguousarray(dense, dtype=np.float16).reshape(-1)
         if q.size != self.dim:
             raise RetrievalError(f"query has {q.size} components, the store {self.dim}")
         ticket = self._armi.ctypes.c_int64()
-        self._armi.call("armi_stream_submit", self._handle, q.ctypes.data,
-                        self._armi.ctypes.byref(ticket))
+        if sparse is not None and self.hybrid and len(sparse[0]) > 0:
+            idx = np.ascontiguousarray(sparse[0], dtype=np.int32)
+            val = np.ascontiguousarray(sparse[1], dtype=np.float32)
+            if idx.size > 256:
+                raise RetrievalError("a sparse query may hold at most 256 terms")
+            self._armi.call("armi_stream_submit_hybrid", self._handle, q.ctypes.data,
+                            idx.ctypes.data, val.ctypes.data, idx.size,
+                            self._armi.ctypes.byref(ticket))
+        else:
+            self._armi.call("armi_stream_submit", self._handle, q.ctypes.data,
+                            self._armi.ctypes.byref(ticket))
         return ticket.value
 
     def submit(self, query: EmbeddingResult) -> int:
-        return self.submit_arrays(np.asarray(query.dense, dtype=np.float32))
+        return self.submit_arrays(np.asarray(query.dense, dtype=np.float32),
+                                  query_sparse_arrays(query.sparse))
 
     def raw_result(self, ticket: int, timeout: float = 60.0):
-        """(scores float32 [k], ids int64 [k], count) of a ticket."""
+        """(scores [k] (fp64 RRF scores on the hybrid branch, else float32 cosine), ids int64
+        [k], count) of a ticket."""
         scores = np.empty(self.k, dtype=np.float32)
+        rank = np.empty(self.k, dtype=np.float64)
         ids = np.empty(self.k, dtype=np.int64)
         count = self._armi.ctypes.c_int32()
+        mode = self._armi.ctypes.c_int32()
         self._armi.call("armi_stream_wait", self._handle, ticket, scores.ctypes.data,
-                        ids.ctypes.data, None, self._armi.ctypes.byref(count), timeout * 1e6)
-        return scores, ids, count.value
+                        ids.ctypes.data, rank.ctypes.data, self._armi.ctypes.byref(count),
+                        self._armi.ctypes.byref(mode), timeout * 1e6)
+        return (rank if mode.value == 1 else scores), ids, count.value
 
     def result(self, ticket: int, timeout: float = 60.0) -> list[RetrievalResult]:
         """The ticket's list[RetrievalResult] (as MI355XRetriever.search builds it)."""
@@ -238,15 +267,26 @@ class StreamServer:
                         self._armi.ctypes.byref(q))
         return b.value, q.value
 
-    def loadgen(self, queries: np.ndarray, n_queries: int, qps: float, seed: int = 0):
-        """Native open-loop Poisson load at `qps` (armi_stream_loadgen): per-query latency in
-        seconds and the elapsed time from the first submit to the last completion."""
+    def loadgen(self, queries: np.ndarray, n_queries: int, qps: float, seed: int = 0,
+                sparse_csr: tuple[np.ndarray, np.ndarray, np.ndarray] | None = None):
+        """Native open-loop Poisson load at `qps` (armi_stream_loadgen): query i = row
+        (i % len(queries)) with, on a hybrid server, the terms of CSR row (i % len(queries)).
+        Returns per-query latency in seconds and the elapsed time from the first submit to the
+        last completion."""
         q = np.ascontiguousarray(queries, dtype=np.float16).reshape(-1, self.dim)
         lat = np.empty(n_queries, dtype=np.float64)
         el = self._armi.ctypes.c_double()
         done = self._armi.ctypes.c_int64()
-        self._armi.call("armi_stream_loadgen", self._handle, q.ctypes.data, q.shape[0], n_queries,
-                        float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
+        ptrs = (None, None, None)
+        keep = None
+        if sparse_csr is not None and self.hybrid:
+            keep = tuple(np.ascontiguousarray(a, dtype=t)
+                         for a, t in zip(sparse_csr, (np.int32, np.int32, np.float32)))
+            if keep[0].size != q.shape[0] + 1:
+                raise ValueError("one CSR row per query vector is required")
+            ptrs = tuple(a.ctypes.data for a in keep)
+        self._armi.call("armi_stream_loadgen", self._handle, q.ctypes.data, *ptrs, q.shape[0],
+                        n_queries, float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
                         self._armi.ctypes.byref(done))
         return lat * 1e-6, el.value
 

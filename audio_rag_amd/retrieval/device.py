@@ -169,6 +169,10 @@ class SparseIndex:
         except Exception:
             pass
 
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._handle
+
     def workspace_bytes(self, n_queries: int, k: int) -> int:
         return int(query("armi_sparse_workspace_bytes", self._handle, n_queries, k))
 

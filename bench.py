@@ -249,6 +249,8 @@ def main() -> None:
     ap.add_argument("--ingest-chunks", type=int, default=20000, help="ingest: chunks embedded")
     ap.add_argument("--max-batch", type=int, default=64,
                     help="stream (native): largest batch the server coalesces")
+    ap.add_argument("--search-type", choices=["dense", "hybrid"], default="dense",
+                    help="stream: dense top-k, or hybrid (dense + sparse prefetch 2k, RRF)")
     ap.add_argument("--initial-k", type=int, default=20)
     ap.add_argument("--rerank-dtype", choices=["fp32", "bf16", "fp16"], default="fp16",
                     help="cross-encoder GEMM dtype (fp16: fp16 GEMMs + fused fp16 attention, "
@@ -751,20 +753,27 @@ def stream_main(args) -> None:
     from audio_rag_amd.retrieval.device import DenseIndex
     from audio_rag_amd.retrieval.mi355x import MI355XRetriever
 
+    from audio_rag_amd.retrieval.device import SparseIndex
+
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n, dim, k = args.chunks, args.dim, args.top_k
+    hybrid = args.search_type == "hybrid"
     rows = make_rows(0, n, dim, dev)
     payloads = [{"text": "", "start": 0.0, "end": 0.0, "speaker": None, "metadata": {}}] * n
-    ret = MI355XRetriever(RetrievalConfig(top_k=k, search_type="dense"), dim)
-    ret.attach_collection(ChunkCollection.from_indexes("audio_rag", DenseIndex(rows), payloads))
+    ret = MI355XRetriever(RetrievalConfig(top_k=k, search_type=args.search_type), dim)
+    sidx = SparseIndex(*make_sparse_rows(0, n, dev), vocab=VOCAB) if hybrid else None
+    ret.attach_collection(ChunkCollection.from_indexes("audio_rag", DenseIndex(rows), payloads,
+                                                       sidx))
     qs = make_queries(1, 4096, dim, dev, seed=1)[0].cpu().numpy()
+    q_csr = tuple(t.cpu().numpy() for t in make_sparse_queries(4096, dev, seed=1000)) if hybrid else None
     n_q = int(args.qps * args.duration)
     if args.stream_front == "native":
-        with StreamServer(ret, max_batch=args.max_batch, max_wait_ms=args.max_wait_ms) as srv:
-            srv.loadgen(qs, 4096, qps=args.qps, seed=6)  # warm-up
+        with StreamServer(ret, max_batch=args.max_batch, max_wait_ms=args.max_wait_ms,
+                          search_type=args.search_type) as srv:
+            srv.loadgen(qs, 4096, qps=args.qps, seed=6, sparse_csr=q_csr)  # warm-up
             b0, q0 = srv.stats()
-            lat, elapsed = srv.loadgen(qs, n_q, qps=args.qps, seed=7)
+            lat, elapsed = srv.loadgen(qs, n_q, qps=args.qps, seed=7, sparse_csr=q_csr)
             b1, q1 = srv.stats()
         batches, served = b1 - b0, q1 - q0
         value = n_q / elapsed
@@ -786,9 +795,11 @@ def stream_main(args) -> None:
                     done.append(t)
             return cb
 
+        sp = (lambda i: (q_csr[1][q_csr[0][i]:q_csr[0][i + 1]], q_csr[2][q_csr[0][i]:q_csr[0][i + 1]])
+              ) if hybrid else (lambda i: None)
         with QueryBatcher(ret, max_batch=64, max_wait_ms=args.max_wait_ms) as qb:
             for i in range(256):  # warm-up
-                qb.submit_arrays(qs[i % 4096]).result()
+                qb.submit_arrays(qs[i % 4096], sp(i % 4096)).result()
             gaps = rng.exponential(1.0 / args.qps, size=n_q)
             t0 = time.perf_counter()
             t_next = t0
@@ -798,7 +809,7 @@ def stream_main(args) -> None:
                 delay = t_next - time.perf_counter()
                 if delay > 0:
                     time.sleep(delay)  # releases the GIL to the batcher thread (never spin here)
-                f = qb.submit_arrays(qs[i % 4096])
+                f = qb.submit_arrays(qs[i % 4096], sp(i % 4096))
                 f.add_done_callback(on_done(time.perf_counter()))
                 futs.append(f)
             for f in futs:
@@ -822,13 +833,16 @@ def stream_main(args) -> None:
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic: N(0,1) rows and queries L2-normalised then cast to fp16, resident in HBM",
-        "config": {"workload": (f"streaming dense top-{k}: open-loop Poisson arrivals at "
+        "config": {"workload": (f"streaming {args.search_type} top-{k}"
+                                + (f" (prefetch {2 * k} + {2 * k}, RRF)" if hybrid else "")
+                                + ": open-loop Poisson arrivals at "
                                 f"{args.qps:.0f} q/s for {args.duration:.1f} s, {front}, batches "
                                 f"<= {args.max_batch} / <= {args.max_wait_ms} ms -> exact cosine "
                                 f"top-{k} over "
-                                f"{n} x {dim} fp16 chunks"),
+                                f"{n} x {dim} fp16 chunks"
+                                + (" + Zipf sparse vectors" if hybrid else "")),
                    "n_chunks": n, "dim": dim, "top_k": k, "offered_qps": args.qps,
-                   "front_end": args.stream_front,
+                   "front_end": args.stream_front, "search_type": args.search_type,
                    "parallelism": "single GPU, batching server"},
         "p50_ms": float(np.percentile(lat_ms, 50)),
         "p99_ms": float(np.percentile(lat_ms, 99)),

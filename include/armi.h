@@ -146,22 +146,37 @@ int armi_kernel_timing_read(int slot, double* total_ms, int64_t* launches);
  * those of armi_dense_topk for that query alone (exact ranking). Thread-safe; the index must
  * outlive the server. */
 typedef struct armi_stream armi_stream;
+typedef struct armi_sparse_index armi_sparse_index; /* declared again below */
 int armi_stream_create(const armi_index* index, int k, int max_batch, double max_wait_us,
                        armi_stream** out);
+/* Hybrid server: a query submitted with sparse terms is answered as QdrantRetriever.search's
+ * hybrid branch (qdrant.py:272-298: dense and sparse prefetch 2k, armi_rrf_fuse with rrf_k,
+ * limit k; scores are the RRF scores, in `rank` as fp64); one submitted without terms as its
+ * dense branch (dense top-k, cosine scores). k <= 120. Both indexes must outlive the server. */
+int armi_stream_create_hybrid(const armi_index* index, const armi_sparse_index* sparse, int k,
+                              int rrf_k, int max_batch, double max_wait_us, armi_stream** out);
 int armi_stream_destroy(armi_stream* server);
 /* query: host fp16 [dim], copied before return; *ticket identifies its result. */
 int armi_stream_submit(armi_stream* server, const uint16_t* query, int64_t* ticket);
+/* The same with the query's sparse terms (ascending indices, nnz <= 256; nnz = 0 = no sparse
+ * vector); needs a hybrid server when nnz > 0. */
+int armi_stream_submit_hybrid(armi_stream* server, const uint16_t* query,
+                              const int32_t* sp_indices, const float* sp_values, int nnz,
+                              int64_t* ticket);
 /* Blocks until the ticket's result is published (at most timeout_us), then copies its k
- * scores / ids / rank keys (each nullable) and the valid count. Results stay readable until
- * 2^20 later tickets have been submitted. */
+ * scores / ids / rank keys (each nullable), the valid count and the branch taken (mode:
+ * 0 dense, 1 hybrid; nullable). Results stay readable until 2^20 later tickets have been
+ * submitted. */
 int armi_stream_wait(armi_stream* server, int64_t ticket, float* scores, int64_t* ids,
-                     double* rank, int32_t* count, double timeout_us);
+                     double* rank, int32_t* count, int32_t* mode, double timeout_us);
 int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);
 /* Native open-loop load generator (bench.py --workload stream): n_queries arrivals as a
  * Poisson process at `qps` from one thread, query i = row (i % n_vectors) of `queries` (host
- * fp16 [n_vectors][dim]); latency_us[i] = completion - submit of query i; elapsed_s = last
+ * fp16 [n_vectors][dim]) with, when q_indptr is non-null, the sparse terms of CSR row
+ * (i % n_vectors); latency_us[i] = completion - submit of query i; elapsed_s = last
  * completion - first submit. n_queries <= 2^19. */
-int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, int64_t n_vectors,
+int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, const int32_t* q_indptr,
+                        const int32_t* q_indices, const float* q_values, int64_t n_vectors,
                         int64_t n_queries, double qps, uint64_t seed, double* latency_us,
                         double* elapsed_s, int64_t* completed);
 
@@ -227,7 +242,7 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
                    int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
 /* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)
- * hidden [n_seq][L][width] -> out [n_seq]. */
+ * hidden [n_seq][L][width] -> out [n_seq]; width <= 2048 (8 sequences per workgroup). */
 int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const float* dense_b,
                               const float* out_w, const float* out_b, float* out, int n_seq,
                               int L, int width, hipStream_t stream);

@@ -123,6 +123,39 @@ def test_stream_server_matches_oracle(gpu, oracle_mod, store):
         assert [r.score for r in got[i]] == [float(s) for s in want.scores[i, :want.count[i]]], i
 
 
+def test_stream_server_hybrid_matches_oracle(gpu, oracle_mod, store):
+    """Native server, hybrid: queries with sparse terms (i % 4 != 0) get the RRF fusion of the
+    dense and sparse 2k prefetches with fp64 RRF scores; queries without fall back to dense
+    top-k (QdrantRetriever.search strategy choice, qdrant.py:253-264). Concurrent callers, one
+    load-generator pass over the same CSR."""
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    _, _, (qi, qx, qv), qd = store
+    got = [None] * NQ
+    with StreamServer(ret, max_batch=16, max_wait_ms=3.0, search_type="hybrid") as srv:
+        def client(lo):
+            tickets = []
+            for i in range(lo, NQ, 3):
+                sp = (qx[qi[i]:qi[i + 1]], qv[qi[i]:qi[i + 1]]) if i % 4 else None
+                tickets.append((i, srv.submit_arrays(qd[i].view(np.float16), sp)))
+            for i, t in tickets:
+                got[i] = srv.result(t)
+        ts = [threading.Thread(target=client, args=(c,)) for c in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        batches, served = srv.stats()
+        assert served == NQ and batches < NQ, (batches, served)
+        lat, elapsed = srv.loadgen(qd.view(np.float16), 1000, qps=20000.0, seed=4,
+                                   sparse_csr=(qi, qx, qv))
+        assert lat.shape == (1000,) and (lat > 0).all() and elapsed > 0
+    for i in range(NQ):
+        want = _expected(oracle_mod, store, i, "hybrid", None)
+        assert [(r.chunk.text, r.score) for r in got[i]] == want, i
+
+
 def test_stream_server_loadgen_and_filtered_edge(gpu, oracle_mod, store):
     """The native load generator completes every arrival with positive latencies; a server over
     a tiny store returns fewer than k results where the store has fewer rows."""
