@@ -54,6 +54,9 @@ constexpr int kMaxPool = 4096;  // pooled candidates per query in the merge kern
 // delta = kDeltaSafety * dim * 2^-24 * |q|: the fp32 accumulation error bound gamma_dim * |q|
 // (|sum| <= sum |q_i x_i| <= |q||x|) with a 4x allowance for the MFMA's internal ordering.
 constexpr double kDeltaSafety = 4.0;
+// The four-wave scan's approximate scores carry a row code in their 6 low mantissa bits: up to
+// 2^-18 |score| more (scores are at most |q| (1 + 2^-10) in the certificate's units); 2^-17 |q|.
+constexpr double kEncodeSlack = 1.0 / 131072.0;
 
 template <int M>
 __device__ __forceinline__ void topm_insert(float x, int32_t id, float (&s)[M], int32_t (&ix)[M],
@@ -1308,6 +1311,359 @@ __global__ __launch_bounds__(kGThreads) void dense_gemm_scan_p8_kernel(
   }
 }
 
+// Four-wave tiled scan: one wave per SIMD, each wave owning a 128-row x 128-query block of the
+// 256 x 256 tile (16 v_mfma_f32_32x32x16_f16 accumulators = 256 AccVGPRs), so a k-step carries
+// twice the MFMA work per wave of the eight-wave kernels and half their fragment reads per MFMA
+// (4 + 4 ds_read_b128 per 16 MFMAs). Same candidate output as dense_gemm_scan_glds_kernel.
+//   * LDS ring of four 32-wide k-step stages (512 image rows x 64 B = 32 KB each: 256 corpus
+//     rows, then the 256-query block; chunk c of image row ir at slot c ^ ((ir >> 2) & 3)) plus
+//     two 1-KB inverse-norm copies (tile parity), issued by wave 0 with the tile's first stage;
+//   * per k-step s: [first half] the 16 MFMAs of sub-step 0 with pieces 0-3 of stage s+3 and the
+//     sub-step 1 fragment reads of stage s between them -> vmcnt(12) retires stage s+1 ->
+//     s_barrier -> [second half] the 16 MFMAs of sub-step 1 with pieces 4-7 of stage s+3 and the
+//     sub-step 0 fragment reads of stage s+1 between them; the tile epilogue after the last k-step;
+//   * a wave's 8 pieces per stage are 1-KB LDS-DMA instructions whose per-lane source offsets
+//     are fixed (the swizzle of a piece depends on the lane only), so an issue is one
+//     instruction over a scalar base.
+constexpr int kW4Threads = 256;
+constexpr int kW4Img = (kG2Rows + kGQB) * 64;  // one 32-wide k-step stage
+constexpr int kW4Norm = 4 * kW4Img;            // the two inverse-norm copies follow the ring
+
+template <int DIM>
+constexpr size_t gemm_w4_lds_bytes() {
+  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
+  constexpr size_t ring = (size_t)kW4Norm + 2048;
+  return ring > lists ? ring : lists;
+}
+
+// ABL (probe build only, results wrong): 1 no LDS-DMA pieces in the k-loop, 2 no tile
+// epilogue, 4 no MFMAs, 8 no mid-step barrier.
+template <int DIM, int ABL>
+__global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void dense_gemm_scan_w4_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
+    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
+  constexpr int KT = DIM / 32;  // k-steps per row tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int id = blockIdx.x;
+  int qb, rp;
+  if (n_qb == 2) {
+    qb = (id >> 3) & 1;
+    rp = (id >> 4) * 8 + (id & 7);
+  } else {
+    qb = id % n_qb;
+    rp = id / n_qb;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int64_t lo = (int64_t)rp * rows_per_range;
+  const int64_t hi = min(lo + rows_per_range, n_rows);
+  const int q_base = qb * kGQB;
+  const int n_here = (int)(hi - lo);
+  const int last_row = (int)(n_rows - 1 - lo);                   // clamp target (row offset)
+  const int last4 = (int)(((n_rows + 31) / 32) * 32 - 4 - lo);  // last 16-B group of the norms
+  const unsigned char* __restrict__ rsrc = reinterpret_cast<const unsigned char*>(rows + lo * DIM);
+  const unsigned char* __restrict__ qsrc =
+      reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
+  const float* __restrict__ inv_r = inv_norm32 + lo;
+
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int wr = wave >> 1;  // row group: rows wr*128 + m*32 + ...
+  const int wq = wave & 1;   // query group: queries wq*128 + n*32 + r
+
+  float sl[4][kLaneList];
+  int32_t il[4][kLaneList];
+  float dl[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    dl[n] = kNegInf;
+#pragma unroll
+    for (int j = 0; j < kLaneList; ++j) { sl[n][j] = kNegInf; il[n][j] = -1; }
+  }
+
+  const int n_tiles = (n_here + kG2Rows - 1) / kG2Rows;
+  // piece p of a stage, this wave: image rows p*64 + prow (p < 4: corpus rows of the tile,
+  // p >= 4: queries (p-4)*64 + prow of the block); lane slot lane % 4 holds chunk c. Corpus rows
+  // are clamped to the store (the last tile of a range, and the tail stages nobody reads); the
+  // byte offsets are 32-bit (the host keeps a range below 4 GiB) over a scalar base.
+  const int prow = wave * 16 + (lane >> 2);
+  const int c = (lane & 3) ^ ((lane >> 4) & 3);
+  const uint32_t c16 = (uint32_t)(c * 16);
+  uint32_t b_off[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int q = min(q_base + p * 64 + prow, nq - 1);
+    b_off[p] = (uint32_t)((q - q_base) * DIM * 2) + c16;
+  }
+  auto issue_piece = [&](int st, int p) {
+    const int tn = st / KT;
+    const int t = st - tn * KT;
+    lds_ptr_t dst = (lds_ptr_t)(smem + (st & 3) * kW4Img + (p * 4 + wave) * 1024);
+    if (p < 4) {
+      const uint32_t row = (uint32_t)min(tn * kG2Rows + p * 64 + prow, last_row);
+      __builtin_amdgcn_global_load_lds(rsrc + t * 64 + (row * (uint32_t)(DIM * 2) + c16), dst, 16,
+                                       0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds(qsrc + t * 64 + b_off[p - 4], dst, 16, 0, 0);
+    }
+  };
+  // inverse norms of row tile tn -> LDS [kW4Norm + (tn & 1) KB] (wave 0, 4 rows per lane;
+  // clamped to the padded norm array, rows past the range are masked anyway)
+  auto issue_norms = [&](int tn) {
+    if (wave == 0) {
+      const int rr = min(tn * kG2Rows + 4 * lane, last4);
+      __builtin_amdgcn_global_load_lds(inv_r + rr, (lds_ptr_t)(smem + kW4Norm + (tn & 1) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  const int swz = (r >> 2) & 3;
+  const uint32_t a_lane = lds0 + (uint32_t)(wr * 128 + r) * 64;
+  const uint32_t b_lane = lds0 + (uint32_t)(kG2Rows + wq * 128 + r) * 64;
+  const uint32_t co0 = (uint32_t)(((0 + h) ^ swz) << 4);
+  const uint32_t co1 = (uint32_t)(((2 + h) ^ swz) << 4);
+  u32x4 fa[2][4], fb[2][4];  // [sub-step][row block m / query block n]
+  // fragment item i of sub-step `sub` of stage st: i < 4 row block i, else query block i - 4
+  auto read_item = [&](int st, int sub, int i) {
+    const uint32_t stage = (uint32_t)((st & 3) * kW4Img) + (sub ? co1 : co0);
+    if (i < 4) {
+      const uint32_t addr = a_lane + stage;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[sub][i]) : "v"(addr), "i"(i * 2048));
+    } else {
+      const uint32_t addr = b_lane + stage;
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(fb[sub][i - 4]) : "v"(addr), "i"((i - 4) * 2048));
+    }
+  };
+  // the fragment reads of a sub-step have landed (ties the registers to the wait)
+  auto frags_ready = [&](int sub) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[sub][0]), "+v"(fa[sub][1]), "+v"(fa[sub][2]), "+v"(fa[sub][3]),
+                   "+v"(fb[sub][0]), "+v"(fb[sub][1]), "+v"(fb[sub][2]), "+v"(fb[sub][3])
+                 :: "memory");
+  };
+
+  {
+    // an AGPR operand anywhere in the kernel makes hipcc select the AGPR form of the MFMAs
+    // (accumulators in AccVGPRs); the ArchVGPR form would need all 512 registers for them
+    int zero = 0;
+    asm volatile("; agpr-form hint %0" ::"a"(zero));
+  }
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
+
+  // Tile epilogue without compares (one wave per SIMD: nothing overlaps it, so no wave-divergent
+  // insertion per score and no lane masks): each score carries its row code m*16 + j in its 6 low
+  // mantissa bits (a perturbation below 2^-18 |score|, covered by the certificate's kEncodeSlack),
+  // so per lane and query block a max/min chain keeps the tile's best two scores WITH their rows
+  // and the largest score below them ("third"): 7 VALU per score. Rows outside the range or
+  // dropped by the filter (and rows the index marks invalid: NaN inverse norm) score -FLT_MAX
+  // instead. The two best join the lane list, third the discarded bound; a row leaves the
+  // candidates only at or below its lane-tile's third or by eviction from the list, both covered by
+  // the bound, so dense_merge_kernel's certificate holds (it fails only where one lane-tile of 64
+  // rows holds three of the top k).
+  auto epilogue = [&](int tile) {
+    float b1[4], b2[4], b3[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) { b1[n] = kNegInf; b2[n] = kNegInf; b3[n] = kNegInf; }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      __builtin_amdgcn_sched_barrier(0);
+      const int ro = tile * kG2Rows + wr * 128 + m * 32;  // row offset of the 32-row block
+      const int64_t rb = lo + ro;
+      uint32_t linv = lds0 + (uint32_t)(kW4Norm + (tile & 1) * 1024 +
+                                        (wr * 128 + m * 32 + 4 * h) * 4);
+      // block m's norms are read after block m-1's scores are folded (else hipcc hoists the
+      // four blocks' norms and masks together)
+      asm volatile("" : "+v"(linv) : "v"(b3[0]), "v"(b3[1]), "v"(b3[2]), "v"(b3[3]));
+      u32x4 invw[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
+      uint32_t valid = ro + 32 <= n_here ? 0xffffffffu
+                                         : (ro >= n_here ? 0u : (1u << (n_here - ro)) - 1u);
+      if (row_mask && valid) valid &= (uint32_t)(row_mask[rb >> 6] >> (rb & 63));
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(invw[0]), "+v"(invw[1]), "+v"(invw[2]), "+v"(invw[3]) :: "memory");
+      // score = fma(acc, inv, bias): (inv, 0) for a live row, (0, -FLT_MAX) otherwise
+      float inv[16], bias[16];
+      const uint32_t vb = valid >> (4 * h);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t w4v[4] = {invw[g].x, invw[g].y, invw[g].z, invw[g].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * g + e;
+          const float iv = __uint_as_float(w4v[e]);
+          const bool live = ((vb >> ((j & 3) + 8 * (j >> 2))) & 1u) && iv == iv;
+          inv[j] = live ? iv : 0.0f;
+          bias[j] = live ? 0.0f : -3.4028234663852886e38f;
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        __builtin_amdgcn_sched_barrier(0);
+        // read here from AccVGPRs (else hipcc copies all 256 accumulators out at the loop exit),
+        // after the previous block is folded (else the four blocks of m are read out together)
+        asm volatile("" : "+a"(acc[m][n]) : "v"(b3[(n + 3) & 3]));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
+          // code m*16 + j (an inline constant) in the low 6 mantissa bits
+          const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
+          const float t = fminf(b1[n], e);
+          b1[n] = fmaxf(b1[n], e);
+          const float t2 = fminf(b2[n], t);
+          b2[n] = fmaxf(b2[n], t);
+          b3[n] = fmaxf(b3[n], t2);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int32_t rbase = (int32_t)(lo + tile * kG2Rows + wr * 128) + 4 * h;
+    // code m*16 + j -> row rbase + m*32 + (j & 3) + 8 (j >> 2); -FLT_MAX scores (no live row)
+    // stay out of the lists and the bound
+    constexpr float kDead = -1.0e38f;
+    auto row_of = [&](float b) {
+      const int32_t code = (int32_t)(__float_as_uint(b) & 63u);
+      return rbase + ((code >> 4) << 5) + (code & 3) + ((code & 12) << 1);
+    };
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      if (b1[n] > kDead) topm_insert<kLaneList>(b1[n], row_of(b1[n]), sl[n], il[n], dl[n]);
+      if (b2[n] > kDead) topm_insert<kLaneList>(b2[n], row_of(b2[n]), sl[n], il[n], dl[n]);
+      if (b3[n] > kDead) dl[n] = fmaxf(dl[n], b3[n]);
+    }
+  };
+
+  const int n_steps = n_tiles * KT;
+  if (n_steps > 0) {
+    // prologue: stages 0-2 whole; stage 0 retired (the 16 younger pieces stay in flight)
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+      if (st % KT == 0) issue_norms(st / KT);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) issue_piece(st, p);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) read_item(0, 0, i);
+    frags_ready(0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int tile = 0; tile < n_tiles; ++tile) {
+      // fresh accumulators per tile (a loop-invariant zero: no conditional reset in the k-loop,
+      // so the 256 accumulators stay put in AccVGPRs)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
+      for (int kt = 0; kt < KT; ++kt) {
+        const int s = tile * KT + kt;
+        // Stages past the last k-step are issued too (rows clamped into the store, never read),
+        // so every wait keeps the same count and the loop carries no issue branches.
+        const int s3 = s + 3;
+        if (s3 % KT == 0) issue_norms(s3 / KT);
+        // ---- first half: sub-step 0 MFMAs; sub-step 1 reads of stage s (between the first 8
+        // MFMAs, so their latency hides behind the last 8); pieces 0-3 of stage s+3
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if constexpr (!(ABL & 4))
+            acc[i >> 2][i & 3] = mfma16(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
+          if (i < 8) read_item(s, 1, i);
+          if (!(ABL & 1) && i >= 8 && (i & 1)) issue_piece(s3, (i - 8) >> 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        frags_ready(1);
+        // retire stage s+1 (younger: stage s+2 whole, the first half of s+3)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // ---- second half: sub-step 1 MFMAs; sub-step 0 reads of stage s+1; pieces 4-7 of s+3
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if constexpr (!(ABL & 4))
+            acc[i >> 2][i & 3] = mfma16(fa[1][i >> 2], fb[1][i & 3], acc[i >> 2][i & 3]);
+          if (i < 8) read_item(s + 1, 0, i);
+          if (!(ABL & 1) && i >= 8 && (i & 1)) issue_piece(s3, 4 + ((i - 8) >> 1));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        frags_ready(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) asm volatile("" : "+a"(acc[m][n]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (!(ABL & 2)) epilogue(tile);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // workgroup lists (the layout of dense_gemm_scan_glds_kernel); the tail stages' DMA must land
+  // before the ring is reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
+  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);      // [256][4]
+  {
+    const int slot = (wr * 2 + h) * kLaneList;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int q = wq * 128 + n * 32 + r;
+#pragma unroll
+      for (int j = 0; j < kLaneList; ++j) {
+        lkey[q * 16 + slot + j] = sl[n][j];
+        lrow[q * 16 + slot + j] = il[n][j];
+      }
+      ldisc[q * 4 + wr * 2 + h] = dl[n];
+    }
+  }
+  __syncthreads();
+  for (int round = 0; round < kGQB / 16; ++round) {  // 4 waves x 4 queries per round
+    const int ql = (round * 4 + wave) * 4 + (lane >> 4);
+    float key = lkey[ql * 16 + (lane & 15)];
+    int32_t row = lrow[ql * 16 + (lane & 15)];
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const float ok = __shfl_xor(key, stride);
+        const int32_t orow = __shfl_xor(row, stride);
+        const bool lower = (lane & stride) == 0;
+        const bool desc = (lane & size) == 0;
+        const bool other_better = armi::approx_better(ok, orow, key, row);
+        const bool take_other = (lower == desc) ? other_better : !other_better;
+        if (take_other) { key = ok; row = orow; }
+      }
+    }
+    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
+    const int qg = q_base + ql;
+    if (qg < nq) {
+      const size_t base = (size_t)rp * nq + qg;
+      cand_key[base * kKW + rank] = key;
+      cand_row[base * kKW + rank] = row;
+      if (rank == 0) {
+        const float* dd = ldisc + ql * 4;
+        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
+      }
+    }
+  }
+}
+
 // This lane's DIM/64 contiguous fp16 elements of a vector, as raw 8-byte words.
 template <int DIM>
 __device__ __forceinline__ void load_raw(const uint16_t* __restrict__ v, int lane,
@@ -1575,7 +1931,8 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   int n_out;
   if (n_valid >= k) {
     const double kth = rkey[k - 1] * (1.0 / 16777216.0);
-    const double delta = kDeltaSafety * (double)DIM * (1.0 / 16777216.0) * qnorm_real;
+    const double delta =
+        (kDeltaSafety * (double)DIM * (1.0 / 16777216.0) + kEncodeSlack) * qnorm_real;
     certified = kth > (double)bound + delta;
     n_out = k;
   } else {
@@ -1840,15 +2197,19 @@ int gemm_ablate() {
 #endif
 }
 
-// Schedule of the tiled scan: the four-stage kernel (default) or the phase-pipelined one
-// (ARMI_GEMM_FORM=p8, A/B measurements; measured 2.00 vs 1.67-1.73 ms at the 10M / 8-way
-// per-rank shape, profiles/r02_p8_scan_ab.txt).
-bool use_p8_form() {
-  static const bool p8 = [] {
+// Schedule of the LDS-DMA tiled scan: the four-wave kernel (default), the eight-wave four-stage
+// kernel (ARMI_GEMM_FORM=glds) or the phase-pipelined one (ARMI_GEMM_FORM=p8). Measured at the
+// 10M / 8-way per-rank shape: w4 1.49 ms, glds 1.67-1.78 ms, p8 2.00 ms; at 1M rows G = 4 / 8:
+// w4 196 / 171-186 us, glds 243 / 243 us (profiles/r02_w4_scan_ab.txt, r02_p8_scan_ab.txt).
+enum class GemmForm { W4, GLDS, P8 };
+GemmForm gemm_form() {
+  static const GemmForm f = [] {
     const char* e = getenv("ARMI_GEMM_FORM");
-    return e && e[0] == 'p';
+    if (e && e[0] == 'g') return GemmForm::GLDS;
+    if (e && e[0] == 'p') return GemmForm::P8;
+    return GemmForm::W4;
   }();
-  return p8;
+  return f;
 }
 
 struct GemmPlan {
@@ -1977,7 +2338,27 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     }
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    if (glds && use_p8_form()) {
+    // the four-wave kernel addresses a range's rows with 32-bit byte offsets
+    const bool w4_fits = (gp.rows_per_range + kG2Rows) * (int64_t)DIM * 2 < (int64_t(1) << 32);
+    if (glds && gemm_form() == GemmForm::W4 && w4_fits) {
+      auto kern = dense_gemm_scan_w4_kernel<DIM, 0>;
+#ifdef ARMI_PROBE_BUILD
+      switch (gemm_ablate()) {
+        case 1: kern = dense_gemm_scan_w4_kernel<DIM, 1>; break;
+        case 2: kern = dense_gemm_scan_w4_kernel<DIM, 2>; break;
+        case 3: kern = dense_gemm_scan_w4_kernel<DIM, 3>; break;
+        case 4: kern = dense_gemm_scan_w4_kernel<DIM, 4>; break;
+        case 8: kern = dense_gemm_scan_w4_kernel<DIM, 8>; break;
+        case 9: kern = dense_gemm_scan_w4_kernel<DIM, 9>; break;
+        default: break;
+      }
+#endif
+      if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
+      kern<<<dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(), stream>>>(
+          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
+          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
+      ARMI_LAUNCHED("dense_gemm_scan_w4_kernel");
+    } else if (glds && gemm_form() == GemmForm::P8) {
       auto kern = dense_gemm_scan_p8_kernel<DIM, 0>;
 #ifdef ARMI_PROBE_BUILD
       switch (gemm_ablate()) {
