@@ -19,6 +19,7 @@ ARMI_OK = 0
 ARMI_FLAG_CERTIFIED = 1
 ARMI_FLAG_FALLBACK = 2
 TIMING_DENSE_SCAN, TIMING_SPARSE_SCAN, TIMING_ENCODER_GEMM = 0, 1, 2
+SCAN_FP16, SCAN_INT8_FILTER, SCAN_TILED_FP16 = 0, 1, 2  # armi_dense_scan_form
 ABI_VERSION = 1
 
 c_void_p = ctypes.c_void_p
@@ -33,6 +34,7 @@ SIGNATURES: dict[str, tuple] = {
     "armi_last_error": (ctypes.c_char_p, []),
     "armi_abi_version": (c_int, []),
     "armi_index_create": (c_int, [c_int, c_void_p, c_int64, c_int, c_int64, ctypes.POINTER(c_void_p), c_void_p]),
+    "armi_dense_scan_form": (c_int, [c_void_p, c_int, c_int]),
     "armi_index_destroy": (c_int, [c_void_p]),
     "armi_index_rows": (c_int64, [c_void_p]),
     "armi_index_dim": (c_int, [c_void_p]),

@@ -17,6 +17,11 @@ struct armi_index {
   double* inv_norm = nullptr;    // [n_tiles*32] 1/sqrt(norm2)
   float* inv_norm32 = nullptr;   // [n_tiles*32] inv_norm * 2^24 as fp32 (NaN = invalid / padding)
   unsigned long long* invalid = nullptr;  // [1] count of rows outside the fp16 domain
+  // int8 filter image of the rows (the first pass of the 64-query scan reads these 1-byte
+  // components instead of the 2-byte fp16 ones): row r ~= s_r * rows8[r], s_r = max_i |x_ri| / 127
+  int8_t* rows8 = nullptr;       // [n_tiles*32][dim] round(x / s_r) (0 for invalid / padding)
+  float* a32 = nullptr;          // [n_tiles*32] s_r / |x_r| (score scale; NaN = invalid / padding)
+  float* e32 = nullptr;          // [n_tiles*32] >= ||x_r - s_r rows8[r]||_2 / |x_r| (per unit |q|)
 };
 
 // Sparse store: a device inverted index built at create time from the caller's CSR (which may

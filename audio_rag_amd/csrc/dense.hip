@@ -309,6 +309,264 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+
+// 4 int8 components (one dword) -> 4 fp16 fragments components (two dwords), exactly: the
+// biased byte u = b + 128 becomes the fp16 1024 + u (bits 0x64uu), minus 1152 = b.
+__device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& hi) {
+  const uint32_t u = d ^ 0x80808080u;
+  const half2v bias = {(_Float16)1152.0f, (_Float16)1152.0f};
+  const half2v l = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(0x64646464u, u, 0x04010400u));
+  const half2v h = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(0x64646464u, u, 0x04030402u));
+  lo = __builtin_bit_cast(uint32_t, l - bias);
+  hi = __builtin_bit_cast(uint32_t, h - bias);
+}
+
+// Int8-filter form of dense_scan_kernel: the default 64-query scan (round 2). Each row's first
+// pass reads its 1-byte int8 image (rows8, one 1 KB row at dim 1024) instead of its 2-byte fp16
+// components: half the HBM bytes of the HBM-bound pass. Lane half h loads 16-B chunks 8g+4h+i of
+// its row (16 int8 each), converts them exactly to fp16 (i8x4_to_f16) and runs the same
+// v_mfma_f32_32x32x16_f16 against the fp16 query image (k-step s, half h = query components
+// 128(s>>3) + 64h + 8(s&7) .. +7, the corpus chunk's order). The lane-list key is an UPPER
+// BOUND of the fp16 row's cosine: acc * a32[row] + e32[row] * |q| (a32 = s/|x|; e32 bounds the
+// quantisation term |q.(x - s x8)|/|x| by Cauchy-Schwarz; |q| rounded up), so the rows
+// dense_merge_kernel discards still satisfy exact <= bound + delta (delta: the fp32 accumulation
+// term, unchanged) and its certificate holds as for the fp16 scan; it rescoring more of the pool
+// (kc_i8) absorbs the looser keys.
+template <int DIM>
+__global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
+    const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
+    int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
+    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
+    int guard) {
+  constexpr int KSTEPS = DIM / 16;
+  constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
+  constexpr int DEPTH = GROUPS % 4 == 0 ? 4 : 2;  // groups in flight per lane
+  int qb = 0, rp = blockIdx.x;
+  if (n_qb > 1) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    qb = j % n_qb;
+    rp = (j / n_qb) * 8 + xcd;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
+  const int q0 = qb * kQB;
+  const int nq = min(kQB, q_stride - q0);
+  const uint16_t* __restrict__ queries = queries_all + (size_t)q0 * DIM;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
+  float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB]
+
+  const int wave = armi::wave_id();
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
+  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
+  int64_t t = t_begin + wave;
+  auto row_ptr = [&](int64_t tile) -> const u32x4* {
+    int64_t rr = tile * TILE_ROWS + r;
+    rr = rr < n_rows ? rr : n_rows - 1;
+    return reinterpret_cast<const u32x4*>(rows8 + rr * DIM) + 4 * h;
+  };
+  const u32x4* cur = row_ptr(t < t_end ? t : t_begin);
+  u32x4 buf[DEPTH][4];
+  if (t < t_end) {
+#pragma unroll
+    for (int g = 0; g < DEPTH; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 8 * g + i);
+  }
+
+  // 1. Query fragment image (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) and
+  //    the query norms, rounded up (fp32 sum of 1024 squares: relative error < 2^-13).
+  for (int e = threadIdx.x; e < KSTEPS * 2 * kQB; e += kThreads) {
+    const int q = e & (kQB - 1);
+    const int sh = e >> 6;
+    const int hh = sh & 1;
+    const int s = sh >> 1;
+    const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off);
+    qimg[e] = v;
+  }
+  for (int q = wave; q < kQB; q += kWaves) {
+    float ss = 0.0f;
+    if (q < nq) {
+#pragma unroll
+      for (int i = 0; i < DIM / 64; ++i) {
+        const float v = (float)__builtin_bit_cast(_Float16, queries[(size_t)q * DIM + lane + 64 * i]);
+        ss += v * v;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    if (lane == 0) qnorm[q] = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
+  }
+  __syncthreads();
+  const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
+
+  float s0[kLaneList], s1[kLaneList];
+  int32_t i0[kLaneList], i1[kLaneList];
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
+  }
+  float d0 = kNegInf, d1 = kNegInf;
+
+  if (t < t_end) {
+    for (; t < t_end; t += kWaves) {
+      const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
+      const u32x4* nxt = row_ptr(tn);
+      int qoff = h * kQB + r;
+      asm volatile("" : "+v"(qoff));
+      const u32x4* qv = qimg + qoff;
+      f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+      for (int g = 0; g < GROUPS; ++g) {
+        u32x4 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = buf[g % DEPTH][i];
+        if (g + DEPTH < GROUPS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) buf[g % DEPTH][i] = stream_load(cur + 8 * (g + DEPTH) + i);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            buf[g % DEPTH][i] = stream_load(nxt + 8 * (g + DEPTH - GROUPS) + i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t c[8];  // fp16 pairs of components 0-7 (c[0..3]) and 8-15 (c[4..7])
+          i8x4_to_f16(a[i].x, c[0], c[1]);
+          i8x4_to_f16(a[i].y, c[2], c[3]);
+          i8x4_to_f16(a[i].z, c[4], c[5]);
+          i8x4_to_f16(a[i].w, c[6], c[7]);
+#if defined(ARMI_PROBE_BUILD) && ARMI_I8_ABL == 1  // timing only: no conversion
+          const u32x4 f0 = a[i], f1 = a[i];
+          (void)c;
+#else
+          const u32x4 f0 = {c[0], c[1], c[2], c[3]}, f1 = {c[4], c[5], c[6], c[7]};
+#endif
+          const int s = 8 * g + 2 * i;
+#if defined(ARMI_PROBE_BUILD) && ARMI_I8_ABL == 2  // timing only: no MFMAs
+          asm volatile("" :: "v"(f0), "v"(f1), "v"(qv[s * 2 * kQB]), "v"(qv[(s + 1) * 2 * kQB + 32]));
+#else
+          acc0 = mfma16(f0, qv[s * 2 * kQB], acc0);
+          acc1 = mfma16(f0, qv[s * 2 * kQB + 32], acc1);
+          acc0 = mfma16(f1, qv[(s + 1) * 2 * kQB], acc0);
+          acc1 = mfma16(f1, qv[(s + 1) * 2 * kQB + 32], acc1);
+#endif
+        }
+      }
+      cur = nxt;
+
+      // Epilogue: lane holds rows (j&3) + 8*(j>>2) + 4*h of the tile, queries r and 32 + r.
+      const int64_t row0 = t * TILE_ROWS;
+      float sc[16], ec[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(a32 + row0 + 8 * q + 4 * h);
+        sc[4 * q + 0] = v.x; sc[4 * q + 1] = v.y; sc[4 * q + 2] = v.z; sc[4 * q + 3] = v.w;
+        const float4 w = *reinterpret_cast<const float4*>(e32 + row0 + 8 * q + 4 * h);
+        ec[4 * q + 0] = w.x; ec[4 * q + 1] = w.y; ec[4 * q + 2] = w.z; ec[4 * q + 3] = w.w;
+      }
+      // invalid and filtered rows: NaN scale (never a lane-list entry, ignored by the bound)
+      if (row_mask) {
+        const uint32_t mbits = (uint32_t)(row_mask[row0 >> 6] >> (row0 & 63));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (!((mbits >> ((j & 3) + 8 * (j >> 2) + 4 * h)) & 1u)) sc[j] = __builtin_nanf("");
+      }
+      float x0[16], x1[16];
+      float mx0 = kNegInf, mx1 = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        x0[j] = __builtin_fmaf(acc0[j], sc[j], ec[j] * qn0);
+        x1[j] = __builtin_fmaf(acc1[j], sc[j], ec[j] * qn1);
+        mx0 = fmaxf(mx0, x0[j]);
+        mx1 = fmaxf(mx1, x1[j]);
+      }
+      const int32_t rbase = (int32_t)row0 + 4 * h;
+      if (__any(mx0 > s0[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(x0[j] > s0[kLaneList - 1])) {
+            d0 = fmaxf(d0, x0[j]);
+            continue;
+          }
+          topm_insert<kLaneList>(x0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+        }
+      } else {
+        d0 = fmaxf(d0, mx0);
+      }
+      if (__any(mx1 > s1[kLaneList - 1])) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (guard && !__any(x1[j] > s1[kLaneList - 1])) {
+            d1 = fmaxf(d1, x1[j]);
+            continue;
+          }
+          topm_insert<kLaneList>(x1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+        }
+      } else {
+        d1 = fmaxf(d1, mx1);
+      }
+    }
+  }
+
+  // 2. Workgroup merge (as dense_scan_kernel; the query image is dead: overlay it).
+  __syncthreads();
+  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][64]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * 64 * 4);        // [kQB][64]
+  float* ldisc = reinterpret_cast<float*>(smem + kQB * 64 * 8);           // [kQB][16]
+  const int slot = wave * 2 + h;
+#pragma unroll
+  for (int j = 0; j < kLaneList; ++j) {
+    lkey[r * 64 + slot * kLaneList + j] = s0[j];
+    lrow[r * 64 + slot * kLaneList + j] = i0[j];
+    lkey[(32 + r) * 64 + slot * kLaneList + j] = s1[j];
+    lrow[(32 + r) * 64 + slot * kLaneList + j] = i1[j];
+  }
+  ldisc[r * 16 + slot] = d0;
+  ldisc[(32 + r) * 16 + slot] = d1;
+  __syncthreads();
+  constexpr int QW = kQB / kWaves;
+  float key[QW], b[QW];
+  int32_t row[QW];
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq) {
+    const int q = wave * QW + qq;
+    key[qq] = lkey[q * 64 + lane];
+    row[qq] = lrow[q * 64 + lane];
+    b[qq] = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
+  }
+  armi::wave_sort_approx_desc_n<QW>(key, row);
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq)
+    if (lane == kKW) b[qq] = fmaxf(b[qq], key[qq]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int qq = 0; qq < QW; ++qq) b[qq] = fmaxf(b[qq], __shfl_xor(b[qq], off));
+#pragma unroll
+  for (int qq = 0; qq < QW; ++qq) {
+    const int q = wave * QW + qq;
+    if (q >= nq) break;
+    const size_t base = (size_t)rp * q_stride + q0 + q;
+    if (lane < kKW) {
+      cand_key[base * kKW + lane] = key[qq];
+      cand_row[base * kKW + lane] = row[qq];
+    }
+    if (lane == 0) cand_bound[base] = b[qq];
+  }
+}
+
+template <int DIM>
+constexpr int scan_i8_lds_bytes() {
+  return scan_lds_bytes<DIM>() + kQB * 4;
+}
 
 // Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
 // step: G * 64 queries over a 1/G shard). A GEMM-tiled form of dense_scan_kernel: both operands
@@ -2212,6 +2470,21 @@ GemmForm gemm_form() {
   return f;
 }
 
+// The 64-query scan reads the int8 filter image (dense_scan_i8_kernel) for k <= 16, with the
+// merge rescoring the kc_i8 best upper bounds; ARMI_DENSE_FILTER=fp16 forces the fp16 scan (A/B).
+// Beyond k = 16 the looser keys would need rescoring pools past the merge's 256 rows.
+constexpr int kI8MaxK = 16;
+bool use_i8_filter(const armi_index* idx, int k) {
+  static const bool off = [] {
+    const char* e = getenv("ARMI_DENSE_FILTER");
+    return e && e[0] == 'f';
+  }();
+  return !off && idx->rows8 != nullptr && k <= kI8MaxK;
+}
+// Rows rescored per query after the int8 pass: the rows whose key (an upper bound) reaches the
+// k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008).
+int kc_i8(int k) { return k <= 6 ? 64 : 128; }
+
 struct GemmPlan {
   int n_qb = 0;
   int n_ranges = 0;
@@ -2317,6 +2590,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                     const Workspace& w, hipStream_t stream) {
   const ScanPlan sp = plan_scan(idx, k, nq);
   int n_wg = sp.n_wg;
+  int kc = sp.kc;
   if (use_gemm_scan(nq)) {
     const GemmPlan gp = plan_gemm(idx, nq);
     n_wg = gp.n_ranges;
@@ -2412,6 +2686,17 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
       ARMI_LAUNCHED("dense_gemm_scan_kernel");
     }
     if (int rc = tl.end()) return rc;
+  } else if (use_i8_filter(idx, k)) {
+    kc = kc_i8(k);
+    if (int rc = allow_lds(dense_scan_i8_kernel<DIM>, scan_i8_lds_bytes<DIM>())) return rc;
+    armi::TimedLaunch tl;
+    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
+    dense_scan_i8_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(),
+                                stream>>>(
+        idx->rows8, idx->a32, idx->e32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
+    ARMI_LAUNCHED("dense_scan_i8_kernel");
+    if (int rc = tl.end()) return rc;
   } else {
     if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
@@ -2426,7 +2711,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
-      w.inv_q, w.qnorm, k, sp.kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
+      w.inv_q, w.qnorm, k, kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
       out_flags);
   ARMI_LAUNCHED("dense_merge_kernel");
   return launch_exact<DIM>(idx, queries, nq, k, row_mask, out_scores, out_ids, out_rank,
@@ -2449,6 +2734,13 @@ int dispatch_dim(int dim, F&& f) {
 extern "C" {
 
 // Workspace layout: [carved buffers][rank scratch nq*k doubles][flags nq u32]
+int armi_dense_scan_form(const armi_index* idx, int n_queries, int k) {
+  if (!idx || n_queries <= 0 || k <= 0) return -1;
+  k = std::min(k, kMaxK);
+  if (use_gemm_scan(n_queries)) return ARMI_SCAN_TILED_FP16;
+  return use_i8_filter(idx, k) ? ARMI_SCAN_INT8_FILTER : ARMI_SCAN_FP16;
+}
+
 size_t armi_dense_workspace_bytes(const armi_index* idx, int n_queries, int k) {
   if (!idx || n_queries <= 0 || k <= 0) return 0;
   k = std::min(k, kMaxK);

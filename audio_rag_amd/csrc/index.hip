@@ -6,6 +6,7 @@
 // normalised copy, the store keeps the fp16 vector the encoder produced and an exact norm, so
 // the search ranks by the exact cosine of those fp16 values.
 #include <cmath>
+#include <type_traits>
 
 #include "armi_index.h"
 
@@ -56,6 +57,59 @@ __global__ __launch_bounds__(256) void row_norms_kernel(const uint16_t* __restri
   }
 }
 
+// One wave per row: the int8 filter image. s = max |x_i| / 127 (fp32), q_i = rint(x_i / s),
+// a32 = s / |x|, e32 = ||x - s q||_2 / |x| rounded up (the quantisation term of the filter's
+// score bound: |q.(x - s q)| / |x| <= |q| e32 by Cauchy-Schwarz).
+template <int DIM>
+__global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restrict__ rows,
+                                                         int64_t n_rows, int64_t n_padded,
+                                                         const double* __restrict__ inv_norm,
+                                                         const int64_t* __restrict__ norm2,
+                                                         int8_t* __restrict__ rows8,
+                                                         float* __restrict__ a32,
+                                                         float* __restrict__ e32) {
+  constexpr int E = DIM / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
+  if (row >= n_padded) return;
+  int8_t* dst = rows8 + row * DIM;
+  if (row >= n_rows || norm2[row] < 0) {  // padding or invalid: never a result
+#pragma unroll
+    for (int i = 0; i < E; ++i) dst[lane + 64 * i] = 0;
+    if (lane == 0) {
+      a32[row] = __builtin_nanf("");
+      e32[row] = 0.0f;
+    }
+    return;
+  }
+  const uint16_t* src = rows + row * DIM;
+  float x[E];
+  float mx = 0.0f;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    x[i] = (float)__builtin_bit_cast(_Float16, src[lane + 64 * i]);
+    mx = fmaxf(mx, fabsf(x[i]));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
+  double err = 0.0;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const float qv = fminf(fmaxf(rintf(x[i] / s), -127.0f), 127.0f);
+    dst[lane + 64 * i] = (int8_t)qv;
+    const double d = (double)x[i] - (double)s * (double)qv;  // exact in fp64
+    err += d * d;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
+  if (lane == 0) {
+    const double inv = inv_norm[row] * 16777216.0;  // 1 / |x|
+    a32[row] = (float)((double)s * inv);
+    e32[row] = (float)(sqrt(err) * inv * (1.0 + 1.0 / 1048576.0)) ;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -86,6 +140,9 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
   if (e == hipSuccess) e = hipMalloc(&idx->inv_norm, padded * sizeof(double));
   if (e == hipSuccess) e = hipMalloc(&idx->inv_norm32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&idx->invalid, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&idx->rows8, padded * dim);
+  if (e == hipSuccess) e = hipMalloc(&idx->a32, padded * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&idx->e32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMemsetAsync(idx->invalid, 0, sizeof(unsigned long long), stream);
   if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "armi_index_create alloc"); }
   const int64_t blocks = (padded + 3) / 4;
@@ -93,6 +150,18 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
       rows, n_rows, padded, dim, idx->norm2, idx->inv_norm, idx->inv_norm32, idx->invalid);
   e = hipGetLastError();
   if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "row_norms_kernel"); }
+  auto filt = [&](auto D) {
+    row_filter_kernel<decltype(D)::value><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+        rows, n_rows, padded, idx->inv_norm, idx->norm2, idx->rows8, idx->a32, idx->e32);
+  };
+  switch (dim) {
+    case 256: filt(std::integral_constant<int, 256>{}); break;
+    case 512: filt(std::integral_constant<int, 512>{}); break;
+    case 768: filt(std::integral_constant<int, 768>{}); break;
+    default: filt(std::integral_constant<int, 1024>{}); break;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "row_filter_kernel"); }
   *out = idx;
   return ARMI_OK;
 }
@@ -103,6 +172,9 @@ int armi_index_destroy(armi_index* idx) {
   hipFree(idx->inv_norm);
   hipFree(idx->inv_norm32);
   hipFree(idx->invalid);
+  hipFree(idx->rows8);
+  hipFree(idx->a32);
+  hipFree(idx->e32);
   delete idx;
   return ARMI_OK;
 }

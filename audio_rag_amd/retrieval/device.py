@@ -92,6 +92,10 @@ class DenseIndex:
             _device_copy(dst.data_ptr(), src.value, dst.numel() * dst.element_size())
         return out
 
+    def scan_form(self, n_queries: int, k: int) -> int:
+        """Which scan armi_dense_topk runs for this call shape (_armi.SCAN_*)."""
+        return int(query("armi_dense_scan_form", self._handle, n_queries, k))
+
     def workspace_bytes(self, n_queries: int, k: int, exact: bool = False) -> int:
         fn = "armi_dense_exact_workspace_bytes" if exact else "armi_dense_workspace_bytes"
         return int(query(fn, self._handle, n_queries, k))

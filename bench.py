@@ -207,8 +207,10 @@ def cpu_baseline(wl: str, ref: CpuReference, queries: np.ndarray, q_csr: list | 
     return res
 
 
-def read_traffic() -> float | None:
-    p = ROOT / "profiles" / "dense_scan_traffic.json"
+def read_traffic(form: int = 0) -> float | None:
+    """HBM bytes per launch of the 64-query scan from the committed PMC pass (FETCH_SIZE +
+    WRITE_SIZE, gfx950-corrected) for the scan form armi_dense_scan_form reports."""
+    p = ROOT / "profiles" / ("dense_scan_i8_traffic.json" if form == 1 else "dense_scan_traffic.json")
     if p.exists():
         try:
             return float(json.loads(p.read_text())["hbm_bytes_per_launch"])
@@ -421,13 +423,21 @@ def main() -> None:
     scan_avg_ms = tot_ms.value / max(launches.value, 1)
     shard_rows = hi - lo
     nq_scan = world * batch  # queries each rank's scan processes per step (all-gathered)
-    alg_bytes = shard_rows * dim * 2 + shard_rows * 4 + nq_scan * dim * 2
+    form = index.scan_form(nq_scan, pre_k)  # which scan armi_dense_topk ran (include/armi.h)
+    if form == _armi.SCAN_INT8_FILTER:
+        # int8 filter image (1 B / component) + a32, e32 (8 B / row) + the fp16 queries
+        alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim * 2
+        scan_kernel = f"dense_scan_i8_kernel<{dim}>"
+    else:
+        alg_bytes = shard_rows * dim * 2 + shard_rows * 4 + nq_scan * dim * 2
+        scan_kernel = (f"dense_scan_kernel<{dim}>" if form == _armi.SCAN_FP16
+                       else f"dense_gemm_scan_w4_kernel<{dim}>")
     alg_flops = 2.0 * shard_rows * dim * nq_scan
     # the scan's bound: HBM while the batch is small (arithmetic intensity ~ queries/pass flop/B),
     # the fp16 MFMA once the all-gathered batch of a multi-GPU step passes the ridge
     mfma_bound = alg_flops / (MFMA_PEAK_TFLOPS["fp16"] * 1e12) > alg_bytes / (HBM_PEAK_GBS * 1e9)
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic = read_traffic()
+    traffic = read_traffic(form)
     result = {
         "metric": METRIC,
         "value": total_queries / elapsed,
@@ -461,8 +471,7 @@ def main() -> None:
         "certified_frac": certified,
         "roofline": ({
             "bound": "hbm",
-            "kernel": ("dense_scan_kernel<1024>" if nq_scan <= 128
-                       else "dense_gemm_scan_glds_kernel<1024>"),
+            "kernel": scan_kernel,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -473,7 +482,7 @@ def main() -> None:
             "launches_timed": launches.value,
         } if not mfma_bound else {
             "bound": "mfma",
-            "kernel": "dense_gemm_scan_glds_kernel<1024>",
+            "kernel": scan_kernel,
             "achieved": alg_flops / (scan_avg_ms * 1e-3) / 1e12,
             "peak": MFMA_PEAK_TFLOPS["fp16"],
             "unit": "TFLOP/s",

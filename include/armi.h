@@ -81,9 +81,24 @@ int64_t armi_index_invalid_rows(const armi_index* index);
 /* device pointers of the per-row norm arrays built at create time:
  *   norm2[r]     = sum_i (2^24 * x_ri)^2 as an exact int64
  *   inv_norm[r]  = 1.0 / sqrt((double) norm2[r])       (0.0 for a zero row)
- *   inv_norm32[r]= (float)(inv_norm[r] * 2^24)          (scale factor of the fast scan) */
+ *   inv_norm32[r]= (float)(inv_norm[r] * 2^24)          (scale factor of the fast scan)
+ * The index also keeps an int8 filter image of the rows (1 B per component, built at create
+ * time: s_r = max_i |x_ri| / 127, round(x_ri / s_r)) with s_r / |x_r| and a Cauchy-Schwarz bound
+ * of the quantisation error per row; the 64-query scan reads it for k <= 16 (armi_dense_scan_form). */
 int armi_index_norms(const armi_index* index, const int64_t** norm2, const double** inv_norm,
                      const float** inv_norm32);
+
+/* The scan armi_dense_topk runs for n_queries queries and top-k (for roofline accounting):
+ *   ARMI_SCAN_FP16         64-query scan over the fp16 rows (2 B per component)
+ *   ARMI_SCAN_INT8_FILTER  64-query scan over the index's int8 filter image (1 B per component
+ *                          + 8 B per row), then an exact fp16 rescore of the best upper bounds
+ *                          (k <= 16; the default for those k)
+ *   ARMI_SCAN_TILED_FP16   > 128 queries: the LDS-tiled MFMA scan over the fp16 rows
+ * Results are the same exact ranking on every form. -1 for invalid arguments. */
+#define ARMI_SCAN_FP16 0
+#define ARMI_SCAN_INT8_FILTER 1
+#define ARMI_SCAN_TILED_FP16 2
+int armi_dense_scan_form(const armi_index* index, int n_queries, int k);
 
 /* Workspace bytes needed by armi_dense_topk for n_queries queries and top-k. */
 size_t armi_dense_workspace_bytes(const armi_index* index, int n_queries, int k);
