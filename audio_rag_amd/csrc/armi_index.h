@@ -19,7 +19,8 @@ struct armi_index {
   unsigned long long* invalid = nullptr;  // [1] count of rows outside the fp16 domain
   // int8 filter image of the rows (the first pass of the 64-query scan reads these 1-byte
   // components instead of the 2-byte fp16 ones): row r ~= s_r * rows8[r], s_r = max_i |x_ri| / 127
-  int8_t* rows8 = nullptr;       // [n_tiles*32][dim] round(x / s_r) (0 for invalid / padding)
+  int8_t* rows8 = nullptr;       // [n_tiles][dim / 16][32][16] round(x / s_r) (0 for invalid /
+                                 // padding): 16-B chunk c of row r at tile r/32, chunk c, lane r%32
   float* a32 = nullptr;          // [n_tiles*32] s_r / |x_r| (score scale; NaN = invalid / padding)
   float* e32 = nullptr;          // [n_tiles*32] >= ||x_r - s_r rows8[r]||_2 / |x_r| (per unit |q|)
 };

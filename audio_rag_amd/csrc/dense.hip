@@ -333,14 +333,21 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& 
 // dense_merge_kernel discards still satisfy exact <= bound + delta (delta: the fp32 accumulation
 // term, unchanged) and its certificate holds as for the fp16 scan; it rescoring more of the pool
 // (kc_i8) absorbs the looser keys.
-template <int DIM>
+// QI8 (k <= 6): the queries are int8 too (t_q = max |q_i| / 127) and the MFMA is
+// v_mfma_i32_32x32x32_i8: exact int32 dots, no conversion VALU, half the MFMA cycles of the fp16
+// form; the key adds the query's own quantisation term: acc * t a32 + e32 |q| + e_q (1 + e32)
+// with e_q >= ||q - t_q q8||_2 (|q.x - (t q8).(s x8)| / |x| <= |q| e32 + ||q - t q8|| |s x8| / |x|).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+template <int DIM, bool QI8>
 __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     int guard) {
-  constexpr int KSTEPS = DIM / 16;
+  constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
   constexpr int DEPTH = GROUPS % 4 == 0 ? 4 : 2;  // groups in flight per lane
   int qb = 0, rp = blockIdx.x;
@@ -355,7 +362,9 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   const uint16_t* __restrict__ queries = queries_all + (size_t)q0 * DIM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
-  float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB]
+  float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
+  float* qscale = qnorm + kQB;  // [kQB] t_q (QI8)
+  float* qerr = qscale + kQB;   // [kQB] e_q (QI8)
 
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
@@ -364,10 +373,10 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
   int64_t t = t_begin + wave;
+  // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
+  // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
   auto row_ptr = [&](int64_t tile) -> const u32x4* {
-    int64_t rr = tile * TILE_ROWS + r;
-    rr = rr < n_rows ? rr : n_rows - 1;
-    return reinterpret_cast<const u32x4*>(rows8 + rr * DIM) + 4 * h;
+    return reinterpret_cast<const u32x4*>(rows8 + tile * TILE_ROWS * DIM) + r + 4 * h * 32;
   };
   const u32x4* cur = row_ptr(t < t_end ? t : t_begin);
   u32x4 buf[DEPTH][4];
@@ -375,36 +384,85 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
     for (int g = 0; g < DEPTH; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 8 * g + i);
+      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 32 * (8 * g + i));
   }
 
-  // 1. Query fragment image (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) and
-  //    the query norms, rounded up (fp32 sum of 1024 squares: relative error < 2^-13).
+  // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13) and, QI8,
+  //    t_q and e_q (rounded up, plus 2^-20 |q| for the rounding of t_q * q8_i). Then the
+  //    fragment image: fp16 (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) or
+  //    QI8 int8 (components 128(s>>2) + 64h + 16(s&3) .. +15), the corpus chunks' order.
+  for (int q = wave; q < kQB; q += kWaves) {
+    float v[DIM / 64];
+    float ss = 0.0f, mx = 0.0f;
+#pragma unroll
+    for (int i = 0; i < DIM / 64; ++i) {
+      v[i] = q < nq ? (float)__builtin_bit_cast(_Float16, queries[(size_t)q * DIM + lane + 64 * i])
+                    : 0.0f;
+      ss += v[i] * v[i];
+      mx = fmaxf(mx, fabsf(v[i]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ss += __shfl_xor(ss, off);
+      mx = fmaxf(mx, __shfl_xor(mx, off));
+    }
+    const float qn = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
+    if constexpr (QI8) {
+      const float t = mx > 0.0f ? mx / 127.0f : 1.0f;
+      float ee = 0.0f;
+#pragma unroll
+      for (int i = 0; i < DIM / 64; ++i) {
+        const float d = v[i] - t * fminf(fmaxf(rintf(v[i] / t), -127.0f), 127.0f);
+        ee += d * d;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) ee += __shfl_xor(ee, off);
+      if (lane == 0) {
+        qscale[q] = t;
+        qerr[q] = sqrtf(ee) * (1.0f + 1.0f / 4096.0f) + qn * (1.0f / 1048576.0f);
+      }
+    }
+    if (lane == 0) qnorm[q] = qn;
+  }
+  if constexpr (QI8) __syncthreads();
   for (int e = threadIdx.x; e < KSTEPS * 2 * kQB; e += kThreads) {
     const int q = e & (kQB - 1);
     const int sh = e >> 6;
     const int hh = sh & 1;
     const int s = sh >> 1;
-    const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off);
-    qimg[e] = v;
-  }
-  for (int q = wave; q < kQB; q += kWaves) {
-    float ss = 0.0f;
-    if (q < nq) {
+    if constexpr (QI8) {
+      if (q < nq) {
+        const int off = 128 * (s >> 2) + 64 * hh + 16 * (s & 3);
+        const float t = qscale[q];
+        uint32_t w[4];
 #pragma unroll
-      for (int i = 0; i < DIM / 64; ++i) {
-        const float v = (float)__builtin_bit_cast(_Float16, queries[(size_t)q * DIM + lane + 64 * i]);
-        ss += v * v;
+        for (int d = 0; d < 4; ++d) {
+          uint32_t pk = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const float x = (float)__builtin_bit_cast(
+                _Float16, queries[(size_t)q * DIM + off + 4 * d + b]);
+            const int qi = (int)fminf(fmaxf(rintf(x / t), -127.0f), 127.0f);
+            pk |= ((uint32_t)qi & 0xffu) << (8 * b);
+          }
+          w[d] = pk;
+        }
+        v = u32x4{w[0], w[1], w[2], w[3]};
       }
+    } else {
+      const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
+      if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-    if (lane == 0) qnorm[q] = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
+    qimg[e] = v;
   }
   __syncthreads();
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
+  float qt0 = 1.0f, qt1 = 1.0f, qe0 = 0.0f, qe1 = 0.0f;
+  if constexpr (QI8) {
+    qt0 = qscale[r]; qt1 = qscale[32 + r];
+    qe0 = qerr[r]; qe1 = qerr[32 + r];
+  }
 
   float s0[kLaneList], s1[kLaneList];
   int32_t i0[kLaneList], i1[kLaneList];
@@ -421,7 +479,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       int qoff = h * kQB + r;
       asm volatile("" : "+v"(qoff));
       const u32x4* qv = qimg + qoff;
-      f32x16 acc0 = {}, acc1 = {};
+      using Acc = std::conditional_t<QI8, i32x16, f32x16>;
+      Acc acc0 = {}, acc1 = {};
 #pragma unroll
       for (int g = 0; g < GROUPS; ++g) {
         u32x4 a[4];
@@ -429,13 +488,27 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         for (int i = 0; i < 4; ++i) a[i] = buf[g % DEPTH][i];
         if (g + DEPTH < GROUPS) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) buf[g % DEPTH][i] = stream_load(cur + 8 * (g + DEPTH) + i);
+          for (int i = 0; i < 4; ++i)
+            buf[g % DEPTH][i] = stream_load(cur + 32 * (8 * (g + DEPTH) + i));
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            buf[g % DEPTH][i] = stream_load(nxt + 8 * (g + DEPTH - GROUPS) + i);
+            buf[g % DEPTH][i] = stream_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (QI8) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int s = 4 * g + i;
+            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                __builtin_bit_cast(i32x4, a[i]), __builtin_bit_cast(i32x4, qv[s * 2 * kQB]), acc0,
+                0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                __builtin_bit_cast(i32x4, a[i]), __builtin_bit_cast(i32x4, qv[s * 2 * kQB + 32]),
+                acc1, 0, 0, 0);
+          }
+          continue;
+        } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           uint32_t c[8];  // fp16 pairs of components 0-7 (c[0..3]) and 8-15 (c[4..7])
@@ -458,6 +531,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
           acc0 = mfma16(f1, qv[(s + 1) * 2 * kQB], acc0);
           acc1 = mfma16(f1, qv[(s + 1) * 2 * kQB + 32], acc1);
 #endif
+        }
         }
       }
       cur = nxt;
@@ -483,8 +557,15 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       float mx0 = kNegInf, mx1 = kNegInf;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        x0[j] = __builtin_fmaf(acc0[j], sc[j], ec[j] * qn0);
-        x1[j] = __builtin_fmaf(acc1[j], sc[j], ec[j] * qn1);
+        if constexpr (QI8) {  // int32 dots are exact, |acc| < 2^24 converts exactly
+          x0[j] = __builtin_fmaf((float)acc0[j], sc[j] * qt0,
+                                 __builtin_fmaf(ec[j], qn0 + qe0, qe0));
+          x1[j] = __builtin_fmaf((float)acc1[j], sc[j] * qt1,
+                                 __builtin_fmaf(ec[j], qn1 + qe1, qe1));
+        } else {
+          x0[j] = __builtin_fmaf(acc0[j], sc[j], ec[j] * qn0);
+          x1[j] = __builtin_fmaf(acc1[j], sc[j], ec[j] * qn1);
+        }
         mx0 = fmaxf(mx0, x0[j]);
         mx1 = fmaxf(mx1, x1[j]);
       }
@@ -565,7 +646,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
 template <int DIM>
 constexpr int scan_i8_lds_bytes() {
-  return scan_lds_bytes<DIM>() + kQB * 4;
+  return scan_lds_bytes<DIM>() + kQB * 12;
 }
 
 // Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
@@ -2013,7 +2094,7 @@ __device__ __forceinline__ float from_ord_key(uint32_t k) {
 //   kept (typically ~2*kc of n_wg*kKW) and sorted. Entries below t0 are discards and join the
 //   bound. Small sorts run inside one wave (shuffles, no barriers).
 constexpr int kSelCap = 1024;  // kept entries per query; overflow -> uncertified (exact fallback)
-constexpr int kRescoreBatch = 4;
+constexpr int kRescoreBatch = 8;
 
 template <int DIM>
 __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
@@ -2090,20 +2171,32 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   __syncthreads();
   const float t0 = red[9];
 
-  // filter the pool
+  // filter the pool: 8 entries per thread per round, all loads issued before any is used (a
+  // latency-bound kernel: one memory round trip per round, not per entry)
   float dmax = kNegInf;
-  for (int e = tid; e < pool; e += kMergeThreads) {
-    const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
-    const float kk = cand_key[src];
-    if (kk == kNegInf) continue;
-    if (kk >= t0) {
-      const int slot = atomicAdd(&ctr[0], 1);
-      if (slot < kSelCap) {
-        skey[slot] = kk;
-        srow[slot] = cand_row[src];
+  constexpr int kFilterBatch = 8;
+  for (int e0 = tid; e0 < pool; e0 += kFilterBatch * kMergeThreads) {
+    float kk[kFilterBatch];
+    int32_t rw[kFilterBatch];
+#pragma unroll
+    for (int j = 0; j < kFilterBatch; ++j) {
+      const int e = e0 + j * kMergeThreads;
+      const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
+      kk[j] = e < pool ? cand_key[src] : kNegInf;
+      rw[j] = e < pool ? cand_row[src] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kFilterBatch; ++j) {
+      if (kk[j] == kNegInf) continue;
+      if (kk[j] >= t0) {
+        const int slot = atomicAdd(&ctr[0], 1);
+        if (slot < kSelCap) {
+          skey[slot] = kk[j];
+          srow[slot] = rw[j];
+        }
+      } else {
+        dmax = fmaxf(dmax, kk[j]);
       }
-    } else {
-      dmax = fmaxf(dmax, kk);
     }
   }
 #pragma unroll
@@ -2481,9 +2574,21 @@ bool use_i8_filter(const armi_index* idx, int k) {
   }();
   return !off && idx->rows8 != nullptr && k <= kI8MaxK;
 }
+// int8 queries and the int8 MFMA too (ARMI_DENSE_QUERY=int8, k <= 6; A/B only): parity-green
+// but not faster (scan 0.286 vs 0.275 ms at 1M x 1024: the pass is bound by its loads, not by
+// the int8 -> fp16 conversion), and its looser keys (~45-85 rows reach the 5th cosine) leave
+// some queries uncertified at kc = 128 (exact fallback: 1.40 vs 0.35 ms mean step,
+// profiles/r02_int8_filter_ab.txt).
+bool use_q8(int k) {
+  static const bool on = [] {
+    const char* e = getenv("ARMI_DENSE_QUERY");
+    return e && e[0] == 'i';
+  }();
+  return on && k <= 6;
+}
 // Rows rescored per query after the int8 pass: the rows whose key (an upper bound) reaches the
 // k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008).
-int kc_i8(int k) { return k <= 6 ? 64 : 128; }
+int kc_i8(int k) { return use_q8(k) ? 128 : (k <= 6 ? 64 : 128); }
 
 struct GemmPlan {
   int n_qb = 0;
@@ -2688,11 +2793,13 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (int rc = tl.end()) return rc;
   } else if (use_i8_filter(idx, k)) {
     kc = kc_i8(k);
-    if (int rc = allow_lds(dense_scan_i8_kernel<DIM>, scan_i8_lds_bytes<DIM>())) return rc;
+    const bool qi8 = use_q8(k);
+    auto kern = qi8 ? dense_scan_i8_kernel<DIM, true> : dense_scan_i8_kernel<DIM, false>;
+    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, true>, scan_i8_lds_bytes<DIM>())) return rc;
+    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, false>, scan_i8_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    dense_scan_i8_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(),
-                                stream>>>(
+    kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
     ARMI_LAUNCHED("dense_scan_i8_kernel");

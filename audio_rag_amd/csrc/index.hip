@@ -72,10 +72,13 @@ __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restr
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
   if (row >= n_padded) return;
-  int8_t* dst = rows8 + row * DIM;
+  // tile-blocked layout: 16-B chunk c of row r sits at (r / 32) * 32 * DIM + c * 512 + (r % 32) * 16,
+  // so the scan's wave-wide chunk loads (32 rows x 16 B per lane half) are contiguous 512-B runs
+  int8_t* tile = rows8 + (row >> 5) * 32 * DIM + (row & 31) * 16;
+  auto dst_at = [&](int i) -> int8_t& { return tile[(i >> 4) * 512 + (i & 15)]; };
   if (row >= n_rows || norm2[row] < 0) {  // padding or invalid: never a result
 #pragma unroll
-    for (int i = 0; i < E; ++i) dst[lane + 64 * i] = 0;
+    for (int i = 0; i < E; ++i) dst_at(lane + 64 * i) = 0;
     if (lane == 0) {
       a32[row] = __builtin_nanf("");
       e32[row] = 0.0f;
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restr
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const float qv = fminf(fmaxf(rintf(x[i] / s), -127.0f), 127.0f);
-    dst[lane + 64 * i] = (int8_t)qv;
+    dst_at(lane + 64 * i) = (int8_t)qv;
     const double d = (double)x[i] - (double)s * (double)qv;  // exact in fp64
     err += d * d;
   }
