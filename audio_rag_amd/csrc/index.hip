@@ -143,7 +143,9 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
   if (e == hipSuccess) e = hipMalloc(&idx->inv_norm, padded * sizeof(double));
   if (e == hipSuccess) e = hipMalloc(&idx->inv_norm32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&idx->invalid, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMalloc(&idx->rows8, padded * dim);
+  // whole 32-row tiles (the tile-blocked layout), also for an empty store
+  const int64_t tiled = std::max<int64_t>(idx->n_tiles, 1) * armi::TILE_ROWS;
+  if (e == hipSuccess) e = hipMalloc(&idx->rows8, tiled * dim);
   if (e == hipSuccess) e = hipMalloc(&idx->a32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&idx->e32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMemsetAsync(idx->invalid, 0, sizeof(unsigned long long), stream);
