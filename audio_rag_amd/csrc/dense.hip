@@ -322,6 +322,15 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& 
   hi = __builtin_bit_cast(uint32_t, h - bias);
 }
 
+// Loads of the int8 image (probe builds may try the non-temporal policy: -DARMI_I8_NT).
+__device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_NT)
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 // Int8-filter form of dense_scan_kernel: the default 64-query scan (round 2). Each row's first
 // pass reads its 1-byte int8 image (rows8, one 1 KB row at dim 1024) instead of its 2-byte fp16
 // components: half the HBM bytes of the HBM-bound pass. Lane half h loads 16-B chunks 8g+4h+i of
@@ -364,7 +373,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
   float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
   float* qscale = qnorm + kQB;  // [kQB] t_q (QI8)
-  float* qerr = qscale + kQB;   // [kQB] e_q (QI8)
+  float* qerr = qscale + kQB;   // [kQB] e_q (QI8); [8][kQB] norm partials (fp16 queries)
 
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
@@ -384,13 +393,47 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
     for (int g = 0; g < DEPTH; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) buf[g][i] = stream_load(cur + 32 * (8 * g + i));
+      for (int i = 0; i < 4; ++i) buf[g][i] = i8_load(cur + 32 * (8 * g + i));
   }
 
   // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13) and, QI8,
   //    t_q and e_q (rounded up, plus 2^-20 |q| for the rounding of t_q * q8_i). Then the
   //    fragment image: fp16 (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) or
   //    QI8 int8 (components 128(s>>2) + 64h + 16(s&3) .. +15), the corpus chunks' order.
+  if constexpr (!QI8) {
+    // fp16 image: thread (q = tid % 64, sh0 = tid / 64) copies entries sh = sh0 + 8 i of query q,
+    // all 2*KSTEPS/8 loads in flight at once (a dependent load per entry would cost one L2 round
+    // trip each), and sums its components' squares for the query norm on the way.
+    constexpr int PER = KSTEPS * 2 / (kThreads / kQB);  // entries per thread (16 at dim 1024)
+    const int q = threadIdx.x & (kQB - 1);
+    const int sh0 = threadIdx.x >> 6;
+    u32x4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int sh = sh0 + (kThreads / kQB) * i;
+      const int s = sh >> 1, hh = sh & 1;
+      const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
+      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off)
+                    : u32x4{0u, 0u, 0u, 0u};
+    }
+    float ss = 0.0f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int sh = sh0 + (kThreads / kQB) * i;
+      qimg[sh * kQB + q] = v[i];
+      const half8 hv = __builtin_bit_cast(half8, v[i]);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
+    }
+    qerr[sh0 * kQB + q] = ss;  // partial sums, [8][kQB] (qerr is free in this form)
+    __syncthreads();
+    if (threadIdx.x < kQB) {
+      float t = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kThreads / kQB; ++j) t += qerr[j * kQB + threadIdx.x];
+      qnorm[threadIdx.x] = sqrtf(t) * (1.0f + 1.0f / 4096.0f);
+    }
+  } else {
   for (int q = wave; q < kQB; q += kWaves) {
     float v[DIM / 64];
     float ss = 0.0f, mx = 0.0f;
@@ -456,6 +499,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     }
     qimg[e] = v;
   }
+  }
   __syncthreads();
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
   float qt0 = 1.0f, qt1 = 1.0f, qe0 = 0.0f, qe1 = 0.0f;
@@ -489,11 +533,11 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         if (g + DEPTH < GROUPS) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            buf[g % DEPTH][i] = stream_load(cur + 32 * (8 * (g + DEPTH) + i));
+            buf[g % DEPTH][i] = i8_load(cur + 32 * (8 * (g + DEPTH) + i));
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            buf[g % DEPTH][i] = stream_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
+            buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (QI8) {
@@ -646,7 +690,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
 template <int DIM>
 constexpr int scan_i8_lds_bytes() {
-  return scan_lds_bytes<DIM>() + kQB * 12;
+  return scan_lds_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB);
 }
 
 // Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
