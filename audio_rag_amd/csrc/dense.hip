@@ -50,6 +50,7 @@ constexpr double kNegInfD = -std::numeric_limits<double>::infinity();
 constexpr int64_t kNoOrd = std::numeric_limits<int64_t>::max();
 constexpr int kMaxK = 240;
 constexpr int kMergeThreads = 256;
+constexpr int kDenseMergeThreads = 512;  // dense_merge_kernel: 8 waves share the exact rescore
 constexpr int kMaxPool = 4096;  // pooled candidates per query in the merge kernels
 // delta = kDeltaSafety * dim * 2^-24 * |q|: the fp32 accumulation error bound gamma_dim * |q|
 // (|sum| <= sum |q_i x_i| <= |q||x|) with a 4x allowance for the MFMA's internal ordering.
@@ -2141,7 +2142,7 @@ constexpr int kSelCap = 1024;  // kept entries per query; overflow -> uncertifie
 constexpr int kRescoreBatch = 8;
 
 template <int DIM>
-__global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
+__global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
     const float* __restrict__ cand_bound, int n_wg, int q_stride, const uint16_t* __restrict__ rows,
     const double* __restrict__ inv_norm, const uint16_t* __restrict__ queries,
@@ -2219,12 +2220,12 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
   // latency-bound kernel: one memory round trip per round, not per entry)
   float dmax = kNegInf;
   constexpr int kFilterBatch = 8;
-  for (int e0 = tid; e0 < pool; e0 += kFilterBatch * kMergeThreads) {
+  for (int e0 = tid; e0 < pool; e0 += kFilterBatch * kDenseMergeThreads) {
     float kk[kFilterBatch];
     int32_t rw[kFilterBatch];
 #pragma unroll
     for (int j = 0; j < kFilterBatch; ++j) {
-      const int e = e0 + j * kMergeThreads;
+      const int e = e0 + j * kDenseMergeThreads;
       const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
       kk[j] = e < pool ? cand_key[src] : kNegInf;
       rw[j] = e < pool ? cand_row[src] : 0;
@@ -2261,26 +2262,69 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
     }
     __syncthreads();
     n2 = 64;
+  } else if (n_keep <= 4 * 64 && kc <= 64) {
+    // Top 64 of up to 256 kept entries without a workgroup-wide bitonic sort (one barrier per
+    // stage): each wave sorts a run of 64 in registers, then wave 0 folds the runs pairwise (run
+    // A against run B reversed: the lane-wise better entries are the top 64 of both, a bitonic
+    // sequence that 6 half-cleaner stages sort). Everything folded away joins the bound.
+    {
+      float key = 64 * wave + lane < n_keep ? skey[64 * wave + lane] : kNegInf;
+      int32_t row = 64 * wave + lane < n_keep ? srow[64 * wave + lane] : 0x7fffffff;
+      armi::wave_sort_approx_desc(key, row);
+      skey[64 * wave + lane] = key;
+      srow[64 * wave + lane] = row;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      float key = skey[lane];
+      int32_t row = srow[lane];
+      float lost = kNegInf;
+      for (int run = 1; run < 4 && 64 * run < n_keep; ++run) {
+        const float okey = skey[64 * run + 63 - lane];
+        const int32_t orow = srow[64 * run + 63 - lane];
+        const bool other = armi::approx_better(okey, orow, key, row);
+        lost = fmaxf(lost, other ? key : okey);
+        if (other) { key = okey; row = orow; }
+#pragma unroll
+        for (int stride = 32; stride > 0; stride >>= 1) {
+          const float k2 = __shfl_xor(key, stride);
+          const int32_t r2 = __shfl_xor(row, stride);
+          const bool lower = (lane & stride) == 0;
+          const bool better = armi::approx_better(k2, r2, key, row);
+          if (lower == better) { key = k2; row = r2; }
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) lost = fmaxf(lost, __shfl_xor(lost, off));
+      skey[lane] = key;
+      srow[lane] = row;
+      if (lane == 0) red[10] = lost;
+    }
+    __syncthreads();
+    n2 = 64;
   } else {
     n2 = armi::pow2_at_least(n_keep > kc ? n_keep : kc);
-    for (int e = n_keep + tid; e < n2; e += kMergeThreads) {
+    for (int e = n_keep + tid; e < n2; e += kDenseMergeThreads) {
       skey[e] = kNegInf;
       srow[e] = 0x7fffffff;
     }
     armi::lds_sort_approx_desc(skey, srow, n2);
   }
-  float bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  bound = fmaxf(bound, red[8]);
+  float bound = red[8];
+#pragma unroll
+  for (int w = 0; w < kDenseMergeThreads / 64; ++w) bound = fmaxf(bound, red[w]);
+  if (n_keep > 64 && n_keep <= 4 * 64 && kc <= 64) bound = fmaxf(bound, red[10]);
   if (kc < n2) bound = fmaxf(bound, skey[kc]);
 
   // exact rescore of the kc best, kRescoreBatch rows in flight per wave
-  const int per_wave = kc / 4;
+  constexpr int kMW = kDenseMergeThreads / 64;
+  const int per_wave = (kc + kMW - 1) / kMW;
   for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
     u32x2 raw[kRescoreBatch][DIM / 256];
     int32_t rr[kRescoreBatch];
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
-      const int c = wave + 4 * (i0 + j);
+      const int c = wave + kMW * (i0 + j);
       const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
       rr[j] = live ? srow[c] : -1;
       load_raw<DIM>(rows + (size_t)(live ? rr[j] : 0) * DIM, lane, raw[j]);
@@ -2288,7 +2332,7 @@ __global__ __launch_bounds__(kMergeThreads) void dense_merge_kernel(
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
       if (i0 + j >= per_wave) break;
-      const int c = wave + 4 * (i0 + j);
+      const int c = wave + kMW * (i0 + j);
       double key = kNegInfD;
       int64_t ord = kNoOrd;
       const int64_t dot = dot_fixed<DIM>(qf, raw[j]);
@@ -2860,7 +2904,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
-  dense_merge_kernel<DIM><<<dim3(nq), dim3(kMergeThreads), kMergeLds, stream>>>(
+  dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
       out_flags);
