@@ -12,17 +12,17 @@
 // closed by a sentinel row; rows cut into one contiguous range per CU.
 //
 // Search, one pass per 64 queries:
-//   wave_terms: the 64 queries are dealt to 16 waves, 4 each (wave w owns queries w, w+16, ...).
-//           Per wave: the ascending union of its queries' terms with a 4-bit query mask and the
-//           4 weights.
-//   scan:   workgroup = one row range, wave = 4 queries, lane = one row of a 64-row tile. For each
-//           tile the wave walks its terms in ascending term order; a term whose next posting is
-//           inside the tile loads 64 postings (lane-reversed), keeps the prefix inside the tile
-//           and ds_permutes each value to the lane of its row, where every owning query adds
-//           fl32(w * v) into its fp32 accumulator. Ascending term order per (row, query) is the
-//           Qdrant summation order; nothing else is reordered. Per-term cursors carry over to
-//           the next tile. Each wave keeps a sorted 16-entry list per query (16 lanes each) plus
-//           the best score it dropped.
+//   pass_terms: the 64 queries are dealt to 16 waves, 4 each (slot 4w + i), and every slot gets
+//           the ascending list of its query's terms as (staging row offset, weight).
+//   scan:   workgroup = one row range, wave = 4 queries, lane = two adjacent rows of a 128-row
+//           tile. Each distinct term of the pass is staged once per tile: its holder wave loads
+//           the next 64 (or 128) postings (lane-reversed), keeps the prefix inside the tile and
+//           scatters the values into the term's 128-entry row image in LDS. Then every wave
+//           walks each of its queries' terms in ascending term order and adds fl32(w * v) into
+//           that query's fp32 accumulators of the lane's two rows (packed multiply, packed add).
+//           Ascending term order per (row, query) is the Qdrant summation order; nothing else
+//           is reordered. Per-term cursors carry over to the next tile. Each wave keeps a sorted
+//           16-entry list per query (16 lanes each) plus the best score it dropped.
 //   merge:  per query, pool the range lists, keep the k best, certify against the dropped
 //           bound (scores are exact, so the bound test is strict: k-th > bound).
 //   fallback for uncertified queries: the scan rerun in collect mode gathers every row scoring
@@ -47,16 +47,16 @@ constexpr int kSelCap = 1024;           // kept entries per query in the merge
 constexpr int kMaxK = 240;
 constexpr int kCollectCap = 4096;       // rows per query collected by the fallback
 constexpr int kMaxTerms = 256;          // query terms per query (BGE-M3 queries are short)
-constexpr int kWaveTerms = kQW * kMaxTerms;
 constexpr int kLongTerm = 256;          // postings from which a term gets a range-start table
-constexpr int kPad = 64;
+constexpr int kPad = 128;               // sentinel slots past the last list (two 64-posting loads)
 constexpr int kBatch = 4;               // terms whose LDS reads are in flight together
+constexpr int kTile = 128;              // rows per scan step: two adjacent rows per lane
 constexpr int kMaxRanges = 256;
 constexpr int kMaxU = kQB * kMaxTerms;  // distinct terms of one pass, at most
 constexpr int kU = 128;                 // terms per staging segment
 constexpr int kHold = kU / kWaves;      // terms of a segment staged by one wave
 constexpr int kRegSegs = 64 / kHold;    // segments whose cursors stay in registers
-constexpr size_t kScanLds = (size_t)2 * kU * 64 * 4;   // double-buffered staging, 128 KB
+constexpr size_t kScanLds = (size_t)2 * kU * kTile * 4;  // double-buffered staging, 128 KB
 constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + weights, 128 KB
 constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
@@ -171,26 +171,23 @@ __global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz
 
 // ------------------------------------------------------------------------- per-pass prep
 
-// One term of a wave's list: byte offset of its staging row within a segment buffer
-// ((u % kU) * 256), owning-query mask, the 4 query weights (0 where the query lacks the term),
-// pass term index u. 32 B: one scalar load.
-struct alignas(32) TermMeta {
+// One entry of a query's term list: byte offset of the term's staging row within a segment buffer
+// ((u % kU) * kTile * 4) and the query's weight. 8 B: a batch of 4 entries is one 32-B scalar load.
+struct alignas(8) QTerm {
   int32_t off;
-  int32_t m;
-  float w[kQW];
-  int32_t u;
-  int32_t pad;
+  float w;
 };
 
-// One block for the pass. Sorts the pass's (term, query) pairs by (term, wave, i) with query
-// q = wave + 16 i, numbers the distinct terms u = 0..nU-1 ascending (uterm[u] = term), and builds
-// per wave the ascending list of its terms: (u, 4-bit query mask, 4 weights).
+// One block for the pass. Sorts the pass's (term, query) pairs by (term, slot) where query q sits
+// in slot 4 w + i of wave w, numbers the distinct terms u = 0..nU-1 ascending (uterm[u] = term),
+// and builds per slot the ascending list of its query's terms: (staging offset, weight) in ql and
+// u in qu, qcount entries.
 // flags[q] = 8 when a query has more than 256 terms (the first 256 are used).
 __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const int32_t* __restrict__ q_indptr, const int32_t* __restrict__ q_indices,
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
-    int32_t* __restrict__ n_terms, TermMeta* __restrict__ wl, int32_t* __restrict__ wl_count,
-    int32_t* __restrict__ qof, uint32_t* __restrict__ flags) {
+    int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
+    int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
   float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
@@ -217,7 +214,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     off[tid + 1] = x;
     if (tid == 0) off[0] = 0;
     // balance the waves: queries sorted by term count (desc, then index) are dealt to the waves
-    // in snake order, so each wave's union of terms (its per-tile work) is about the same
+    // in snake order, so each wave's sum of term counts (its per-tile work) is about the same
     int sk = (tid < nq ? n : -1) * 64 + (63 - tid);
 #pragma unroll
     for (int size = 2; size <= 64; size <<= 1) {
@@ -343,36 +340,27 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
   __syncthreads();
   for (int e = e0; e < e1; ++e) key[e] = rek[e - e0];  // term id -> u (same order)
   __syncthreads();
-  // wave w of this block writes list w: one entry per (u, w) group (at most 4 queries each)
-  int run = 0;
+  // wave w of this block writes the lists of slots 4 w + i: its queries' terms, ascending u
+  int run[kQW] = {0, 0, 0, 0};
   for (int c0 = 0; c0 < n2; c0 += 64) {
     const int e = c0 + lane;
     const uint32_t k = e < n2 ? key[e] : 0xffffffffu;  // LDS past n2 was never written
-    const bool mine = k != 0xffffffffu && (int)((k >> 2) & 15u) == wave;
-    const bool head = mine && (e == 0 || (key[e - 1] >> 2) != (k >> 2));
-    const unsigned long long hb = __ballot(head);
-    if (head) {
-      const int idx = run + __popcll(hb & ((1ull << lane) - 1ull));
-      int m = 0;
-      float w4[kQW] = {0.f, 0.f, 0.f, 0.f};
-      for (int x = e; x < n2 && x < e + kQW; ++x) {
-        const uint32_t kx = key[x];
-        if (kx == 0xffffffffu || (kx >> 2) != (k >> 2)) break;
-        m |= 1 << (kx & 3u);
-        w4[kx & 3u] = val[x];
-      }
-      TermMeta tm;
-      tm.u = (int32_t)(k >> 6);
-      tm.off = (tm.u % kU) * 64 * 4;
-      tm.m = m;
 #pragma unroll
-      for (int i = 0; i < kQW; ++i) tm.w[i] = w4[i];
-      tm.pad = 0;
-      wl[wave * kWaveTerms + idx] = tm;
+    for (int i = 0; i < kQW; ++i) {
+      const int slot = wave * kQW + i;
+      const bool mine = k != 0xffffffffu && (int)(k & 63u) == slot;
+      const unsigned long long mb = __ballot(mine);
+      if (mine) {
+        const int idx = run[i] + __popcll(mb & ((1ull << lane) - 1ull));
+        const int32_t u = (int32_t)(k >> 6);
+        ql[slot * kMaxTerms + idx] = QTerm{(u % kU) * kTile * 4, val[e]};
+        qu[slot * kMaxTerms + idx] = u;
+      }
+      run[i] += __popcll(mb);
     }
-    run += __popcll(hb);
   }
-  if (lane == 0) wl_count[wave] = run;
+  if (lane < kQW)
+    qcount[wave * kQW + lane] = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
 }
 
 // ------------------------------------------------------------------------- scan
@@ -422,28 +410,29 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
   return make_int2(c, prow[c]);
 }
 
-// Workgroup = one row range; steps = (64-row tile, segment of 256 pass terms). Staging: term
+// Workgroup = one row range; steps = (128-row tile, segment of kU pass terms). Staging: term
 // u_local of the segment is held by wave u_local & 15 (lane slot u_local >> 4), which keeps its
-// cursor, loads the term's next 64 postings (lane-reversed: posting c+p in lane 63-p), keeps the
-// prefix inside the tile and scatters ~bits(value) to buf[u_local][row - tile start] in LDS
-// (0 = no posting). Compute: wave w walks its own queries' terms of the segment in ascending u,
-// reads buf[u_local][lane] and adds fl32(w * v) into the fp32 accumulator of each owning query
-// (lane = row). Staging of step s+1 is issued before, and written after, the compute of step s
-// (double-buffered LDS, one barrier per step). kCollect = false: per-range candidate lists;
-// kCollect = true: every row scoring >= thr.
+// cursor, loads the term's next 64 postings (lane-reversed: posting c+p in lane 63-p) and, when
+// the tile can hold more, the 64 after them, keeps the prefix inside the tile and scatters
+// ~bits(value) to buf[u_local][row - tile start] in LDS (0 = no posting). Compute: lane l owns
+// rows 2l and 2l+1 of the tile; wave w walks each of its 4 queries' terms of the segment in
+// ascending u, reads the row pair buf[u_local][2l..2l+1] and adds fl32(w * v) into the query's
+// pair of fp32 accumulators (one packed multiply, one packed add). Staging of step s+1 is issued
+// before, and written after, the compute of step s (double-buffered LDS, one barrier per step).
+// kCollect = false: per-range candidate lists; kCollect = true: every row scoring >= thr.
 template <bool kCollect>
 __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const int32_t* __restrict__ term_ptr, const int32_t* __restrict__ prow,
     const float* __restrict__ pval, const int32_t* __restrict__ long_of,
     const int32_t* __restrict__ start_tab, int64_t n_rows, int64_t range_rows, int n_ranges,
     const uint64_t* __restrict__ row_mask, int nq, const int32_t* __restrict__ uterm,
-    const int32_t* __restrict__ n_terms, const TermMeta* __restrict__ wl,
-    const int32_t* __restrict__ wl_count, const int32_t* __restrict__ qof,
-    int2* __restrict__ cursors,
+    const int32_t* __restrict__ n_terms, const QTerm* __restrict__ ql,
+    const int32_t* __restrict__ qu, const int32_t* __restrict__ qcount,
+    const int32_t* __restrict__ qof, int2* __restrict__ cursors,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
     int32_t* __restrict__ coll_row, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][64]
+  extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][kTile]
   const int g = blockIdx.x;
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
@@ -466,12 +455,10 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   const int nSeg = (nU + kU - 1) / kU;
   const int64_t lo = (int64_t)g * range_rows;
   const int64_t hi = min(lo + range_rows, n_rows);
-  const int n_tiles = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
-  const int n_w = has_q ? wl_count[wave] : 0;
-  const TermMeta* my = wl + wave * kWaveTerms;
+  const int n_tiles = hi > lo ? (int)((hi - lo + kTile - 1) / kTile) : 0;
   int2* gcur = cursors + (size_t)g * kMaxU;
 
-  // cursors of the held terms: segments < kRegSegs in lane 16*seg + slot, the rest in memory
+  // cursors of the held terms: segments < kRegSegs in lane 8*seg + slot, the rest in memory
   int2 creg = make_int2(0, kEndRow);
   {
     const int s = lane / kHold, u = s * kU + (lane % kHold) * kWaves + wave;
@@ -484,8 +471,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       gcur[u] = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, prow);
   }
 
-  // per lane (= row within the tile) and query: the two best rows seen in this lane, plus the
-  // best score dropped from the lane
+  // per lane (= row pair within the tile) and query: the two best rows seen in this lane, plus
+  // the best score dropped from the lane
   float l1s[kQW], l2s[kQW], disc[kQW];
   int32_t l1r[kQW], l2r[kQW];
 #pragma unroll
@@ -496,13 +483,21 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     l1r[i] = kEndRow;
     l2r[i] = kEndRow;
   }
-  f2 acc01 = f2{0.f, 0.f}, acc23 = f2{0.f, 0.f};
+  f2 acc[kQW];
+  uint32_t hx[kQW], hy[kQW];  // OR of the staged value bits seen per row: != 0 <=> a shared term
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    acc[i] = f2{0.f, 0.f};
+    hx[i] = 0u;
+    hy[i] = 0u;
+  }
 
-  int32_t srow[kHold];
-  float sval[kHold];
-  uint32_t amask = 0, hmask = 0;
+  int32_t srow0[kHold], srow1[kHold];
+  float sval0[kHold], sval1[kHold];
+  uint32_t amask = 0, bmask = 0, hmask = 0;
+  uint32_t zb0 = 0, zb1 = 0;  // held slots whose row image in buffer 0 / 1 is all zero
   int2 scv = make_int2(0, kEndRow);
-  auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * 64, hi); };
+  auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * kTile, hi); };
   auto issue = [&](int s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
     const int32_t thi = tile_hi(tile);
@@ -514,41 +509,64 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     if (seg >= kRegSegs) cv = mine ? gcur[u] : make_int2(0, kEndRow);
     hmask = (uint32_t)(__ballot(mine) >> base) & ((1u << kHold) - 1u);
     amask = (uint32_t)(__ballot(mine && cv.y < thi) >> base) & ((1u << kHold) - 1u);
-    if (dbg & 2) amask = 0;
+    // posting c + 64 lies at row >= cv.y + 64: the second load can reach the tile only if
+    // cv.y < thi - 64
+    bmask = (uint32_t)(__ballot(mine && cv.y < thi - 64) >> base) & ((1u << kHold) - 1u);
+    if (dbg & 2) amask = bmask = 0;
     scv = cv;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       if ((amask >> k) & 1u) {
         const int c = rl_i(cv.x, base + k);
-        srow[k] = prow[c + 63 - lane];  // posting c + p sits in lane 63 - p
-        sval[k] = pval[c + 63 - lane];
+        srow0[k] = prow[c + 63 - lane];  // posting c + p sits in lane 63 - p
+        sval0[k] = pval[c + 63 - lane];
+        if ((bmask >> k) & 1u) {
+          srow1[k] = prow[c + 127 - lane];  // posting c + 64 + p in lane 63 - p
+          sval1[k] = pval[c + 127 - lane];
+        }
       }
     }
   };
   auto finish = [&](int s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
-    const int32_t tlo = (int32_t)(lo + (int64_t)tile * 64);
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
     const int32_t thi = tile_hi(tile);
     const int base = seg < kRegSegs ? seg * kHold : 0;
-    uint32_t* buf = sbuf + (size_t)(s & 1) * kU * 64;
+    uint32_t* buf = sbuf + (size_t)(s & 1) * kU * kTile;
+    uint32_t zb = (s & 1) ? zb1 : zb0;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
-      uint32_t* row = buf + (k * kWaves + wave) * 64;
+      uint32_t* row = buf + (k * kWaves + wave) * kTile;
       if ((amask >> k) & 1u) {
-        const unsigned long long outb = ~__ballot(srow[k] < thi);
-        const int n_in = outb == 0 ? 64 : __builtin_clzll(outb);  // postings inside the tile
-        const int32_t nr = n_in < 64 ? rl_i(srow[k], 63 - n_in) : thi;
+        const unsigned long long out0 = ~__ballot(srow0[k] < thi);
+        const int n0 = out0 == 0 ? 64 : __builtin_clzll(out0);  // postings inside the tile
+        int n1 = 0;
+        int32_t nr = thi;  // next posting's row, or a lower bound of it
+        if (n0 < 64) {
+          nr = rl_i(srow0[k], 63 - n0);
+        } else if ((bmask >> k) & 1u) {
+          const unsigned long long out1 = ~__ballot(srow1[k] < thi);
+          n1 = out1 == 0 ? 64 : __builtin_clzll(out1);
+          if (n1 < 64) nr = rl_i(srow1[k], 63 - n1);
+        }
         if (lane == base + k) {
-          scv.x += n_in;
+          scv.x += n0 + n1;
           scv.y = nr;
         }
-        row[lane] = 0u;
+        if (n0 + n1 < kTile) reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
         // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
-        if (lane >= 64 - n_in) row[srow[k] - tlo] = __float_as_uint(sval[k]);
-      } else if ((hmask >> k) & 1u) {
-        row[lane] = 0u;  // held but idle this step: an all-miss row
+        if (lane >= 64 - n0) row[srow0[k] - tlo] = __float_as_uint(sval0[k]);
+        if (lane >= 64 - n1) row[srow1[k] - tlo] = __float_as_uint(sval1[k]);
+        zb &= ~(1u << k);
+      } else if (((hmask & ~zb) >> k) & 1u) {
+        reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);  // held, idle: all-miss row
+        zb |= 1u << k;
       }
     }
+    if (s & 1)
+      zb1 = zb;
+    else
+      zb0 = zb;
     if (seg < kRegSegs) {
       creg = scv;
     } else {
@@ -556,89 +574,106 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       if (lane < kHold && u < nU) gcur[u] = scv;
     }
   };
-  // seg_first (lane s) / seg_first2 (lane s - 64): first list index whose term lies in segment
-  // s or later (a pass has at most kMaxU / kU = 128 segments)
+  // qf[i] (lane s) / qf2[i] (lane s - 64): first entry of query slot i's list whose term lies in
+  // segment s or later (a pass has at most kMaxU / kU = 128 segments)
   static_assert(kMaxU / kU <= 128, "two lane slots per segment boundary");
-  auto lower_seg = [&](int sg) {
-    int a0 = 0, n = n_w;
-    while (n > 0) {
-      const int h = n >> 1;
-      if (my[a0 + h].u < sg * kU) {
-        a0 += h + 1;
-        n -= h + 1;
-      } else {
-        n = h;
+  int qn[kQW], qf[kQW], qf2[kQW];
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    const int slot = wave * kQW + i;
+    qn[i] = qw[i] >= 0 ? qcount[slot] : 0;
+    const int32_t* U = qu + slot * kMaxTerms;
+    auto lower_seg = [&](int sg) {
+      int a0 = 0, n = qn[i];
+      while (n > 0) {
+        const int h = n >> 1;
+        if (U[a0 + h] < sg * kU) {
+          a0 += h + 1;
+          n -= h + 1;
+        } else {
+          n = h;
+        }
       }
-    }
-    return a0;
-  };
-  const int seg_first = lane <= nSeg ? lower_seg(lane) : n_w;
-  const int seg_first2 = lane + 64 <= nSeg ? lower_seg(lane + 64) : n_w;
-  auto first_of = [&](int sg) {  // sg is wave-uniform
-    return sg >= nSeg ? n_w : (sg < 64 ? rl_i(seg_first, sg) : rl_i(seg_first2, sg - 64));
-  };
-  // bit i: this lane's row got a posting of one of query i's terms in the current tile
-  uint32_t hb = 0;
-  auto compute = [&](int s) {
-    const int tile = s / nSeg, seg = s - tile * nSeg;
-    (void)tile;
-    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)(s & 1) * kU * 64 + lane);
-    const int j0 = first_of(seg);
-    const int j1 = first_of(seg + 1);
-    // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; an
-    // absent query weight is 0 and adding fl32(0 * v) = +-0 leaves an fp32 sum unchanged, so
-    // every term updates all four accumulators without branches
-    auto term = [&](const TermMeta& tm, uint32_t rv) {
-      const float v = __uint_as_float(rv);
-      hb |= rv != 0u ? (uint32_t)tm.m : 0u;
-      const f2 vv = f2{v, v};
-      acc01 = acc01 + f2{tm.w[0], tm.w[1]} * vv;
-      acc23 = acc23 + f2{tm.w[2], tm.w[3]} * vv;
+      return a0;
     };
-    int j = j0;
-    for (; j + kBatch <= j1; j += kBatch) {
-      TermMeta tm[kBatch];
-      uint32_t rv[kBatch];
-#pragma unroll
-      for (int k = 0; k < kBatch; ++k) tm[k] = my[j + k];  // uniform: scalar loads
-#pragma unroll
-      for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint32_t*>(buf + tm[k].off);
-#pragma unroll
-      for (int k = 0; k < kBatch; ++k) term(tm[k], rv[k]);
-    }
-    for (; j < j1; ++j) {
-      const TermMeta tm = my[j];
-      term(tm, *reinterpret_cast<const uint32_t*>(buf + tm.off));
-    }
+    qf[i] = lane <= nSeg ? lower_seg(lane) : qn[i];
+    qf2[i] = lane + 64 <= nSeg ? lower_seg(lane + 64) : qn[i];
+  }
+  auto first_of = [&](int i, int sg) {  // sg is wave-uniform
+    return sg >= nSeg ? qn[i] : (sg < 64 ? rl_i(qf[i], sg) : rl_i(qf2[i], sg - 64));
   };
-  auto candidates = [&](int tile, uint64_t mrow) {
-    const int32_t tlo = (int32_t)(lo + (int64_t)tile * 64);
-    const int32_t thi = tile_hi(tile);
-    const bool ok = ((mrow >> lane) & 1ull) && (tlo + lane < thi);
+  auto compute = [&](int s) {
+    const int seg = s % nSeg;
+    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)(s & 1) * kU * kTile) + lane * 8;
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
-      const bool cand = ok && ((hb >> i) & 1u);
-      const float sc = i == 0 ? acc01.x : i == 1 ? acc01.y : i == 2 ? acc23.x : acc23.y;
-      if constexpr (kCollect) {
-        const int q = qw[i];
-        if (cand && sc >= tq[i]) {
-          const int slot = atomicAdd(&coll_count[q], 1);
-          if (slot < kCollectCap) {
-            coll_key[(size_t)q * kCollectCap + slot] = sc;
-            coll_row[(size_t)q * kCollectCap + slot] = tlo + lane;
-          }
+      const QTerm* L = ql + (wave * kQW + i) * kMaxTerms;
+      const int j1 = first_of(i, seg + 1);
+      int j = first_of(i, seg);
+      f2 a = acc[i];
+      uint32_t x = hx[i], y = hy[i];
+      // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; a
+      // row without a posting adds fl32(w * 0) = +-0, which leaves an fp32 sum unchanged
+      for (; j + kBatch <= j1; j += kBatch) {
+        QTerm tm[kBatch];
+        uint2 rv[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) tm[k] = L[j + k];  // uniform: one scalar load
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint2*>(buf + tm[k].off);
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+          a = a + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
+          x |= rv[k].x;
+          y |= rv[k].y;
         }
-      } else {
-        // rows reach a lane in ascending order, so strict > keeps equal keys in row order
-        const float x = cand ? sc : kNegInf;
-        const int32_t r = tlo + lane;
-        const bool c1 = x > l1s[i];
-        const bool c2 = x > l2s[i];
-        disc[i] = fmaxf(disc[i], c2 ? l2s[i] : x);
-        l2s[i] = c1 ? l1s[i] : (c2 ? x : l2s[i]);
-        l2r[i] = c1 ? l1r[i] : (c2 ? r : l2r[i]);
-        l1s[i] = c1 ? x : l1s[i];
-        l1r[i] = c1 ? r : l1r[i];
+      }
+      for (; j < j1; ++j) {
+        const QTerm tm = L[j];
+        const uint2 rv = *reinterpret_cast<const uint2*>(buf + tm.off);
+        a = a + f2{tm.w, tm.w} * f2{__uint_as_float(rv.x), __uint_as_float(rv.y)};
+        x |= rv.x;
+        y |= rv.y;
+      }
+      acc[i] = a;
+      hx[i] = x;
+      hy[i] = y;
+    }
+  };
+  auto candidates = [&](int tile, uint64_t m0, uint64_t m1) {
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
+    const int32_t thi = tile_hi(tile);
+    const int32_t r0 = tlo + 2 * lane;
+    const uint64_t mw = lane < 32 ? m0 : m1;
+    const bool ok0 = ((mw >> ((2 * lane) & 63)) & 1ull) && r0 < thi;
+    const bool ok1 = ((mw >> ((2 * lane + 1) & 63)) & 1ull) && r0 + 1 < thi;
+#pragma unroll
+    for (int i = 0; i < kQW; ++i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // the lane's two rows, ascending
+        const bool cand = h == 0 ? (ok0 && hx[i] != 0u) : (ok1 && hy[i] != 0u);
+        const float sc = h == 0 ? acc[i].x : acc[i].y;
+        const int32_t r = r0 + h;
+        if constexpr (kCollect) {
+          const int q = qw[i];
+          if (cand && sc >= tq[i]) {
+            const int slot = atomicAdd(&coll_count[q], 1);
+            if (slot < kCollectCap) {
+              coll_key[(size_t)q * kCollectCap + slot] = sc;
+              coll_row[(size_t)q * kCollectCap + slot] = r;
+            }
+          }
+        } else {
+          // rows reach a lane in ascending order, so strict > keeps equal keys in row order
+          const float x = cand ? sc : kNegInf;
+          const bool c1 = x > l1s[i];
+          const bool c2 = x > l2s[i];
+          disc[i] = fmaxf(disc[i], c2 ? l2s[i] : x);
+          l2s[i] = c1 ? l1s[i] : (c2 ? x : l2s[i]);
+          l2r[i] = c1 ? l1r[i] : (c2 ? r : l2r[i]);
+          l1s[i] = c1 ? x : l1s[i];
+          l1r[i] = c1 ? r : l1r[i];
+        }
       }
     }
   };
@@ -659,22 +694,31 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   ARMI_PROF_ADD(5, t_a, t_b);
   for (int s = 0; s < S; ++s) {
     const int tile = s / nSeg, seg = s - tile * nSeg;
-    // loaded now, used after this step's compute
-    const uint64_t mrow = (row_mask && seg == nSeg - 1) ? row_mask[(lo >> 6) + tile] : ~0ull;
+    // loaded now, used after this step's compute; lo is a multiple of 64, so the tile's rows
+    // are the bits of words tlo / 64 and tlo / 64 + 1
+    uint64_t m0 = ~0ull, m1 = ~0ull;
+    if (row_mask && seg == nSeg - 1) {
+      const int64_t tlo = lo + (int64_t)tile * kTile;
+      m0 = row_mask[tlo >> 6];
+      m1 = tlo + 64 < hi ? row_mask[(tlo >> 6) + 1] : 0ull;
+    }
     ARMI_PROF_T(t_a);
     if (s + 1 < S) issue(s + 1);
     ARMI_PROF_T(t_b);
     ARMI_PROF_ADD(0, t_a, t_b);
     if (has_q) {
       if (seg == 0) {
-        acc01 = f2{0.f, 0.f};
-        acc23 = f2{0.f, 0.f};
-        hb = 0;
+#pragma unroll
+        for (int i = 0; i < kQW; ++i) {
+          acc[i] = f2{0.f, 0.f};
+          hx[i] = 0u;
+          hy[i] = 0u;
+        }
       }
       if (!(dbg & 1)) compute(s);
       ARMI_PROF_T(t_a);
       ARMI_PROF_ADD(1, t_b, t_a);
-      if (seg == nSeg - 1) candidates(tile, mrow);
+      if (seg == nSeg - 1) candidates(tile, m0, m1);
       ARMI_PROF_T(t_b);
       ARMI_PROF_ADD(2, t_a, t_b);
     }
@@ -689,7 +733,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   if ((dbg & 8) && lane == 0) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) g_sparse_prof[((size_t)g * kWaves + wave) * 8 + i] = tp[i];
-    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 6] = n_w;
+    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 6] = qn[0] + qn[1] + qn[2] + qn[3];
     g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 7] = S;
   }
 #endif
@@ -879,8 +923,9 @@ __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
 struct Workspace {
   int32_t* uterm;
   int32_t* n_terms;
-  TermMeta* wl;
-  int32_t* wl_count;
+  QTerm* ql;
+  int32_t* qu;
+  int32_t* qcount;
   int32_t* qof;
   int2* cursors;
   float* cand_key;
@@ -899,8 +944,9 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   const size_t nr = (size_t)std::max(idx->n_ranges, 1);
   w.uterm = cv.take<int32_t>(kMaxU);
   w.n_terms = cv.take<int32_t>(1);
-  w.wl = cv.take<TermMeta>((size_t)kWaves * kWaveTerms);
-  w.wl_count = cv.take<int32_t>(kWaves);
+  w.ql = cv.take<QTerm>((size_t)kQB * kMaxTerms);
+  w.qu = cv.take<int32_t>((size_t)kQB * kMaxTerms);
+  w.qcount = cv.take<int32_t>(kQB);
   w.qof = cv.take<int32_t>(kQB);
   w.cursors = cv.take<int2>(nr * kMaxU);
   w.cand_key = cv.take<float>(nr * kQB * kKW);
@@ -1119,14 +1165,14 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     }
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
     pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
-        q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.wl,
-        w.wl_count, w.qof, pflags);
+        q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
+        w.qcount, w.qof, pflags);
     ARMI_LAUNCHED("pass_terms_kernel");
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
-        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
     if (int rc = tl.end()) return rc;
@@ -1158,7 +1204,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     ARMI_LAUNCHED("sparse_merge_kernel");
     sparse_scan_kernel<true><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
-        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.wl, w.wl_count, w.qof,
+        idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp), dim3(256), lds_collect, stream>>>(
