@@ -51,12 +51,14 @@ constexpr int kLongTerm = 256;          // postings from which a term gets a ran
 constexpr int kPad = 128;               // sentinel slots past the last list (two 64-posting loads)
 constexpr int kBatch = 4;               // terms whose LDS reads are in flight together
 constexpr int kTile = 128;              // rows per scan step: two adjacent rows per lane
+constexpr int kQStride = kMaxTerms + 2 * kBatch;  // list entries per query slot (+ padding)
 constexpr int kMaxRanges = 256;
 constexpr int kMaxU = kQB * kMaxTerms;  // distinct terms of one pass, at most
 constexpr int kU = 128;                 // terms per staging segment
 constexpr int kHold = kU / kWaves;      // terms of a segment staged by one wave
 constexpr int kRegSegs = 64 / kHold;    // segments whose cursors stay in registers
-constexpr size_t kScanLds = (size_t)2 * kU * kTile * 4;  // double-buffered staging, 128 KB
+// two staging buffers, the all-zero row and the 64-entry scratch row of out-of-tile scatters
+constexpr size_t kScanLds = (size_t)(2 * kU + 1) * kTile * 4 + 64 * 4;
 constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + weights, 128 KB
 constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
@@ -171,11 +173,12 @@ __global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz
 
 // ------------------------------------------------------------------------- per-pass prep
 
-// One entry of a query's term list: byte offset of the term's staging row within a segment buffer
-// ((u % kU) * kTile * 4) and the query's weight. 8 B: a batch of 4 entries is one 32-B scalar load.
+// One entry of a query's term list: the query's weight and the byte offset of the term's staging
+// row within a segment buffer ((u % kU) * kTile * 4). 8 B: a batch of 4 entries is one 32-B scalar
+// load, and the weight in the even register of each pair feeds the packed multiply directly.
 struct alignas(8) QTerm {
-  int32_t off;
   float w;
+  int32_t off;
 };
 
 // One block for the pass. Sorts the pass's (term, query) pairs by (term, slot) where query q sits
@@ -353,12 +356,16 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
       if (mine) {
         const int idx = run[i] + __popcll(mb & ((1ull << lane) - 1ull));
         const int32_t u = (int32_t)(k >> 6);
-        ql[slot * kMaxTerms + idx] = QTerm{(u % kU) * kTile * 4, val[e]};
-        qu[slot * kMaxTerms + idx] = u;
+        ql[slot * kQStride + idx] = QTerm{val[e], (u % kU) * kTile * 4};
+        qu[slot * kQStride + idx] = u;
       }
       run[i] += __popcll(mb);
     }
   }
+  // a batch of the scan may read up to kBatch - 1 entries past a list: finite weights there
+#pragma unroll
+  for (int i = 0; i < kQW; ++i)
+    if (lane < kBatch) ql[(wave * kQW + i) * kQStride + run[i] + lane] = QTerm{0.f, 0};
   if (lane < kQW)
     qcount[wave * kQW + lane] = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
 }
@@ -381,6 +388,12 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ float rl_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_or3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
 // first posting of term t at or after row `lo` (range g), with its row
@@ -494,12 +507,13 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 
   int32_t srow0[kHold], srow1[kHold];
   float sval0[kHold], sval1[kHold];
-  uint32_t amask = 0, bmask = 0, hmask = 0;
-  uint32_t zb0 = 0, zb1 = 0;  // held slots whose row image in buffer 0 / 1 is all zero
+  uint32_t amask = 0, bmask = 0;
   int2 scv = make_int2(0, kEndRow);
+  const int rev = 63 - lane;  // posting c + p sits in lane 63 - p
+  // scatter target of a lane whose posting is outside the tile: a 64-entry scratch row
+  uint32_t* const trash = sbuf + (size_t)(2 * kU + 1) * kTile + lane;
   auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * kTile, hi); };
-  auto issue = [&](int s) {
-    const int tile = s / nSeg, seg = s - tile * nSeg;
+  auto issue = [&](int tile, int seg) {
     const int32_t thi = tile_hi(tile);
     const int base = seg < kRegSegs ? seg * kHold : 0;
     int2 cv = creg;
@@ -507,7 +521,6 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const int u = seg * kU + l * kWaves + wave;
     const bool mine = l >= 0 && l < kHold && u < nU;
     if (seg >= kRegSegs) cv = mine ? gcur[u] : make_int2(0, kEndRow);
-    hmask = (uint32_t)(__ballot(mine) >> base) & ((1u << kHold) - 1u);
     amask = (uint32_t)(__ballot(mine && cv.y < thi) >> base) & ((1u << kHold) - 1u);
     // posting c + 64 lies at row >= cv.y + 64: the second load can reach the tile only if
     // cv.y < thi - 64
@@ -518,55 +531,50 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     for (int k = 0; k < kHold; ++k) {
       if ((amask >> k) & 1u) {
         const int c = rl_i(cv.x, base + k);
-        srow0[k] = prow[c + 63 - lane];  // posting c + p sits in lane 63 - p
-        sval0[k] = pval[c + 63 - lane];
+        const int32_t* pr = prow + c;
+        const float* pv = pval + c;
+        srow0[k] = pr[rev];
+        sval0[k] = pv[rev];
         if ((bmask >> k) & 1u) {
-          srow1[k] = prow[c + 127 - lane];  // posting c + 64 + p in lane 63 - p
-          sval1[k] = pval[c + 127 - lane];
+          srow1[k] = pr[64 + rev];  // posting c + 64 + p in lane 63 - p
+          sval1[k] = pv[64 + rev];
         }
       }
     }
   };
-  auto finish = [&](int s) {
-    const int tile = s / nSeg, seg = s - tile * nSeg;
+  // Every held row image is cleared, then the postings inside the tile are scattered into it
+  // (lanes whose posting lies outside write the scratch row instead: no exec-mask branches).
+  auto finish = [&](int tile, int seg, int par) {
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
     const int32_t thi = tile_hi(tile);
     const int base = seg < kRegSegs ? seg * kHold : 0;
-    uint32_t* buf = sbuf + (size_t)(s & 1) * kU * kTile;
-    uint32_t zb = (s & 1) ? zb1 : zb0;
+    uint32_t* buf = sbuf + (size_t)par * kU * kTile;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       uint32_t* row = buf + (k * kWaves + wave) * kTile;
-      if ((amask >> k) & 1u) {
-        const unsigned long long out0 = ~__ballot(srow0[k] < thi);
-        const int n0 = out0 == 0 ? 64 : __builtin_clzll(out0);  // postings inside the tile
-        int n1 = 0;
-        int32_t nr = thi;  // next posting's row, or a lower bound of it
-        if (n0 < 64) {
-          nr = rl_i(srow0[k], 63 - n0);
-        } else if ((bmask >> k) & 1u) {
-          const unsigned long long out1 = ~__ballot(srow1[k] < thi);
-          n1 = out1 == 0 ? 64 : __builtin_clzll(out1);
-          if (n1 < 64) nr = rl_i(srow1[k], 63 - n1);
-        }
-        if (lane == base + k) {
-          scv.x += n0 + n1;
-          scv.y = nr;
-        }
-        if (n0 + n1 < kTile) reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
-        // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
-        if (lane >= 64 - n0) row[srow0[k] - tlo] = __float_as_uint(sval0[k]);
-        if (lane >= 64 - n1) row[srow1[k] - tlo] = __float_as_uint(sval1[k]);
-        zb &= ~(1u << k);
-      } else if (((hmask & ~zb) >> k) & 1u) {
-        reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);  // held, idle: all-miss row
-        zb |= 1u << k;
+      reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
+      const bool act = (amask >> k) & 1u;
+      const bool two = (bmask >> k) & 1u;
+      // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
+      const uint64_t in0 = act ? __ballot(srow0[k] < thi) : 0ull;
+      const int n0 = in0 == ~0ull ? 64 : __builtin_clzll(~in0);  // postings inside the tile
+      const uint64_t in1 = (two && n0 == 64) ? __ballot(srow1[k] < thi) : 0ull;
+      const int n1 = in1 == ~0ull ? 64 : __builtin_clzll(~in1);
+      uint32_t* d0 = lane >= 64 - n0 ? row + (srow0[k] - tlo) : trash;
+      *d0 = __float_as_uint(sval0[k]);
+      if (two) {
+        uint32_t* d1 = lane >= 64 - n1 ? row + (srow1[k] - tlo) : trash;
+        *d1 = __float_as_uint(sval1[k]);
+      }
+      if (act) {
+        // next posting's row, or a lower bound of it
+        const int32_t r0 = rl_i(srow0[k], (63 - n0) & 63), r1 = rl_i(srow1[k], (63 - n1) & 63);
+        const int32_t nr = n0 < 64 ? r0 : (two && n1 < 64 ? r1 : thi);
+        const bool me = lane == base + k;
+        scv.x = me ? scv.x + n0 + n1 : scv.x;
+        scv.y = me ? nr : scv.y;
       }
     }
-    if (s & 1)
-      zb1 = zb;
-    else
-      zb0 = zb;
     if (seg < kRegSegs) {
       creg = scv;
     } else {
@@ -582,7 +590,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   for (int i = 0; i < kQW; ++i) {
     const int slot = wave * kQW + i;
     qn[i] = qw[i] >= 0 ? qcount[slot] : 0;
-    const int32_t* U = qu + slot * kMaxTerms;
+    const int32_t* U = qu + slot * kQStride;
     auto lower_seg = [&](int sg) {
       int a0 = 0, n = qn[i];
       while (n > 0) {
@@ -602,42 +610,43 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   auto first_of = [&](int i, int sg) {  // sg is wave-uniform
     return sg >= nSeg ? qn[i] : (sg < 64 ? rl_i(qf[i], sg) : rl_i(qf2[i], sg - 64));
   };
-  auto compute = [&](int s) {
-    const int seg = s % nSeg;
-    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)(s & 1) * kU * kTile) + lane * 8;
+  auto compute = [&](int seg, int par) {
+    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)par * kU * kTile) + lane * 8;
+    const int zoff = (2 - par) * kU * kTile * 4;  // the all-zero row, relative to buf
+    // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; a row
+    // without a posting adds fl32(w * 0) = +-0, which leaves an fp32 sum unchanged. Batches of
+    // 4 entries; entries past the segment's end (the next segment's, or the zero padding after
+    // the list: finite weights) read the all-zero row, so they add +-0 as well.
+    auto batch = [&](const QTerm* tm, int tail, f2& a, uint32_t& x, uint32_t& y) {
+      uint2 rv[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k)
+        rv[k] = *reinterpret_cast<const uint2*>(buf + (k < tail ? tm[k].off : zoff));
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k)
+        a = a + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
+      x = or3(x, rv[0].x, rv[1].x);
+      x = or3(x, rv[2].x, rv[3].x);
+      y = or3(y, rv[0].y, rv[1].y);
+      y = or3(y, rv[2].y, rv[3].y);
+    };
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
-      const QTerm* L = ql + (wave * kQW + i) * kMaxTerms;
+      const QTerm* L = ql + (wave * kQW + i) * kQStride;
       const int j1 = first_of(i, seg + 1);
       int j = first_of(i, seg);
-      f2 a = acc[i];
-      uint32_t x = hx[i], y = hy[i];
-      // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; a
-      // row without a posting adds fl32(w * 0) = +-0, which leaves an fp32 sum unchanged
       for (; j + kBatch <= j1; j += kBatch) {
         QTerm tm[kBatch];
-        uint2 rv[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) tm[k] = L[j + k];  // uniform: one scalar load
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint2*>(buf + tm[k].off);
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-          a = a + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
-          x |= rv[k].x;
-          y |= rv[k].y;
-        }
+        batch(tm, kBatch, acc[i], hx[i], hy[i]);  // every entry inside the segment
       }
-      for (; j < j1; ++j) {
-        const QTerm tm = L[j];
-        const uint2 rv = *reinterpret_cast<const uint2*>(buf + tm.off);
-        a = a + f2{tm.w, tm.w} * f2{__uint_as_float(rv.x), __uint_as_float(rv.y)};
-        x |= rv.x;
-        y |= rv.y;
+      if (j < j1) {
+        QTerm tm[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) tm[k] = L[j + k];
+        batch(tm, j1 - j, acc[i], hx[i], hy[i]);
       }
-      acc[i] = a;
-      hx[i] = x;
-      hy[i] = y;
     }
   };
   auto candidates = [&](int tile, uint64_t m0, uint64_t m1) {
@@ -678,6 +687,9 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     }
   };
 
+  // the all-zero row after the two staging buffers (read by the padding entries of a batch)
+  if (threadIdx.x < kTile / 2)
+    reinterpret_cast<uint2*>(sbuf + (size_t)2 * kU * kTile)[threadIdx.x] = make_uint2(0u, 0u);
   const int S = n_tiles * nSeg;
   unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long t_a = 0, t_b = 0;
@@ -686,24 +698,27 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   (void)t_b;
   ARMI_PROF_T(t_a);
   if (S > 0) {
-    issue(0);
-    finish(0);
+    issue(0, 0);
+    finish(0, 0, 0);
   }
   __syncthreads();
   ARMI_PROF_T(t_b);
   ARMI_PROF_ADD(5, t_a, t_b);
+  int tile = 0, seg = 0;  // of step s
   for (int s = 0; s < S; ++s) {
-    const int tile = s / nSeg, seg = s - tile * nSeg;
+    const int par = s & 1;
+    const bool last_seg = seg == nSeg - 1;
+    const int tile1 = last_seg ? tile + 1 : tile, seg1 = last_seg ? 0 : seg + 1;  // step s + 1
     // loaded now, used after this step's compute; lo is a multiple of 64, so the tile's rows
     // are the bits of words tlo / 64 and tlo / 64 + 1
     uint64_t m0 = ~0ull, m1 = ~0ull;
-    if (row_mask && seg == nSeg - 1) {
+    if (row_mask && last_seg) {
       const int64_t tlo = lo + (int64_t)tile * kTile;
       m0 = row_mask[tlo >> 6];
       m1 = tlo + 64 < hi ? row_mask[(tlo >> 6) + 1] : 0ull;
     }
     ARMI_PROF_T(t_a);
-    if (s + 1 < S) issue(s + 1);
+    if (s + 1 < S) issue(tile1, seg1);
     ARMI_PROF_T(t_b);
     ARMI_PROF_ADD(0, t_a, t_b);
     if (has_q) {
@@ -715,19 +730,21 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
           hy[i] = 0u;
         }
       }
-      if (!(dbg & 1)) compute(s);
+      if (!(dbg & 1)) compute(seg, par);
       ARMI_PROF_T(t_a);
       ARMI_PROF_ADD(1, t_b, t_a);
-      if (seg == nSeg - 1) candidates(tile, m0, m1);
+      if (last_seg) candidates(tile, m0, m1);
       ARMI_PROF_T(t_b);
       ARMI_PROF_ADD(2, t_a, t_b);
     }
-    if (s + 1 < S) finish(s + 1);
+    if (s + 1 < S) finish(tile1, seg1, par ^ 1);
     ARMI_PROF_T(t_a);
     ARMI_PROF_ADD(3, t_b, t_a);
     if (!(dbg & 4)) __syncthreads();
     ARMI_PROF_T(t_b);
     ARMI_PROF_ADD(4, t_a, t_b);
+    tile = tile1;
+    seg = seg1;
   }
 #ifdef ARMI_SPARSE_PROFILE
   if ((dbg & 8) && lane == 0) {
@@ -944,8 +961,8 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   const size_t nr = (size_t)std::max(idx->n_ranges, 1);
   w.uterm = cv.take<int32_t>(kMaxU);
   w.n_terms = cv.take<int32_t>(1);
-  w.ql = cv.take<QTerm>((size_t)kQB * kMaxTerms);
-  w.qu = cv.take<int32_t>((size_t)kQB * kMaxTerms);
+  w.ql = cv.take<QTerm>((size_t)kQB * kQStride);
+  w.qu = cv.take<int32_t>((size_t)kQB * kQStride);
   w.qcount = cv.take<int32_t>(kQB);
   w.qof = cv.take<int32_t>(kQB);
   w.cursors = cv.take<int2>(nr * kMaxU);

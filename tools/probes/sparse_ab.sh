@@ -9,3 +9,5 @@ for i in 1 2; do
   timeout -k 10 400 python bench.py --workload hybrid --steps 50 --warmup 5 --no-cpu-baseline --latency-iters 5 > gpurun_out/${TAG}_hyb$i.log 2>&1 || exit $?
   echo "hybrid: $(tail -1 gpurun_out/${TAG}_hyb$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["roofline_sparse"]; print(round(d["value"]), round(d["ms_per_step"],3), "sparse_ms", round(s["avg_launch_ms"],4), round(s["achieved"]))')"
 done
+timeout -k 10 300 python tools/sparse_bench.py --iters 100 > gpurun_out/${TAG}_sb.log 2>&1 || exit $?
+echo "sparse alone: $(tail -1 gpurun_out/${TAG}_sb.log)"
