@@ -43,8 +43,7 @@ struct armi_sparse_index {
   int64_t n_postings = 0;        // valid postings + one sentinel per term
   int64_t n_long = 0;
   int32_t* term_ptr = nullptr;   // [vocab+1]
-  int32_t* prow = nullptr;       // [n_postings + 64]
-  float* pval = nullptr;         // [n_postings + 64]
+  int32_t* post = nullptr;       // [n_postings + 128][2]: (row, value bits) per posting
   int32_t* long_of = nullptr;    // [vocab] index into start_tab, -1 for short terms
   int32_t* start_tab = nullptr;  // [n_long][n_ranges]
 };

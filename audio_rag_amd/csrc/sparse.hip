@@ -105,36 +105,31 @@ __global__ void term_ptr_kernel(const uint32_t* __restrict__ skeys, int64_t nnz,
 __global__ void postings_kernel(const uint32_t* __restrict__ skeys, const int32_t* __restrict__ sent,
                                 const int32_t* __restrict__ row_of,
                                 const float* __restrict__ values, int64_t nnz, int32_t vocab,
-                                int32_t* __restrict__ prow, float* __restrict__ pval) {
+                                int2* __restrict__ post) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nnz) return;
   const uint32_t t = skeys[i];
   if (t >= (uint32_t)vocab) return;
   const int64_t pos = i + t;
   const int32_t e = sent[i];
-  prow[pos] = row_of[e];
   // a zero value is kept as -0.0: the scan's staging rows use bit pattern 0 for "no posting",
   // and fl32(w * -0.0) added to an fp32 sum changes it exactly as fl32(w * +0.0) does (not at all)
-  const float v = values[e];
-  pval[pos] = __float_as_uint(v) == 0u ? __uint_as_float(0x80000000u) : v;
+  const uint32_t v = __float_as_uint(values[e]);
+  post[pos] = make_int2(row_of[e], (int32_t)(v == 0u ? 0x80000000u : v));
 }
 
 __global__ void sentinels_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
-                                 int64_t n_postings, int32_t* __restrict__ prow,
-                                 float* __restrict__ pval, int32_t* __restrict__ is_long) {
+                                 int64_t n_postings, int2* __restrict__ post,
+                                 int32_t* __restrict__ is_long) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < vocab) {
     const int32_t s = term_ptr[t + 1] - 1;
-    prow[s] = kEndRow;
-    pval[s] = 0.f;
+    post[s] = make_int2(kEndRow, 0);
     is_long[t] = (s - term_ptr[t]) >= kLongTerm ? 1 : 0;
   } else if (t == vocab) {
     is_long[t] = 0;
   }
-  if (t < kPad) {
-    prow[n_postings + t] = kEndRow;
-    pval[n_postings + t] = 0.f;
-  }
+  if (t < kPad) post[n_postings + t] = make_int2(kEndRow, 0);
 }
 
 __global__ void long_of_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
@@ -149,7 +144,7 @@ __global__ void long_of_kernel(const int32_t* __restrict__ term_ptr, int32_t voc
 __global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
                                  const int32_t* __restrict__ term_ptr,
                                  const int32_t* __restrict__ long_of,
-                                 const int32_t* __restrict__ prow, int64_t range_rows,
+                                 const int2* __restrict__ post, int64_t range_rows,
                                  int n_ranges, int32_t* __restrict__ start_tab) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nnz) return;
@@ -161,8 +156,8 @@ __global__ void start_tab_kernel(const uint32_t* __restrict__ skeys, int64_t nnz
   const int32_t first = term_ptr[t];
   const int32_t last = term_ptr[t + 1] - 2;
   const int32_t rel = (int32_t)(pos - first);
-  const int64_t r = prow[pos];
-  const int64_t prev = pos == first ? -1 : (int64_t)prow[pos - 1];
+  const int64_t r = post[pos].x;
+  const int64_t prev = pos == first ? -1 : (int64_t)post[pos - 1].x;
   int32_t* tab = start_tab + (size_t)l * n_ranges;
   const int64_t g_lo = (prev + range_rows) / range_rows;  // ceil((prev + 1) / R)
   const int64_t g_hi = min(r / range_rows, (int64_t)n_ranges - 1);
@@ -401,7 +396,7 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
                                              const int32_t* __restrict__ term_ptr,
                                              const int32_t* __restrict__ long_of,
                                              const int32_t* __restrict__ start_tab,
-                                             const int32_t* __restrict__ prow) {
+                                             const int2* __restrict__ post) {
   const int32_t b = term_ptr[t];
   const int32_t l = long_of[t];
   int32_t c;
@@ -411,7 +406,7 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
     int32_t a = b, n = term_ptr[t + 1] - 1 - b;
     while (n > 0) {
       const int32_t h = n >> 1;
-      if (prow[a + h] < lo) {
+      if (post[a + h].x < lo) {
         a += h + 1;
         n -= h + 1;
       } else {
@@ -420,7 +415,7 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
     }
     c = a;
   }
-  return make_int2(c, prow[c]);
+  return make_int2(c, post[c].x);
 }
 
 // Workgroup = one row range; steps = (128-row tile, segment of kU pass terms). Staging: term
@@ -435,8 +430,8 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
 // kCollect = false: per-range candidate lists; kCollect = true: every row scoring >= thr.
 template <bool kCollect>
 __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
-    const int32_t* __restrict__ term_ptr, const int32_t* __restrict__ prow,
-    const float* __restrict__ pval, const int32_t* __restrict__ long_of,
+    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
+    const int32_t* __restrict__ long_of,
     const int32_t* __restrict__ start_tab, int64_t n_rows, int64_t range_rows, int n_ranges,
     const uint64_t* __restrict__ row_mask, int nq, const int32_t* __restrict__ uterm,
     const int32_t* __restrict__ n_terms, const QTerm* __restrict__ ql,
@@ -476,12 +471,12 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   {
     const int s = lane / kHold, u = s * kU + (lane % kHold) * kWaves + wave;
     if (s < nSeg && u < nU)
-      creg = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, prow);
+      creg = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, post);
   }
   for (int s = kRegSegs; s < nSeg; ++s) {
     const int u = s * kU + lane * kWaves + wave;
     if (lane < kHold && u < nU)
-      gcur[u] = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, prow);
+      gcur[u] = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, post);
   }
 
   // per lane (= row pair within the tile) and query: the two best rows seen in this lane, plus
@@ -505,11 +500,13 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     hy[i] = 0u;
   }
 
-  int32_t srow0[kHold], srow1[kHold];
-  float sval0[kHold], sval1[kHold];
-  uint32_t amask = 0, bmask = 0;
+  // staged postings of the held terms: lane l holds postings c + 2 (63 - l) (.x row, .y value
+  // bits) and c + 2 (63 - l) + 1 (.z, .w) of the term's cursor c: one 16-B load per term
+  typedef int32_t p4 __attribute__((ext_vector_type(4), aligned(8)));
+  p4 sp[kHold];
+  uint32_t amask = 0;
   int2 scv = make_int2(0, kEndRow);
-  const int rev = 63 - lane;  // posting c + p sits in lane 63 - p
+  const int rev2 = 2 * (63 - lane);
   // scatter target of a lane whose posting is outside the tile: a 64-entry scratch row
   uint32_t* const trash = sbuf + (size_t)(2 * kU + 1) * kTile + lane;
   auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * kTile, hi); };
@@ -522,28 +519,21 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const bool mine = l >= 0 && l < kHold && u < nU;
     if (seg >= kRegSegs) cv = mine ? gcur[u] : make_int2(0, kEndRow);
     amask = (uint32_t)(__ballot(mine && cv.y < thi) >> base) & ((1u << kHold) - 1u);
-    // posting c + 64 lies at row >= cv.y + 64: the second load can reach the tile only if
-    // cv.y < thi - 64
-    bmask = (uint32_t)(__ballot(mine && cv.y < thi - 64) >> base) & ((1u << kHold) - 1u);
-    if (dbg & 2) amask = bmask = 0;
+    if (dbg & 2) amask = 0;
     scv = cv;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       if ((amask >> k) & 1u) {
-        const int c = rl_i(cv.x, base + k);
-        const int32_t* pr = prow + c;
-        const float* pv = pval + c;
-        srow0[k] = pr[rev];
-        sval0[k] = pv[rev];
-        if ((bmask >> k) & 1u) {
-          srow1[k] = pr[64 + rev];  // posting c + 64 + p in lane 63 - p
-          sval1[k] = pv[64 + rev];
-        }
+        const int2* pc = post + rl_i(cv.x, base + k);  // uniform
+        sp[k] = *reinterpret_cast<const p4*>(pc + rev2);
       }
     }
   };
   // Every held row image is cleared, then the postings inside the tile are scattered into it
   // (lanes whose posting lies outside write the scratch row instead: no exec-mask branches).
+  // The in-tile postings are a prefix of the 128 loaded (rows ascend to the list's sentinel):
+  // with ne / no the even / odd positions' in-tile prefixes (lane 63 holds positions 0 and 1),
+  // the prefix length is min(2 ne, 2 no + 1).
   auto finish = [&](int tile, int seg, int par) {
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
     const int32_t thi = tile_hi(tile);
@@ -553,25 +543,22 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     for (int k = 0; k < kHold; ++k) {
       uint32_t* row = buf + (k * kWaves + wave) * kTile;
       reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
-      const bool act = (amask >> k) & 1u;
-      const bool two = (bmask >> k) & 1u;
-      // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
-      const uint64_t in0 = act ? __ballot(srow0[k] < thi) : 0ull;
-      const int n0 = in0 == ~0ull ? 64 : __builtin_clzll(~in0);  // postings inside the tile
-      const uint64_t in1 = (two && n0 == 64) ? __ballot(srow1[k] < thi) : 0ull;
-      const int n1 = in1 == ~0ull ? 64 : __builtin_clzll(~in1);
-      uint32_t* d0 = lane >= 64 - n0 ? row + (srow0[k] - tlo) : trash;
-      *d0 = __float_as_uint(sval0[k]);
-      if (two) {
-        uint32_t* d1 = lane >= 64 - n1 ? row + (srow1[k] - tlo) : trash;
-        *d1 = __float_as_uint(sval1[k]);
-      }
-      if (act) {
-        // next posting's row, or a lower bound of it
-        const int32_t r0 = rl_i(srow0[k], (63 - n0) & 63), r1 = rl_i(srow1[k], (63 - n1) & 63);
-        const int32_t nr = n0 < 64 ? r0 : (two && n1 < 64 ? r1 : thi);
+      if ((amask >> k) & 1u) {
+        const uint64_t be = __ballot(sp[k].x < thi), bo = __ballot(sp[k].z < thi);
+        const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
+        const int no = bo == ~0ull ? 64 : __builtin_clzll(~bo);
+        const int n = min(2 * ne, 2 * no + 1);  // postings inside the tile
+        // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
+        uint32_t* d0 = rev2 < n ? row + (sp[k].x - tlo) : trash;
+        uint32_t* d1 = rev2 + 1 < n ? row + (sp[k].z - tlo) : trash;
+        *d0 = (uint32_t)sp[k].y;
+        *d1 = (uint32_t)sp[k].w;
+        // the next posting's row, or a lower bound of it
+        const int nl = (63 - (n >> 1)) & 63;
+        const int32_t re = rl_i(sp[k].x, nl), ro = rl_i(sp[k].z, nl);
+        const int32_t nr = n < kTile ? ((n & 1) ? ro : re) : thi;
         const bool me = lane == base + k;
-        scv.x = me ? scv.x + n0 + n1 : scv.x;
+        scv.x = me ? scv.x + n : scv.x;
         scv.y = me ? nr : scv.y;
       }
     }
@@ -1040,15 +1027,14 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(hipStreamSynchronize(stream));
   idx->n_postings = n_post;
   const size_t cap = (size_t)n_post + kPad;
-  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->prow), cap * 4));
-  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->pval), cap * 4));
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->post), cap * 8));
   if (nnz > 0) {
     postings_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(skeys, sent, row_of, values, nnz, vocab,
-                                                            idx->prow, idx->pval);
+                                                            reinterpret_cast<int2*>(idx->post));
     ARMI_LAUNCHED("postings_kernel");
   }
   sentinels_kernel<<<grid_for(std::max<int64_t>((int64_t)vocab + 1, kPad), 256), 256, 0, stream>>>(
-      idx->term_ptr, vocab, idx->n_postings, idx->prow, idx->pval, is_long);
+      idx->term_ptr, vocab, idx->n_postings, reinterpret_cast<int2*>(idx->post), is_long);
   ARMI_LAUNCHED("sentinels_kernel");
   size_t scan_bytes = 0;
   ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, is_long, scan, vocab + 1, stream));
@@ -1066,7 +1052,8 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->start_tab), tab * 4));
   if (nnz > 0 && n_long > 0 && idx->n_ranges > 0) {
     start_tab_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(skeys, nnz, vocab, idx->term_ptr,
-                                                             idx->long_of, idx->prow,
+                                                             idx->long_of,
+                                                             reinterpret_cast<const int2*>(idx->post),
                                                              idx->range_rows, idx->n_ranges,
                                                              idx->start_tab);
     ARMI_LAUNCHED("start_tab_kernel");
@@ -1077,8 +1064,7 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
 
 void free_index(armi_sparse_index* idx) {
   (void)hipFree(idx->term_ptr);
-  (void)hipFree(idx->prow);
-  (void)hipFree(idx->pval);
+  (void)hipFree(idx->post);
   (void)hipFree(idx->long_of);
   (void)hipFree(idx->start_tab);
   delete idx;
@@ -1188,7 +1174,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
-        idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
+        idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
     ARMI_LAUNCHED("sparse_scan_kernel");
@@ -1220,7 +1206,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         out_scores, out_ids, out_count, pflags, w.kth);
     ARMI_LAUNCHED("sparse_merge_kernel");
     sparse_scan_kernel<true><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
-        idx->term_ptr, idx->prow, idx->pval, idx->long_of, idx->start_tab, idx->n_rows,
+        idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg);
     ARMI_LAUNCHED("sparse_collect_kernel");
