@@ -60,6 +60,9 @@ constexpr int kRegSegs = 64 / kHold;    // segments whose cursors stay in regist
 // two staging buffers, the all-zero row and the 64-entry scratch row of out-of-tile scatters
 constexpr size_t kScanLds = (size_t)(2 * kU + 1) * kTile * 4 + 64 * 4;
 constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + weights, 128 KB
+constexpr int kBitmapVocab = 1 << 18;   // vocabularies up to which a pass numbers its terms by bitmap
+constexpr int kBmWords = kBitmapVocab / 32;
+constexpr size_t kPrepBmLds = (size_t)kBmWords * 8;    // term bitmap + per-word prefix, 64 KB
 constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 constexpr uint32_t kFlagOverflow = 4u;
@@ -176,6 +179,149 @@ struct alignas(8) QTerm {
   int32_t off;
 };
 
+// Wave 0 of a pass_terms block (tid = lane < 64): per-query term counts (first 256 terms;
+// flags[q] = 8 beyond), their exclusive offsets off[0..64], and the query -> slot deal: queries
+// sorted by term count (desc, then index) are dealt to the 16 waves in snake order, so each
+// wave's sum of term counts (its per-tile work) is about the same; slot 4 w + i of wave w.
+__device__ __forceinline__ void deal_queries(const int32_t* __restrict__ q_indptr, int nq, int tid,
+                                             int32_t* off, int32_t* qslot,
+                                             int32_t* __restrict__ qof,
+                                             uint32_t* __restrict__ flags) {
+  const int lane = tid;
+  int n = 0;
+  if (tid < nq) {
+    const int32_t len = q_indptr[tid + 1] - q_indptr[tid];
+    n = min(len, kMaxTerms);
+    flags[tid] = len > kMaxTerms ? 8u : 0u;
+  }
+  int x = n;  // inclusive scan of the per-query counts
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  off[tid + 1] = x;
+  if (tid == 0) off[0] = 0;
+  int sk = (tid < nq ? n : -1) * 64 + (63 - tid);
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int o = __shfl_xor(sk, stride);
+      const bool lower = (lane & stride) == 0;
+      const bool desc = (lane & size) == 0;
+      if ((lower == desc) ? (o > sk) : (o < sk)) sk = o;
+    }
+  }
+  const int r = lane;  // rank
+  const int q = 63 - (sk & 63);
+  const int w = ((r >> 4) & 1) ? 15 - (r & 15) : (r & 15);
+  const int slot = (w << 2) | (r >> 4);
+  qslot[q] = slot;
+  qof[slot] = r < nq ? q : -1;
+}
+
+// The pass's query terms when vocab <= kBitmapVocab (BGE-M3: 250 002), without a sort: the
+// distinct terms are the set bits of an LDS bitmap over the vocabulary, u(t) = the number of set
+// bits below t (per-word prefix counts + a popcount), and since every query's indices ascend
+// (the C ABI's contract), each slot's list is its query's own terms in CSR order, already in
+// ascending u. Same outputs as pass_terms_kernel.
+__global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
+    const int32_t* __restrict__ q_indptr, const int32_t* __restrict__ q_indices,
+    const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
+    int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
+    int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* bits = reinterpret_cast<uint32_t*>(smem);               // [kBmWords]
+  int32_t* wpre = reinterpret_cast<int32_t*>(smem + kBmWords * 4);  // [kBmWords]
+  __shared__ int32_t off[kQB + 1];
+  __shared__ int32_t qslot[kQB];
+  __shared__ int32_t wsum[kScanThreads / 64];
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int nw = (vocab + 31) >> 5;
+  for (int i = tid; i < nw; i += kScanThreads) bits[i] = 0u;
+  if (tid < kQB) deal_queries(q_indptr, nq, tid, off, qslot, qof, flags);
+  __syncthreads();
+  const int total = off[kQB];
+  for (int e = tid; e < total; e += kScanThreads) {
+    int a = 0, n = kQB;  // q = last index with off[q] <= e
+    while (n > 1) {
+      const int h = n >> 1;
+      if (off[a + h] <= e) a += h;
+      n -= h;
+    }
+    const int32_t t = q_indices[q_indptr[a] + (e - off[a])];
+    if (t >= 0 && t < vocab) atomicOr(&bits[t >> 5], 1u << (t & 31));
+  }
+  __syncthreads();
+  // exclusive prefix of the per-word set-bit counts (kPer consecutive words per thread), and
+  // uterm[u] = t for every set bit
+  constexpr int kPer = kBmWords / kScanThreads;
+  int cnt[kPer];
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int w = tid * kPer + j;
+    cnt[j] = w < nw ? __popc(bits[w]) : 0;
+    sum += cnt[j];
+  }
+  int x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int run = x - sum;
+  for (int v = 0; v < wave; ++v) run += wsum[v];
+  if (tid == kScanThreads - 1) *n_terms = run + sum;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int w = tid * kPer + j;
+    if (w < nw) {
+      wpre[w] = run;
+      uint32_t b = bits[w];
+      int u = run;
+      while (b) {
+        uterm[u++] = w * 32 + __builtin_ctz(b);
+        b &= b - 1u;
+      }
+    }
+    run += cnt[j];
+  }
+  __syncthreads();
+  // wave w writes the lists of slots 4 w + i
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    const int slot = wave * kQW + i;
+    const int q = qof[slot];
+    int m = 0;
+    if (q >= 0) {
+      const int32_t p0 = q_indptr[q];
+      const int n = off[q + 1] - off[q];
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const int j = c0 + lane;
+        const int32_t t = j < n ? q_indices[p0 + j] : -1;
+        const bool ok = t >= 0 && t < vocab;
+        const unsigned long long mb = __ballot(ok);
+        if (ok) {
+          const int idx = m + __popcll(mb & ((1ull << lane) - 1ull));
+          const int32_t u = wpre[t >> 5] + __popc(bits[t >> 5] & ((1u << (t & 31)) - 1u));
+          ql[slot * kQStride + idx] = QTerm{q_values[p0 + j], (u % kU) * kTile * 4};
+          qu[slot * kQStride + idx] = u;
+        }
+        m += __popcll(mb);
+      }
+    }
+    // a batch of the scan may read up to kBatch - 1 entries past a list: finite weights there
+    if (lane < kBatch) ql[slot * kQStride + m + lane] = QTerm{0.f, 0};
+    if (lane == 0) qcount[slot] = m;
+  }
+}
+
 // One block for the pass. Sorts the pass's (term, query) pairs by (term, slot) where query q sits
 // in slot 4 w + i of wave w, numbers the distinct terms u = 0..nU-1 ascending (uterm[u] = term),
 // and builds per slot the ascending list of its query's terms: (staging offset, weight) in ql and
@@ -195,42 +341,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
   const int tid = threadIdx.x;
   const int wave = armi::wave_id();
   const int lane = tid & 63;
-  if (tid < kQB) {
-    int n = 0;
-    if (tid < nq) {
-      const int32_t len = q_indptr[tid + 1] - q_indptr[tid];
-      n = min(len, kMaxTerms);
-      flags[tid] = len > kMaxTerms ? 8u : 0u;
-    }
-    // inclusive scan of the per-query counts within wave 0
-    int x = n;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(x, d);
-      if (lane >= d) x += y;
-    }
-    off[tid + 1] = x;
-    if (tid == 0) off[0] = 0;
-    // balance the waves: queries sorted by term count (desc, then index) are dealt to the waves
-    // in snake order, so each wave's sum of term counts (its per-tile work) is about the same
-    int sk = (tid < nq ? n : -1) * 64 + (63 - tid);
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const int o = __shfl_xor(sk, stride);
-        const bool lower = (lane & stride) == 0;
-        const bool desc = (lane & size) == 0;
-        if ((lower == desc) ? (o > sk) : (o < sk)) sk = o;
-      }
-    }
-    const int r = lane;  // rank
-    const int q = 63 - (sk & 63);
-    const int w = ((r >> 4) & 1) ? 15 - (r & 15) : (r & 15);
-    const int slot = (w << 2) | (r >> 4);
-    qslot[q] = slot;
-    qof[slot] = r < nq ? q : -1;
-  }
+  if (tid < kQB) deal_queries(q_indptr, nq, tid, off, qslot, qof, flags);
   __syncthreads();
   const int total = off[kQB];
   const int n2 = armi::pow2_at_least(max(total, 2));
@@ -1153,6 +1264,9 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect));
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepLds));
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_bitmap_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepBmLds));
+  static const bool sort_terms = getenv("ARMI_SPARSE_PASS") && getenv("ARMI_SPARSE_PASS")[0] == 's';
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds));
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<true>),
@@ -1167,9 +1281,14 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       continue;
     }
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
-    pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
-        q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-        w.qcount, w.qof, pflags);
+    if (idx->vocab <= kBitmapVocab && !sort_terms)
+      pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
+          q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
+          w.qcount, w.qof, pflags);
+    else
+      pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
+          q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
+          w.qcount, w.qof, pflags);
     ARMI_LAUNCHED("pass_terms_kernel");
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;

@@ -183,3 +183,22 @@ def test_sparse_max_k_and_several_passes(gpu, oracle_mod):
     q = oracle_mod.sparse_queries(150, seed=62)
     idx = _sparse_index(csr, gpu, base=3)
     _same(_run(idx, q, MAX_K, gpu), oracle_mod.sparse_topk(*csr, *q, MAX_K, ordinal_base=3))
+
+
+@pytest.mark.parametrize("vocab", [250002, 1 << 20])
+def test_sparse_pass_term_numbering_paths(gpu, oracle_mod, vocab):
+    """A pass numbers its distinct terms by an LDS bitmap when vocab <= 2^18 (BGE-M3) and by a
+    sort otherwise (pass_terms_bitmap_kernel / pass_terms_kernel): both give the oracle's answer.
+    With vocab = 2^20 the ids >= 200 000 are moved up by 300 000 (an order-preserving map, so
+    every query stays ascending), so terms live above the bitmap's range too."""
+    from audio_rag_amd.retrieval.device import SparseIndex
+
+    indptr, indices, values = oracle_mod.sparse_corpus(6000, seed=71)
+    qi, qx, qv = oracle_mod.sparse_queries(64, seed=72)
+    if vocab > 250002:
+        indices = np.where(indices >= 200000, indices + 300000, indices).astype(np.int32)
+        qx = np.where(qx >= 200000, qx + 300000, qx).astype(np.int32)
+    idx = SparseIndex(_t(indptr, gpu), _t(indices, gpu), _t(values, gpu), vocab, 5)
+    for k in (3, 20):
+        want = oracle_mod.sparse_topk(indptr, indices, values, qi, qx, qv, k, ordinal_base=5)
+        _same(_run(idx, (qi, qx, qv), k, gpu), want)
