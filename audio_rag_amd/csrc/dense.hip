@@ -2675,8 +2675,16 @@ bool use_q8(int k) {
   return on && k <= 6;
 }
 // Rows rescored per query after the int8 pass: the rows whose key (an upper bound) reaches the
-// k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008).
-int kc_i8(int k) { return use_q8(k) ? 128 : (k <= 6 ? 64 : 128); }
+// k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008). k <= 10
+// rescores 64 (hybrid's dense prefetch of 10: 6 400 of 6 400 queries certified at 1M rows, step
+// 0.255 vs 0.273 ms with 128, tools/probes/kc_ab.sh); a query whose k-th cosine sits among more
+// near-equal bounds takes the exact fallback, so only its time depends on this choice.
+// ARMI_DENSE_KC=64|128 forces either (A/B).
+int kc_i8(int k) {
+  static const int forced = getenv("ARMI_DENSE_KC") ? atoi(getenv("ARMI_DENSE_KC")) : 0;
+  if (forced == 64 || forced == 128) return forced;
+  return use_q8(k) ? 128 : (k <= 10 ? 64 : 128);
+}
 
 struct GemmPlan {
   int n_qb = 0;

@@ -8,7 +8,6 @@ from __future__ import annotations
 
 import ctypes
 import os
-from dataclasses import dataclass
 
 import torch
 
@@ -19,15 +18,48 @@ MAX_K = 240
 QUERY_BLOCK = 64  # queries per scan pass of armi_dense_topk
 
 
-@dataclass
 class TopK:
-    """Per-query top-k on the device. ids are chunk ordinals (-1 past count)."""
+    """Per-query top-k on the device. ids are chunk ordinals (-1 past count).
 
-    scores: torch.Tensor  # float32 [B, k]
-    ids: torch.Tensor     # int64   [B, k]
-    rank: torch.Tensor    # float64 [B, k] ranking key (dense only; RRF score for fused lists)
-    count: torch.Tensor   # int32   [B]
-    flags: torch.Tensor | None = None  # int32 [B] ARMI_FLAG_* bits (dense only)
+    scores  float32 [B, k]
+    ids     int64   [B, k]
+    rank    float64 [B, k] ranking key (dense: the exact cosine key; sparse: the scores; fused
+            lists: the RRF score)
+    count   int32   [B]
+    flags   int32   [B] ARMI_FLAG_* bits, or None
+
+    A list whose kernel writes only one of scores / rank gets the other converted on first access
+    (on the stream current then), so a hybrid step that reads neither launches no conversion."""
+
+    __slots__ = ("_scores", "ids", "_rank", "count", "flags")
+
+    def __init__(self, scores=None, ids=None, rank=None, count=None, flags=None):
+        self._scores, self.ids, self._rank, self.count, self.flags = scores, ids, rank, count, flags
+
+    @property
+    def scores(self) -> torch.Tensor | None:
+        if self._scores is None and self._rank is not None:
+            self._scores = self._rank.float()
+        return self._scores
+
+    @scores.setter
+    def scores(self, t) -> None:
+        self._scores = t
+
+    @property
+    def rank(self) -> torch.Tensor | None:
+        if self._rank is None and self._scores is not None:
+            self._rank = self._scores.double()
+        return self._rank
+
+    @rank.setter
+    def rank(self, t) -> None:
+        self._rank = t
+
+    def tensors(self) -> tuple:
+        """The device tensors this list holds now (no lazy conversion)."""
+        return tuple(t for t in (self._scores, self.ids, self._rank, self.count, self.flags)
+                     if t is not None)
 
 
 def _check_fp16_2d(t: torch.Tensor, name: str, dim: int | None = None) -> None:
@@ -190,7 +222,6 @@ class SparseIndex:
         dev = self.device
         out = TopK(scores=torch.empty((b, k), dtype=torch.float32, device=dev),
                    ids=torch.empty((b, k), dtype=torch.int64, device=dev),
-                   rank=torch.empty((0,), dtype=torch.float64, device=dev),
                    count=torch.empty(b, dtype=torch.int32, device=dev),
                    flags=torch.empty(b, dtype=torch.int32, device=dev))
         if b == 0:
@@ -201,7 +232,6 @@ class SparseIndex:
         call("armi_sparse_topk", self._handle, ptr(q_indptr), ptr(q_indices), ptr(q_values), b, k,
              ptr(row_mask), ptr(out.scores), ptr(out.ids), ptr(out.count), ptr(out.flags),
              ptr(workspace), workspace.numel(), stream_handle())
-        out.rank = out.scores.double()
         return out
 
 
@@ -235,7 +265,7 @@ def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
     a_cnt, b_cnt = a.count.to(torch.int32).contiguous(), b.count.to(torch.int32).contiguous()
     call("armi_rrf_fuse", ptr(a_ids), ptr(a_cnt), ka, ptr(b_ids), ptr(b_cnt), kb, n, rrf_k, limit,
          ptr(out_ids), ptr(out_score), ptr(out_count), stream_handle())
-    return TopK(scores=out_score.float(), ids=out_ids, rank=out_score, count=out_count)
+    return TopK(ids=out_ids, rank=out_score, count=out_count)
 
 
 class ConcurrentHybrid:
@@ -258,9 +288,8 @@ class ConcurrentHybrid:
             s = sparse_fn()
         d = dense_fn()
         main.wait_stream(self.side)
-        for t in (s.scores, s.ids, s.rank, s.count, s.flags):
-            if t is not None:
-                t.record_stream(main)
+        for t in s.tensors():
+            t.record_stream(main)
         return rrf_fuse(d, s, limit, rrf_k=rrf_k)
 
 

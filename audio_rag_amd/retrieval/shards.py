@@ -204,7 +204,6 @@ class ShardedSearch:
             s = self.local_sparse(all_csr, k)
         d = self.local_dense(all_q, k)
         main.wait_stream(self._side)
-        for t in (s.scores, s.ids, s.rank, s.count, s.flags):
-            if t is not None:
-                t.record_stream(main)
+        for t in s.tensors():
+            t.record_stream(main)
         return d, s
