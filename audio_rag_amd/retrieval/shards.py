@@ -80,14 +80,20 @@ def pad_csr(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,
     n = int(indptr.numel()) - 1
     dev = indptr.device
     ip = indptr.to(torch.int64)
-    count = (ip[1:] - ip[:-1]).to(torch.int32)
+    # callers refuse queries longer than `slots` up front (query_sparse_arrays raises); the
+    # clamp only keeps the padded CSR self-consistent without a host synchronisation
+    count = (ip[1:] - ip[:-1]).clamp(max=slots).to(torch.int32)
     pi = torch.zeros(n * slots + 1, dtype=torch.int32, device=dev)
     pv = torch.zeros(n * slots + 1, dtype=torch.float32, device=dev)
     nnz = int(idx.numel())  # the tensor's size, known on the host
-    if nnz:
+    if nnz and n:
         e = torch.arange(nnz, dtype=torch.int64, device=dev)
-        q = torch.searchsorted(ip[1:], e, right=True)  # query owning element e
-        pos = q * slots + (e - ip[q])
+        # query owning element e; entries past indptr[-1] (a CSR may carry unused trailing
+        # entries, e.g. the first rows of a larger query batch) and terms past a query's `slots`
+        # go to the dump slot n * slots, so no write lands outside the buffers
+        q = torch.searchsorted(ip[1:], e, right=True).clamp_(max=n - 1)
+        j = e - ip[q]
+        pos = torch.where((e < ip[n]) & (j < slots), q * slots + j, torch.full_like(e, n * slots))
         pi.index_copy_(0, pos, idx.to(torch.int32))
         pv.index_copy_(0, pos, val.to(torch.float32))
     return count, pi[:-1].view(n, slots), pv[:-1].view(n, slots)

@@ -270,11 +270,18 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # ARMI_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks sharing the GPUs of a
+    # smaller box (RCCL refuses two ranks on one device); the driver's runs use RCCL
+    backend = os.environ.get("ARMI_BENCH_BACKEND", "nccl")
+    gpu = local_rank % max(torch.cuda.device_count(), 1) if backend == "gloo" else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from audio_rag_amd import _armi
     from audio_rag_amd.retrieval.device import (ConcurrentHybrid, DenseIndex, SparseIndex, TopK,
@@ -464,7 +471,8 @@ def main() -> None:
                                   f"queries per GPU per step"),
             }[wl],
             "n_chunks": n, "dim": dim, "batch_per_gpu": batch, "top_k": k,
-            "parallelism": f"corpus-shard{world}",
+            "parallelism": f"corpus-shard{world}" + ("" if backend == "nccl" or world == 1
+                                                      else f" ({backend} rehearsal, shared GPUs)"),
         },
         "p50_ms": statistics.median(lat) * 1e3,
         "p50_single_query_ms": statistics.median(lat1) * 1e3,

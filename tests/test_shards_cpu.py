@@ -158,3 +158,21 @@ def test_pad_unpad_csr_roundtrip():
     assert ip2.tolist() == indptr.tolist()
     n = int(indptr[-1])
     assert ix2[:n].tolist() == idx.tolist() and vx2[:n].tolist() == val.tolist()
+
+
+def test_pad_csr_ignores_trailing_entries():
+    """A CSR whose index / value arrays run past indptr[-1] (bench.py's single-query probe keeps
+    the whole batch's term arrays under a one-query indptr) pads only the live entries; the
+    trailing ones must not be written anywhere (they went past the buffer before: a GPU fault in
+    the N > 1 hybrid rehearsal)."""
+    from audio_rag_amd.retrieval.shards import pad_csr, unpad_csr
+
+    indptr = torch.tensor([0, 3], dtype=torch.int32)
+    idx = torch.arange(10, 10 + 700, dtype=torch.int32)  # 700 entries, 3 live
+    val = torch.arange(700, dtype=torch.float32)
+    cnt, pi, pv = pad_csr(indptr, idx, val)
+    assert cnt.tolist() == [3] and pi[0, :3].tolist() == [10, 11, 12] and pi[0, 3:].eq(0).all()
+    ip2, ix2, vx2 = unpad_csr(cnt, pi, pv)
+    assert ip2.tolist() == [0, 3] and ix2[:3].tolist() == [10, 11, 12] and vx2[:3].tolist() == [0, 1, 2]
+    empty = pad_csr(torch.zeros(1, dtype=torch.int32), idx, val)
+    assert empty[1].shape == (0, 256)

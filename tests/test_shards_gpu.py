@@ -1,0 +1,98 @@
+"""Sharded search with the real kernels: G ranks (one process each) share cuda:0 and exchange over
+gloo (RCCL refuses two ranks on one device), so ShardedSearch (audio_rag_amd/retrieval/shards.py)
+runs exactly what bench.py runs at N = G — the query all-gather, the local libarmi scans of all
+G*B queries (grouped int8 scan at 128 queries, four-wave tiled scan at 256), the packed candidate
+all-gather, armi_topk_merge_shards and RRF after the merge — and every rank must hold the global
+answer of the oracle over the whole corpus for its own queries. The collective backend is the
+only difference from an N-GPU run. Reference: a single Qdrant collection answers the same
+search (retrieval/qdrant.py:281-332)."""
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+N, DIM, B, K = 24000, 1024, 64, 5
+VOCAB = 250002
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex, merge_shards, rrf_fuse
+    from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
+    from oracle import oracle as o
+
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    rows = o.unit_fp16(N, DIM, seed=3)
+    indptr, indices, values = o.sparse_corpus(N, seed=4)
+    lo, hi = shard_range(N, rank, world)
+    dense = DenseIndex(t(rows[lo:hi].view(np.float16)), ordinal_base=lo)
+    a, b = indptr[lo], indptr[hi]
+    sparse = SparseIndex(t(indptr[lo:hi + 1] - a), t(indices[a:b]), t(values[a:b]), VOCAB, lo)
+    ws = torch.empty(dense.workspace_bytes(world * B, 2 * K), dtype=torch.uint8, device=dev)
+    sws = torch.empty(sparse.workspace_bytes(world * B, 2 * K), dtype=torch.uint8, device=dev)
+    ss = ShardedSearch(lambda q, kk: dense.topk(q, kk, workspace=ws), merge_shards,
+                       local_sparse=lambda c, kk: sparse.topk(*c, kk, workspace=sws),
+                       rrf=lambda x, y, kk: rrf_fuse(x, y, kk))
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    q_mine = t(q_all[rank * B:(rank + 1) * B].view(np.float16))
+    qi, qx, qv = o.sparse_queries(B * world, seed=6)
+    qa, qb = qi[rank * B], qi[(rank + 1) * B]
+    q_csr = (t(qi[rank * B:(rank + 1) * B + 1] - qa), t(qx[qa:qb]), t(qv[qa:qb]))
+    d = ss.dense(q_mine, K)
+    s = ss.sparse(q_csr, K)
+    h = ss.hybrid(q_mine, q_csr, K)
+    torch.cuda.synchronize()
+    c = lambda x: x.cpu().numpy()
+    np.savez(Path(out_dir) / f"rank{rank}.npz", d_ids=c(d.ids), d_rank=c(d.rank), d_cnt=c(d.count),
+             s_ids=c(s.ids), s_sc=c(s.scores), s_cnt=c(s.count), h_ids=c(h.ids), h_sc=c(h.rank),
+             h_cnt=c(h.count))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_search_real_kernels_equal_global(tmp_path, oracle_mod, world):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    o = oracle_mod
+    rows = o.unit_fp16(N, DIM, seed=3)
+    csr = o.sparse_corpus(N, seed=4)
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    qcsr = o.sparse_queries(B * world, seed=6)
+    gd = o.dense_topk(rows, q_all, K)
+    gs = o.sparse_topk(*csr, *qcsr, K)
+    gd2 = o.dense_topk(rows, q_all, 2 * K)
+    gs2 = o.sparse_topk(*csr, *qcsr, 2 * K)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        sl = slice(r * B, (r + 1) * B)
+        np.testing.assert_array_equal(z["d_ids"], gd.ids[sl])
+        np.testing.assert_array_equal(z["d_rank"], gd.rank[sl])
+        np.testing.assert_array_equal(z["d_cnt"], gd.count[sl])
+        np.testing.assert_array_equal(z["s_cnt"], gs.count[sl])
+        for q in range(B):
+            c = gs.count[sl][q]
+            np.testing.assert_array_equal(z["s_ids"][q, :c], gs.ids[sl][q, :c])
+            np.testing.assert_array_equal(z["s_sc"][q, :c], gs.scores[sl][q, :c])
+            g = r * B + q
+            want = o.rrf([list(gd2.ids[g, :gd2.count[g]]), list(gs2.ids[g, :gs2.count[g]])], K)
+            assert z["h_cnt"][q] == len(want)
+            assert [int(x) for x in z["h_ids"][q, :len(want)]] == [p for p, _ in want]
+            assert [float(x) for x in z["h_sc"][q, :len(want)]] == [v for _, v in want]
