@@ -388,6 +388,77 @@ __global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
   *reinterpret_cast<u32x4*>(x + i8) = v;
 }
 
+// Attention of one query token per sequence (the <s> token, position 0) over all its keys: the
+// last encoder layer of the cross-encoder, whose only consumer is the classification head on the
+// <s> row (XLMRobertaClassificationHead reads features[:, 0, :]), needs no other query row.
+// One workgroup per (head, sequence), 4 waves: scores of the keys (one key per thread per round,
+// its 128-B K row as 8 x 16-B loads), masked softmax in fp32, then P.V with thread (channel c,
+// key group g) summing keys j = g mod 4 (each V row read as 64 consecutive halves: coalesced).
+// Layout as attention_f16_kernel: qkv [n_seq][L][3][H][64]; ctx [n_seq][H][64] (= [n_seq][d]).
+constexpr int kClsThreads = 256;
+__global__ __launch_bounds__(kClsThreads) void attention_cls_f16_kernel(
+    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
+    int L, int heads, float scale) {
+  __shared__ float qs[kDh];
+  __shared__ float p[kMaxL];
+  __shared__ float red[kClsThreads / 64];
+  __shared__ float part[kClsThreads / 64][kDh];
+  const int head = blockIdx.x, seq = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int d3 = 3 * heads * kDh;
+  const uint16_t* __restrict__ base = qkv + (size_t)seq * L * d3;
+  if (tid < kDh) qs[tid] = (float)__builtin_bit_cast(_Float16, base[head * kDh + tid]) * scale;
+  __syncthreads();
+  float m = -INFINITY;
+  for (int j = tid; j < L; j += kClsThreads) {
+    float sc = -INFINITY;
+    if (mask[(size_t)seq * L + j] != 0) {
+      const u32x4* krow =
+          reinterpret_cast<const u32x4*>(base + (size_t)j * d3 + (heads + head) * kDh);
+      u32x4 kv[kDh / 8];
+#pragma unroll
+      for (int t = 0; t < kDh / 8; ++t) kv[t] = krow[t];
+      sc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kDh / 8; ++t) {
+        const half8 hk = __builtin_bit_cast(half8, kv[t]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sc += qs[8 * t + e] * (float)hk[e];
+      }
+    }
+    p[j] = sc;
+    m = fmaxf(m, sc);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();  // red is reused for the sum
+  float sum = 0.f;
+  for (int j = tid; j < L; j += kClsThreads) {
+    const float e = p[j] == -INFINITY ? 0.f : expf(p[j] - m);
+    p[j] = e;
+    sum += e;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  const float total = red[0] + red[1] + red[2] + red[3];
+  const uint16_t* __restrict__ vcol = base + (2 * heads + head) * kDh + lane;
+  float acc = 0.f;
+  for (int j = wave; j < L; j += kClsThreads / 64)
+    acc += p[j] * (float)__builtin_bit_cast(_Float16, vcol[(size_t)j * d3]);
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (tid < kDh) {
+    const float o = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    ctx[((size_t)seq * heads + head) * kDh + tid] =
+        __builtin_bit_cast(uint16_t, (_Float16)(total > 0.f ? o / total : 0.f));
+  }
+}
+
 size_t attention_lds_bytes(int L) {
   const int lp = (L + 31) & ~31;
   return (size_t)lp * kKStride * 2 + (size_t)kDh * (lp + 4) * 2 + (size_t)lp * 4;
@@ -416,6 +487,21 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
   attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(kThreads), lds,
                          stream>>>(qkv, mask, ctx, L, heads, scale_log2);
   ARMI_LAUNCHED("attention_f16_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_attention_cls_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* ctx,
+                               int n_seq, int L, int heads, int head_dim, float scale,
+                               hipStream_t stream) {
+  ARMI_REQUIRE(head_dim == kDh, "attention_cls_f16: head_dim must be 64");
+  ARMI_REQUIRE(L >= 1 && L <= kMaxL, "attention_cls_f16: L must be in [1, 512]");
+  ARMI_REQUIRE(heads >= 1 && heads <= 65535, "attention_cls_f16: bad head count");
+  if (n_seq <= 0) return ARMI_OK;
+  ARMI_REQUIRE(n_seq <= 65535, "attention_cls_f16: n_seq must be <= 65535 per call");
+  ARMI_REQUIRE(qkv && mask && ctx, "attention_cls_f16: null pointer argument");
+  attention_cls_f16_kernel<<<dim3(heads, n_seq), dim3(kClsThreads), 0, stream>>>(qkv, mask, ctx,
+                                                                                   L, heads, scale);
+  ARMI_LAUNCHED("attention_cls_f16_kernel");
   return ARMI_OK;
 }
 

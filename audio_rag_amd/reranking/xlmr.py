@@ -14,6 +14,7 @@ stream with fp32 LayerNorm statistics: max |score error| 6.5e-5 - 9.6e-5 vs the 
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -132,42 +133,115 @@ class CrossEncoderXLMR:
              ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, L, d, s)
         return probs
 
+    # Two-stream form (A/B, off by default): at or above this many tokens the sequences split into
+    # two halves whose layer ops interleave on two streams. Measured slower at the configs[2]
+    # shape (912 vs 929 q/s, profiles/r02h_rerank_ab.txt): the GEMMs hold every CU, so the other
+    # half's HBM-bound kernels find nothing to overlap. ARMI_RERANK_SPLIT_MIN_TOKENS enables it.
+    split_min_tokens = int(os.environ.get("ARMI_RERANK_SPLIT_MIN_TOKENS", str(1 << 62)))
+
     def _layers_f16_residual(self, h16: torch.Tensor, mask: torch.Tensor, n: int,
                              L: int) -> torch.Tensor:
         """Encoder layers with an all-fp16 residual stream (armi_enc_add_layernorm_f16: fp16 in
-        and out, fp32 statistics), then the classification head on the fp32 <s> rows."""
+        and out, fp32 statistics), then the classification head on the fp32 <s> rows.
+        Large batches run as two half-batches on two streams with their ops issued alternately,
+        so one half's HBM-bound kernels (attention, GELU, add + LayerNorm) overlap the other
+        half's MFMA-bound GEMMs; every sequence's arithmetic is unchanged."""
+        if n < 2 or n * L < self.split_min_tokens:
+            gen = self._layer_ops(h16, mask, n, L)
+            for _ in gen:
+                pass
+            return self._result
+        main = torch.cuda.current_stream()
+        if getattr(self, "_streams", None) is None:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+        half = n // 2
+        parts = [(h16[:half * L], mask[:half], half), (h16[half * L:], mask[half:], n - half)]
+        gens, outs = [], [None, None]
+        for i, (st, (hh, mm, nn)) in enumerate(zip(self._streams, parts)):
+            st.wait_stream(main)
+            hh.record_stream(st)
+            mm.record_stream(st)
+            gens.append((i, st, self._layer_ops(hh, mm, nn, L)))
+        while gens:
+            alive = []
+            for i, st, g in gens:
+                with torch.cuda.stream(st):
+                    try:
+                        next(g)
+                        alive.append((i, st, g))
+                    except StopIteration as e:
+                        outs[i] = e.value
+            gens = alive
+        for st, o in zip(self._streams, outs):
+            main.wait_stream(st)
+            o.record_stream(main)
+        return torch.cat(outs)
+
+    def _layer_ops(self, h16: torch.Tensor, mask: torch.Tensor, n: int, L: int):
+        """Generator over the launches of _layers_f16_residual on the caller's current stream
+        (one yield per kernel); returns the [n] probabilities (also left in self._result)."""
         d, H, dh = self.d, self.heads, self.dh
         s = stream_handle()
         rows = n * L
         lin = torch.nn.functional.linear
         scale = 1.0 / math.sqrt(dh)
-        for ly in self.layers:
+        last = len(self.layers) - 1
+        for i, ly in enumerate(self.layers):
             qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])
-            ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
-            call("armi_enc_attention_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh, scale, s)
+            yield
+            if i == last:
+                # The head reads only the <s> row of the last layer's output, and every op after
+                # the attention is row-wise: the last layer runs its attention for the <s> query
+                # alone (over all keys) and its output projection, LayerNorms and FFN on those n
+                # rows, not on n * L. The <s> rows come out the same as in the full layer.
+                ctx = torch.empty((n, d), dtype=torch.float16, device=self.device)
+                call("armi_enc_attention_cls_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh,
+                     scale, s)
+                h16, rows = h16.view(n, L, d)[:, 0].contiguous(), n
+            else:
+                ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
+                call("armi_enc_attention_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh, scale,
+                     s)
+            del qkv
+            yield
             attn = lin(ctx, ly["wo_h"], ly["bo_h"])
+            yield
             h1 = torch.empty_like(h16)
             call("armi_enc_add_layernorm_f16", ptr(attn), ptr(h16), ptr(ly["ln1"][0]),
                  ptr(ly["ln1"][1]), ptr(h1), rows, d, self.eps, s)
+            del attn
+            yield
             inter = lin(h1, ly["wi_h"], ly["bi_h"])
+            yield
             call("armi_enc_gelu_f16", ptr(inter), None, rows, inter.shape[1], s)
+            yield
             out = lin(inter, ly["wo2_h"], ly["bo2_h"])
+            del inter
+            yield
             h16 = torch.empty_like(h1)
             call("armi_enc_add_layernorm_f16", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
                  ptr(ly["ln2"][1]), ptr(h16), rows, d, self.eps, s)
-        cls = h16.view(n, L, d)[:, 0].float().contiguous()  # [n, d]
+            del out
+            yield
+        cls = h16.float()  # [n, d]: the last layer's <s> rows
         probs = torch.empty(n, dtype=torch.float32, device=self.device)
         call("armi_enc_cls_head_sigmoid", ptr(cls), ptr(self.head[0]), ptr(self.head[1]),
              ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, 1, d, s)
+        self._result = probs
         return probs
 
     def flops(self, n: int, L: int) -> float:
-        """Matmul FLOPs of one forward over n sequences of length L (projections, FFN,
-        QK^T and PV; the fused attention recomputes QK^T once more, not counted)."""
+        """Matmul FLOPs one forward over n sequences of length L computes (projections, FFN,
+        QK^T and PV; the fused attention recomputes QK^T once more, not counted). The default
+        fp16 forward's last layer computes only the <s> rows after its QKV projection."""
         d, ff, layers = self.d, self.layers[0]["wi_t"].shape[1], len(self.layers)
         per_tok = 2 * (4 * d * d + 2 * d * ff)
         attn = 2 * 2 * L * L * d
-        return float(layers * (n * L * per_tok + n * attn))
+        full = float(layers * (n * L * per_tok + n * attn))
+        if self.gemm_dtype != torch.float16 or self.residual != "fp16":
+            return full
+        last = n * L * 2 * 3 * d * d + n * 2 * 2 * L * d + n * 2 * (d * d + 2 * d * ff)
+        return float((layers - 1) * (n * L * per_tok + n * attn) + last)
 
     def _mm(self, x: torch.Tensor, ly: dict, name: str, bias: torch.Tensor | None) -> torch.Tensor:
         if self.gemm_dtype == torch.float32:

@@ -272,6 +272,14 @@ int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const f
  * for the P.V product (fp32 accumulate). */
 int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* ctx, int n_seq,
                            int L, int heads, int head_dim, float scale, hipStream_t stream);
+/* Attention of the <s> query (position 0) of each sequence over its keys, same qkv / mask
+ * layout as armi_enc_attention_f16; ctx is [n_seq][heads][head_dim] fp16. The last layer of the
+ * cross-encoder only feeds the classification head's <s> row (CrossEncoder.predict ->
+ * XLMRobertaClassificationHead, reranking/bge.py:119-123), so only that query row is computed.
+ * Scores, softmax and the P.V sum are fp32. */
+int armi_enc_attention_cls_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* ctx,
+                               int n_seq, int L, int heads, int head_dim, float scale,
+                               hipStream_t stream);
 /* out = LayerNorm(x + res) with x fp16 and res fp32 (nullable); writes fp32 out and, when out16
  * is not null, its fp16 rounding (the next GEMM's operand). */
 int armi_enc_layernorm_residual_f16(const uint16_t* x, const float* res, const float* gamma,

@@ -212,6 +212,24 @@ def test_attention_f16_peaked_scores(gpu):
     torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
 
 
+@pytest.mark.parametrize("L", [1, 7, 256, 300, 512])
+def test_attention_cls_f16_matches_fp32_reference(gpu, L):
+    """armi_enc_attention_cls_f16 (the <s> query only, the last layer's one consumer) against the
+    position-0 row of fp32 eager attention; ragged masks incl. a single live key."""
+    g = torch.Generator().manual_seed(300 + L)
+    n, H, dh = 4, 12, 64
+    qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
+    mask = torch.ones(n, L, dtype=torch.int32)
+    mask[1, max(1, L // 2):] = 0
+    mask[2, 1:] = 0
+    ref = _attention_ref(qkv, mask, H, dh)[:, 0]
+    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
+    out = torch.empty(n, H * dh, dtype=torch.float16, device=gpu)
+    _call("armi_enc_attention_cls_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
+          1 / math.sqrt(dh))
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=2e-3)
+
+
 @pytest.mark.parametrize("width", [768, 1024, 640])  # vectorised (768, 1024) and generic kernels
 def test_layernorm_f16_and_gelu_f16(gpu, width):
     g = torch.Generator().manual_seed(3)
@@ -267,6 +285,35 @@ def test_cross_encoder_fp16_within_1e3(gpu, L, residual):
     with open(Path(__file__).resolve().parent.parent / "gpurun_out" / "rerank_fp16_error.txt", "a") as f:
         f.write(f"L={L} n={n} residual={residual} max_abs_score_error={err:.3e}\n")
     torch.testing.assert_close(got, ref, rtol=0, atol=1e-3)
+
+
+def test_cross_encoder_fp16_two_stream_split_within_1e3(gpu):
+    """The two-stream form of the fp16 forward (half-batches with interleaved ops, what the
+    1,280-pair configs[2] rerank runs) against transformers fp32 (1e-3) and the one-stream form
+    of the same call (GEMMs over half the rows may pick other library kernels: 1e-4)."""
+    from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
+
+    hf = build_reranker(seed=5, arch=dict(attn_implementation="eager"))
+    g = torch.Generator().manual_seed(12)
+    n, L = 9, 128  # odd n: unequal halves
+    ids = torch.randint(4, hf.config.vocab_size, (n, L), generator=g)
+    ids[:, 0] = 0
+    mask = torch.ones(n, L, dtype=torch.long)
+    for i in range(n):
+        ln = L - 7 * i
+        ids[i, 16] = 2
+        ids[i, 17] = 2
+        ids[i, ln - 1] = 2
+        ids[i, ln:] = 1
+        mask[i, ln:] = 0
+    ref = _hf_scores(hf, ids, mask)
+    enc = CrossEncoderXLMR(hf, gpu)
+    enc.to_dtype(torch.float16)
+    one = enc.forward(ids.int().to(gpu), mask.int().to(gpu)).cpu()
+    enc.split_min_tokens = 1
+    two = enc.forward(ids.int().to(gpu), mask.int().to(gpu)).cpu()
+    torch.testing.assert_close(two, one, rtol=0, atol=1e-4)
+    torch.testing.assert_close(two, ref, rtol=0, atol=1e-3)
 
 
 def test_cross_encoder_bf16_gemms_within_budget(gpu):
