@@ -55,22 +55,27 @@ def _bytes(t: torch.Tensor, n: int) -> torch.Tensor:
     return t.contiguous().reshape(n, -1).view(torch.uint8)
 
 
-def pack_rows(parts: list[torch.Tensor]) -> tuple[torch.Tensor, list[tuple[int, torch.dtype, tuple]]]:
+def pack_rows(parts: list[torch.Tensor]) -> tuple[torch.Tensor, list[tuple[int, int, torch.dtype, tuple]]]:
     """Concatenates per-query tensors (leading dim n) into one uint8 [n, bytes] buffer; returns it
-    with the layout unpack_rows needs."""
+    with the layout unpack_rows needs. Parts are laid out by element size, largest first, so every
+    part starts at a multiple of its own element size: a one-row slice of the buffer (contiguous,
+    so not copied by unpack_rows) can be viewed as its dtype in place."""
     n = int(parts[0].shape[0])
-    layout = [(int(_bytes(p, n).shape[1]), p.dtype, tuple(p.shape[1:])) for p in parts]
-    return torch.cat([_bytes(p, n) for p in parts], dim=1), layout
+    order = sorted(range(len(parts)), key=lambda i: -parts[i].element_size())
+    layout, off = [None] * len(parts), 0
+    for i in order:
+        nbytes = int(_bytes(parts[i], n).shape[1])
+        layout[i] = (off, nbytes, parts[i].dtype, tuple(parts[i].shape[1:]))
+        off += nbytes
+    return torch.cat([_bytes(parts[i], n) for i in order], dim=1), layout
 
 
 def unpack_rows(buf: torch.Tensor, layout) -> list[torch.Tensor]:
-    """Inverse of pack_rows on a buffer [..., bytes]: tensors [..., *shape] of the packed dtypes."""
-    out, off = [], 0
+    """Inverse of pack_rows on a buffer [..., bytes]: tensors [..., *shape] of the packed dtypes,
+    in the order pack_rows received them."""
     lead = tuple(buf.shape[:-1])
-    for nbytes, dtype, shape in layout:
-        out.append(buf[..., off:off + nbytes].contiguous().view(dtype).reshape(lead + shape))
-        off += nbytes
-    return out
+    return [buf[..., off:off + nbytes].contiguous().view(dtype).reshape(lead + shape)
+            for off, nbytes, dtype, shape in layout]
 
 
 def pad_csr(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,

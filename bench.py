@@ -276,7 +276,9 @@ def main() -> None:
     gpu = local_rank % max(torch.cuda.device_count(), 1) if backend == "gloo" else local_rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    distributed = world > 1
+    # ARMI_BENCH_SHARDED=1 runs the sharded step (collectives, merge) even at WORLD_SIZE 1: the
+    # exchange's own cost on one GPU, without any link latency
+    distributed = world > 1 or os.environ.get("ARMI_BENCH_SHARDED") == "1"
     if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)

@@ -160,6 +160,26 @@ def test_pad_unpad_csr_roundtrip():
     assert ix2[:n].tolist() == idx.tolist() and vx2[:n].tolist() == val.tolist()
 
 
+def test_unpack_single_row_of_mixed_dtypes():
+    """One query's row of a packed hybrid exchange (bench.py's single-query probe at WORLD_SIZE 1:
+    the slice is contiguous, so unpack_rows views it in place) with 8-byte parts after 4-byte
+    ones in the caller's order: every part must come back intact (a float64 part at byte offset
+    204 could not be viewed before the element-size ordering)."""
+    from audio_rag_amd.retrieval.shards import pack_rows, unpack_rows
+
+    k = 10
+    parts = [torch.randn(3, k, dtype=torch.float64), torch.arange(3 * k).reshape(3, k),
+             torch.randn(3, k), torch.arange(3, dtype=torch.int32).view(3, 1),
+             torch.randn(3, k, dtype=torch.float64), torch.arange(3 * k).reshape(3, k) + 7,
+             torch.randn(3, k), torch.arange(3, dtype=torch.int32).view(3, 1) + 1]
+    buf, layout = pack_rows(parts)
+    g = buf.reshape(1, 3, -1)
+    for r in range(3):
+        got = unpack_rows(g[:, r:r + 1], layout)
+        for a, b in zip(got, parts):
+            assert a.dtype == b.dtype and torch.equal(a.reshape(b[r:r + 1].shape), b[r:r + 1])
+
+
 def test_pad_csr_ignores_trailing_entries():
     """A CSR whose index / value arrays run past indptr[-1] (bench.py's single-query probe keeps
     the whole batch's term arrays under a one-query indptr) pads only the live entries; the
