@@ -48,6 +48,9 @@ SIGNATURES: dict[str, tuple] = {
                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "armi_topk_merge_shards": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "armi_topk_merge_shards_packed": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                              c_int64, c_int, c_int, c_int, c_int, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_void_p]),
     "armi_scan_timing_enable": (c_int, [c_int]),
     "armi_scan_timing_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_kernel_timing_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),

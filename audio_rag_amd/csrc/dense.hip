@@ -2453,14 +2453,22 @@ __global__ __launch_bounds__(256) void dense_exact_scan_kernel(
   }
 }
 
-// Generic merge of sorted-or-unsorted (key, ordinal) lists. Element j of list s for query q
-// sits at s*stride_s + q*stride_q + j; lists hold `width` slots of which counts (nullable)
-// say how many are valid (otherwise ordinal == kNoOrd marks an empty slot).
+// Byte strides of the lists merge_lists_kernel reads: element j of list s for query q sits at
+// s*s8 + q*q8 + 8j (key, ordinal) and s*s4 + q*q4 + 4j (score); its count at s*cs + q*cq. Plain
+// [S][B][k] arrays and the packed rows of the sharded exchange (every field of a (shard, query)
+// row in one byte row, read in place) are both such layouts.
+struct ListLayout {
+  int64_t s8, q8, s4, q4, cs, cq;
+};
+
+// Generic merge of sorted-or-unsorted (key, ordinal) lists (layout above); lists hold `width`
+// slots of which counts (nullable) say how many are valid (otherwise ordinal == kNoOrd marks an
+// empty slot).
 // only_uncertified: skip queries whose flag has CERTIFIED, mark the others FALLBACK.
 __global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
-    const double* __restrict__ in_key, const float* __restrict__ in_score,
-    const int64_t* __restrict__ in_ord, const int32_t* __restrict__ in_count,
-    int64_t stride_s, int64_t stride_q, int64_t count_stride_s, int n_lists, int width,
+    const unsigned char* __restrict__ in_key, const unsigned char* __restrict__ in_score,
+    const unsigned char* __restrict__ in_ord, const unsigned char* __restrict__ in_count,
+    ListLayout lay, int n_lists, int width,
     int pool2, const double* __restrict__ inv_q, int k_out, double* __restrict__ out_key,
     float* __restrict__ out_score, int64_t* __restrict__ out_ord, int32_t* __restrict__ out_count,
     uint32_t* __restrict__ flags, int only_uncertified) {
@@ -2481,13 +2489,17 @@ __global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
     float ss = kNegInf;
     if (e < pool) {
       const int s = e / width, j = e % width;
-      const int cnt = in_count ? in_count[(size_t)s * count_stride_s + q] : width;
+      const int cnt = in_count ? *reinterpret_cast<const int32_t*>(
+                                     in_count + s * lay.cs + q * lay.cq)
+                               : width;
       if (j < cnt) {
-        const size_t at = (size_t)s * stride_s + (size_t)q * stride_q + j;
-        oo = in_ord[at];
+        const int64_t at = s * lay.s8 + q * lay.q8 + 8 * (int64_t)j;
+        oo = *reinterpret_cast<const int64_t*>(in_ord + at);
         if (oo != kNoOrd && oo >= 0) {
-          kk = in_key[at];
-          ss = in_score ? in_score[at] : 0.0f;
+          kk = *reinterpret_cast<const double*>(in_key + at);
+          ss = in_score ? *reinterpret_cast<const float*>(in_score + s * lay.s4 + q * lay.q4 +
+                                                          4 * (int64_t)j)
+                        : 0.0f;
         } else {
           oo = kNoOrd;
         }
@@ -2776,10 +2788,12 @@ int launch_exact(const armi_index* idx, const uint16_t* queries, int nq, int k,
       idx->rows, idx->inv_norm, idx->norm2, row_mask, idx->n_rows, ep.rows_per_block, queries,
       only_uncertified ? flags : nullptr, ep.cap, idx->ordinal_base, w.ex_key, w.ex_ord);
   ARMI_LAUNCHED("dense_exact_scan_kernel");
+  const ListLayout lay{/*s8=*/8 * (int64_t)ep.cap, /*q8=*/8 * (int64_t)ep.n_blocks * ep.cap, 0, 0,
+                       0, 0};
   merge_lists_kernel<<<dim3(nq), dim3(kMergeThreads), lds_merge, stream>>>(
-      w.ex_key, nullptr, w.ex_ord, nullptr, /*stride_s=*/ep.cap,
-      /*stride_q=*/(int64_t)ep.n_blocks * ep.cap, 0, ep.n_blocks, ep.cap, ep.pool2, w.inv_q, k,
-      out_rank, out_scores, out_ids, out_count, flags, only_uncertified);
+      reinterpret_cast<const unsigned char*>(w.ex_key), nullptr,
+      reinterpret_cast<const unsigned char*>(w.ex_ord), nullptr, lay, ep.n_blocks, ep.cap,
+      ep.pool2, w.inv_q, k, out_rank, out_scores, out_ids, out_count, flags, only_uncertified);
   ARMI_LAUNCHED("merge_lists_kernel(exact)");
   return ARMI_OK;
 }
@@ -3036,10 +3050,47 @@ int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const 
                "armi_topk_merge_shards: null pointer argument");
   const int pool2 = armi::pow2_at_least(n_shards * k_in);
   if (int rc = allow_lds(merge_lists_kernel, merge_lds_bytes(pool2))) return rc;
+  const int64_t nk = (int64_t)n_queries * k_in;
+  const ListLayout lay{8 * nk, 8 * (int64_t)k_in, 4 * nk, 4 * (int64_t)k_in,
+                       4 * (int64_t)n_queries, 4};
+  using B = const unsigned char*;
   merge_lists_kernel<<<dim3(n_queries), dim3(kMergeThreads), merge_lds_bytes(pool2), stream>>>(
-      in_rank, in_scores, in_ids, in_count, (int64_t)n_queries * k_in, k_in, n_queries, n_shards,
-      k_in, pool2, nullptr, k_out, out_rank, out_scores, out_ids, out_count, nullptr, 0);
+      reinterpret_cast<B>(in_rank), reinterpret_cast<B>(in_scores), reinterpret_cast<B>(in_ids),
+      reinterpret_cast<B>(in_count), lay, n_shards, k_in, pool2, nullptr, k_out, out_rank,
+      out_scores, out_ids, out_count, nullptr, 0);
   ARMI_LAUNCHED("merge_lists_kernel(shards)");
+  return ARMI_OK;
+}
+
+int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
+                                  int64_t query_stride, int64_t off_rank, int64_t off_scores,
+                                  int64_t off_ids, int64_t off_count, int n_shards,
+                                  int n_queries, int k_in, int k_out, double* out_rank,
+                                  float* out_scores, int64_t* out_ids, int32_t* out_count,
+                                  hipStream_t stream) {
+  ARMI_REQUIRE(n_shards >= 1 && k_in >= 1 && k_out >= 1,
+               "armi_topk_merge_shards_packed: bad sizes");
+  ARMI_REQUIRE((int64_t)n_shards * k_in <= kMaxPool,
+               "armi_topk_merge_shards_packed: n_shards * k_in must be <= 4096");
+  if (n_queries <= 0) return ARMI_OK;
+  ARMI_REQUIRE(packed && out_rank && out_scores && out_ids && out_count,
+               "armi_topk_merge_shards_packed: null pointer argument");
+  const uintptr_t base = reinterpret_cast<uintptr_t>(packed);
+  ARMI_REQUIRE((base + off_rank) % 8 == 0 && (base + off_ids) % 8 == 0 &&
+                   (base + off_scores) % 4 == 0 && (base + off_count) % 4 == 0 &&
+                   query_stride % 8 == 0 && shard_stride % 8 == 0,
+               "armi_topk_merge_shards_packed: fields and strides must be naturally aligned "
+               "(8-byte rank / ids, 4-byte scores / count, strides multiples of 8)");
+  const int pool2 = armi::pow2_at_least(n_shards * k_in);
+  if (int rc = allow_lds(merge_lists_kernel, merge_lds_bytes(pool2))) return rc;
+  const ListLayout lay{shard_stride, query_stride, shard_stride, query_stride, shard_stride,
+                       query_stride};
+  using B = const unsigned char*;
+  B p = static_cast<B>(packed);
+  merge_lists_kernel<<<dim3(n_queries), dim3(kMergeThreads), merge_lds_bytes(pool2), stream>>>(
+      p + off_rank, p + off_scores, p + off_ids, p + off_count, lay, n_shards, k_in, pool2,
+      nullptr, k_out, out_rank, out_scores, out_ids, out_count, nullptr, 0);
+  ARMI_LAUNCHED("merge_lists_kernel(shards, packed)");
   return ARMI_OK;
 }
 

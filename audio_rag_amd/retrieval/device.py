@@ -252,6 +252,27 @@ def merge_shards(rank: torch.Tensor, scores: torch.Tensor, ids: torch.Tensor, co
     return out
 
 
+def merge_shards_packed(buf: torch.Tensor, row0: int, n_queries: int, offsets: tuple[int, int, int, int],
+                        k_in: int, k_out: int) -> TopK:
+    """merge_shards over the all-gathered exchange buffer in place: buf uint8 [S, rows, W] (one
+    byte row per (shard, query), shards.pack_rows' layout), this rank's queries at rows
+    [row0, row0 + n_queries); offsets = byte offsets of (rank f64, scores f32, ids i64, count i32)
+    inside a row. One launch, no per-field copies (armi_topk_merge_shards_packed)."""
+    s, rows, w = buf.shape
+    if not buf.is_contiguous():
+        raise ValueError("merge_shards_packed: the exchange buffer must be contiguous")
+    dev = buf.device
+    out = TopK(scores=torch.empty((n_queries, k_out), dtype=torch.float32, device=dev),
+               ids=torch.empty((n_queries, k_out), dtype=torch.int64, device=dev),
+               rank=torch.empty((n_queries, k_out), dtype=torch.float64, device=dev),
+               count=torch.empty(n_queries, dtype=torch.int32, device=dev))
+    off_rank, off_scores, off_ids, off_count = offsets
+    call("armi_topk_merge_shards_packed", buf.data_ptr() + row0 * w, rows * w, w, off_rank,
+         off_scores, off_ids, off_count, s, n_queries, k_in, k_out, ptr(out.rank),
+         ptr(out.scores), ptr(out.ids), ptr(out.count), stream_handle())
+    return out
+
+
 def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
     """FusionQuery(RRF) of two prefetch lists (qdrant.py:295). rank/scores hold the fp64 RRF
     score (scores as float32 for convenience)."""

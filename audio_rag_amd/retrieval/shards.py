@@ -67,7 +67,10 @@ def pack_rows(parts: list[torch.Tensor]) -> tuple[torch.Tensor, list[tuple[int, 
         nbytes = int(_bytes(parts[i], n).shape[1])
         layout[i] = (off, nbytes, parts[i].dtype, tuple(parts[i].shape[1:]))
         off += nbytes
-    return torch.cat([_bytes(parts[i], n) for i in order], dim=1), layout
+    cols = [_bytes(parts[i], n) for i in order]
+    if off % 8:  # rows a multiple of 8 bytes: every row's fields stay naturally aligned
+        cols.append(torch.empty((n, 8 - off % 8), dtype=torch.uint8, device=parts[0].device))
+    return torch.cat(cols, dim=1), layout
 
 
 def unpack_rows(buf: torch.Tensor, layout) -> list[torch.Tensor]:
@@ -131,10 +134,14 @@ class ShardedSearch:
     this rank's shard and return global ordinals; `merge` combines [S, B, k] lists."""
 
     def __init__(self, local_dense: LocalSearch, merge: Merge, group=None,
-                 local_sparse: Callable | None = None, rrf: Callable | None = None):
+                 local_sparse: Callable | None = None, rrf: Callable | None = None,
+                 merge_packed: Callable | None = None):
+        """merge_packed (device.merge_shards_packed): merges straight from the gathered byte
+        buffer when it lives on the GPU; `merge` serves host buffers (the CPU tests)."""
         self.local_dense = local_dense
         self.local_sparse = local_sparse
         self.merge = merge
+        self.merge_packed = merge_packed
         self.rrf = rrf
         self.group = group
         self.world = dist.get_world_size(group)
@@ -169,6 +176,12 @@ class ShardedSearch:
         parts = [p for t in lists for p in _topk_parts(t)]
         buf, layout = pack_rows(parts)
         g = self._gather(buf)                              # [G, G*nb, bytes]
+        if self.merge_packed is not None and g.is_cuda:
+            # each list's (rank, scores, ids, count) read in place from the gathered rows
+            return [self.merge_packed(g, self.rank * nb, nb,
+                                      tuple(layout[4 * i + j][0] for j in (0, 2, 1, 3)),
+                                      layout[4 * i + 1][3][0], k)
+                    for i in range(len(lists))]
         mine = g[:, self.rank * nb:(self.rank + 1) * nb]   # [G, nb, bytes]
         vals = unpack_rows(mine, layout)
         out = []

@@ -287,7 +287,7 @@ def main() -> None:
 
     from audio_rag_amd import _armi
     from audio_rag_amd.retrieval.device import (ConcurrentHybrid, DenseIndex, SparseIndex, TopK,
-                                                merge_shards, rrf_fuse)
+                                                merge_shards, merge_shards_packed, rrf_fuse)
     from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
 
     n, dim, batch, k = args.chunks, args.dim, args.batch, args.top_k
@@ -324,7 +324,8 @@ def main() -> None:
     if distributed:
         sharded = ShardedSearch(lambda q, kk: index.topk(q, kk, workspace=ws), merge_shards,
                                 local_sparse=(lambda c, kk: sindex.topk(*c, kk, workspace=sws)) if sindex else None,
-                                rrf=lambda a, b, kk: rrf_fuse(a, b, kk))
+                                rrf=lambda a, b, kk: rrf_fuse(a, b, kk),
+                                merge_packed=merge_shards_packed)
 
     # live timing of the cross-encoder forward (runs on torch's current stream)
     rr_timing = {"on": False, "events": [], "flops": 0.0}

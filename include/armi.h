@@ -135,6 +135,19 @@ int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const 
                            int k_out, double* out_rank, float* out_scores, int64_t* out_ids,
                            int32_t* out_count, hipStream_t stream);
 
+/* armi_topk_merge_shards reading the all-gathered exchange buffer in place: per-shard lists
+ * packed one (shard, query) row per byte row — the row of shard s and query q starts at
+ * packed + s * shard_stride + q * query_stride (bytes) and holds k_in ranks (double) at
+ * off_rank, k_in scores (float) at off_scores, k_in ids (int64) at off_ids and the count (int32)
+ * at off_count. Fields must be naturally aligned and both strides multiples of 8. Saves the
+ * per-field copies an unpacked call needs after the RCCL all-gather. */
+int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
+                                  int64_t query_stride, int64_t off_rank, int64_t off_scores,
+                                  int64_t off_ids, int64_t off_count, int n_shards,
+                                  int n_queries, int k_in, int k_out, double* out_rank,
+                                  float* out_scores, int64_t* out_ids, int32_t* out_count,
+                                  hipStream_t stream);
+
 /* Live timing of the dominant kernels for roofline reporting (bench.py): while enabled, every
  * launch of a timed kernel is bracketed by a HIP event pair on the stream it is launched on.
  * _read synchronises on the recorded events of one slot, returns the summed kernel time and the

@@ -29,11 +29,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, packed):
     sys.path.insert(0, str(ROOT))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from audio_rag_amd.retrieval.device import DenseIndex, SparseIndex, merge_shards, rrf_fuse
+    from audio_rag_amd.retrieval.device import (DenseIndex, SparseIndex, merge_shards,
+                                                merge_shards_packed, rrf_fuse)
     from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
     from oracle import oracle as o
 
@@ -49,7 +50,8 @@ def _worker(rank, world, port, out_dir):
     sws = torch.empty(sparse.workspace_bytes(world * B, 2 * K), dtype=torch.uint8, device=dev)
     ss = ShardedSearch(lambda q, kk: dense.topk(q, kk, workspace=ws), merge_shards,
                        local_sparse=lambda c, kk: sparse.topk(*c, kk, workspace=sws),
-                       rrf=lambda x, y, kk: rrf_fuse(x, y, kk))
+                       rrf=lambda x, y, kk: rrf_fuse(x, y, kk),
+                       merge_packed=merge_shards_packed if packed else None)
     q_all = o.unit_fp16(B * world, DIM, seed=5)
     q_mine = t(q_all[rank * B:(rank + 1) * B].view(np.float16))
     qi, qx, qv = o.sparse_queries(B * world, seed=6)
@@ -68,9 +70,11 @@ def _worker(rank, world, port, out_dir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_search_real_kernels_equal_global(tmp_path, oracle_mod, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,packed", [(2, True), (4, True), (2, False)])
+def test_sharded_search_real_kernels_equal_global(tmp_path, oracle_mod, world, packed):
+    """packed: the merge reads the gathered exchange rows in place (armi_topk_merge_shards_packed,
+    what bench.py runs); otherwise unpacked per-field copies into armi_topk_merge_shards."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), packed), nprocs=world, join=True)
     o = oracle_mod
     rows = o.unit_fp16(N, DIM, seed=3)
     csr = o.sparse_corpus(N, seed=4)
