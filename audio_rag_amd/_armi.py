@@ -51,6 +51,10 @@ SIGNATURES: dict[str, tuple] = {
     "armi_topk_merge_shards_packed": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                               c_int64, c_int, c_int, c_int, c_int, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "armi_query_slots_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]),
+    "armi_query_slots_unpack": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int,
+                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "armi_scan_timing_enable": (c_int, [c_int]),
     "armi_scan_timing_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
     "armi_kernel_timing_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),

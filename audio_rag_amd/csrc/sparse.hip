@@ -1181,6 +1181,70 @@ void free_index(armi_sparse_index* idx) {
   delete idx;
 }
 
+// Sparse query CSR <-> fixed slots, the query exchange of a sharded hybrid step (each query's
+// terms padded to `slots` entries, so every rank knows the all-gather's size without a host sync).
+// Pack: one thread per (query, slot); terms past `slots` are dropped (callers refuse such queries
+// first). Unpack: one workgroup reads the gathered rows in place (byte row stride, field offsets),
+// prefix-sums the counts and copies each query's live slots into a CSR.
+__global__ __launch_bounds__(256) void query_slots_pack_kernel(
+    const int32_t* __restrict__ indptr, const int32_t* __restrict__ idx,
+    const float* __restrict__ val, int n, int slots, int32_t* __restrict__ count,
+    int32_t* __restrict__ sidx, float* __restrict__ sval) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * slots) return;
+  const int q = (int)(e / slots), j = (int)(e % slots);
+  const int32_t a = indptr[q];
+  const int32_t c = min(indptr[q + 1] - a, slots);
+  if (j == 0) count[q] = c;
+  sidx[e] = j < c ? idx[a + j] : 0;
+  sval[e] = j < c ? val[a + j] : 0.0f;
+}
+
+constexpr int kUnpackThreads = 1024;
+__global__ __launch_bounds__(kUnpackThreads) void query_slots_unpack_kernel(
+    const unsigned char* __restrict__ rows, int64_t row_stride, int64_t off_count,
+    int64_t off_idx, int64_t off_val, int n, int slots, int32_t* __restrict__ indptr,
+    int32_t* __restrict__ idx, float* __restrict__ val) {
+  __shared__ int32_t wsum[kUnpackThreads / 64];
+  __shared__ int32_t carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    carry = 0;
+    indptr[0] = 0;
+  }
+  __syncthreads();
+  for (int q0 = 0; q0 < n; q0 += kUnpackThreads) {
+    const int q = q0 + tid;
+    const int32_t c =
+        q < n ? min(max(*reinterpret_cast<const int32_t*>(rows + q * row_stride + off_count), 0),
+                    slots)
+              : 0;
+    int32_t x = c;  // inclusive wave scan
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int32_t before = carry;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    const int32_t start = before + x - c;
+    if (q < n) {
+      indptr[q + 1] = start + c;
+      const int32_t* si = reinterpret_cast<const int32_t*>(rows + q * row_stride + off_idx);
+      const float* sv = reinterpret_cast<const float*>(rows + q * row_stride + off_val);
+      for (int j = 0; j < c; ++j) {
+        idx[start + j] = si[j];
+        val[start + j] = sv[j];
+      }
+    }
+    __syncthreads();
+    if (tid == kUnpackThreads - 1) carry = start + c;
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1334,6 +1398,38 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         out_count, pflags);
     ARMI_LAUNCHED("sparse_collect_merge_kernel");
   }
+  return ARMI_OK;
+}
+
+int armi_query_slots_pack(const int32_t* indptr, const int32_t* indices, const float* values,
+                          int n_queries, int slots, int32_t* count, int32_t* slot_indices,
+                          float* slot_values, hipStream_t stream) {
+  ARMI_REQUIRE(slots >= 1, "armi_query_slots_pack: slots must be >= 1");
+  if (n_queries <= 0) return ARMI_OK;
+  ARMI_REQUIRE(indptr && indices && values && count && slot_indices && slot_values,
+               "armi_query_slots_pack: null pointer argument");
+  const int64_t total = (int64_t)n_queries * slots;
+  query_slots_pack_kernel<<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream>>>(
+      indptr, indices, values, n_queries, slots, count, slot_indices, slot_values);
+  ARMI_LAUNCHED("query_slots_pack_kernel");
+  return ARMI_OK;
+}
+
+int armi_query_slots_unpack(const void* rows, int64_t row_stride, int64_t off_count,
+                            int64_t off_indices, int64_t off_values, int n_queries, int slots,
+                            int32_t* indptr, int32_t* indices, float* values,
+                            hipStream_t stream) {
+  ARMI_REQUIRE(slots >= 1, "armi_query_slots_unpack: slots must be >= 1");
+  ARMI_REQUIRE(rows && indptr && indices && values,
+               "armi_query_slots_unpack: null pointer argument");
+  const uintptr_t b = reinterpret_cast<uintptr_t>(rows);
+  ARMI_REQUIRE(row_stride % 4 == 0 && (b + off_count) % 4 == 0 && (b + off_indices) % 4 == 0 &&
+                   (b + off_values) % 4 == 0,
+               "armi_query_slots_unpack: fields and row stride must be 4-byte aligned");
+  query_slots_unpack_kernel<<<dim3(1), dim3(kUnpackThreads), 0, stream>>>(
+      static_cast<const unsigned char*>(rows), row_stride, off_count, off_indices, off_values,
+      n_queries < 0 ? 0 : n_queries, slots, indptr, indices, values);
+  ARMI_LAUNCHED("query_slots_unpack_kernel");
   return ARMI_OK;
 }
 

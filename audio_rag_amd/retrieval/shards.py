@@ -29,6 +29,7 @@ from typing import Callable
 import torch
 import torch.distributed as dist
 
+from audio_rag_amd._armi import call, ptr, stream_handle
 from audio_rag_amd.retrieval.device import TopK
 
 MAX_QUERY_TERMS = 256  # armi_sparse_topk's per-query term capacity (include/armi.h)
@@ -84,9 +85,19 @@ def unpack_rows(buf: torch.Tensor, layout) -> list[torch.Tensor]:
 def pad_csr(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor,
             slots: int = MAX_QUERY_TERMS) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """CSR (indptr [n+1], indices, values) -> fixed slots (count int32 [n], indices int32 [n, slots],
-    values float32 [n, slots]), on the device and without a host synchronisation."""
+    values float32 [n, slots]) without a host synchronisation. GPU tensors: one libarmi launch
+    (armi_query_slots_pack); host tensors (the gloo CPU tests' exchange): torch ops."""
     n = int(indptr.numel()) - 1
     dev = indptr.device
+    if indptr.is_cuda:
+        count = torch.empty(n, dtype=torch.int32, device=dev)
+        pi = torch.empty((n, slots), dtype=torch.int32, device=dev)
+        pv = torch.empty((n, slots), dtype=torch.float32, device=dev)
+        ip32, i32, v32 = (t.to(d).contiguous() for t, d in
+                          ((indptr, torch.int32), (idx, torch.int32), (val, torch.float32)))
+        call("armi_query_slots_pack", ptr(ip32), ptr(i32), ptr(v32), n, slots, ptr(count),
+             ptr(pi), ptr(pv), stream_handle())
+        return count, pi, pv
     ip = indptr.to(torch.int64)
     # callers refuse queries longer than `slots` up front (query_sparse_arrays raises); the
     # clamp only keeps the padded CSR self-consistent without a host synchronisation
@@ -165,6 +176,17 @@ class ShardedSearch:
         buf, layout = pack_rows(parts)
         g = self._gather(buf)                              # [G, nb, bytes]
         g = g.reshape((-1,) + tuple(g.shape[2:]))          # [G*nb, bytes]
+        if g.is_cuda and q_csr is not None:
+            # the CSR straight from the gathered rows (one launch, no per-field copies)
+            dense = unpack_rows(g, layout[:1])[0] if q_dense is not None else None
+            lc, li, lv = layout[-3:]
+            n, slots = int(g.shape[0]), li[3][0]
+            indptr = torch.empty(n + 1, dtype=torch.int32, device=g.device)
+            idx = torch.empty(n * slots, dtype=torch.int32, device=g.device)
+            val = torch.empty(n * slots, dtype=torch.float32, device=g.device)
+            call("armi_query_slots_unpack", g.data_ptr(), int(g.stride(0)), lc[0], li[0], lv[0], n,
+                 slots, ptr(indptr), ptr(idx), ptr(val), stream_handle())
+            return dense, (indptr, idx, val)
         vals = unpack_rows(g, layout)
         dense = vals.pop(0) if q_dense is not None else None
         csr = unpad_csr(*vals) if q_csr is not None else None

@@ -235,6 +235,20 @@ int armi_sparse_topk(const armi_sparse_index* index, const int32_t* q_indptr,
                      int32_t* out_count, uint32_t* out_flags, void* workspace,
                      size_t workspace_bytes, hipStream_t stream);
 
+/* Query-term exchange of the sharded hybrid step (retrieval/shards.py; no reference
+ * counterpart, the reference queries one Qdrant replica). _pack: CSR -> fixed slots (count
+ * int32 [n], slot_indices int32 [n][slots], slot_values float [n][slots], zero-filled; terms past
+ * `slots` are dropped, so callers refuse longer queries first). _unpack: the all-gathered rows
+ * (row q at rows + q * row_stride, its count / indices / values at the byte offsets) -> CSR
+ * (indptr int32 [n + 1], indices, values; capacity n * slots), read in place. */
+int armi_query_slots_pack(const int32_t* indptr, const int32_t* indices, const float* values,
+                          int n_queries, int slots, int32_t* count, int32_t* slot_indices,
+                          float* slot_values, hipStream_t stream);
+int armi_query_slots_unpack(const void* rows, int64_t row_stride, int64_t off_count,
+                            int64_t off_indices, int64_t off_values, int n_queries, int slots,
+                            int32_t* indptr, int32_t* indices, float* values,
+                            hipStream_t stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Reciprocal-rank fusion                                                                     */
 /* ------------------------------------------------------------------------------------------ */

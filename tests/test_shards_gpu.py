@@ -100,3 +100,42 @@ def test_sharded_search_real_kernels_equal_global(tmp_path, oracle_mod, world, p
             assert z["h_cnt"][q] == len(want)
             assert [int(x) for x in z["h_ids"][q, :len(want)]] == [p for p, _ in want]
             assert [float(x) for x in z["h_sc"][q, :len(want)]] == [v for _, v in want]
+
+
+@pytest.mark.gpu
+def test_query_slots_pack_unpack_match_host(gpu):
+    """armi_query_slots_pack / _unpack (the sharded hybrid step's query exchange on the GPU)
+    against the host torch form of the same exchange: ragged, empty, full (MAX_QUERY_TERMS) and
+    over-long (truncated) queries, trailing CSR entries past indptr[-1], 1,300 queries (the
+    unpack's prefix sum runs over two 1,024-query rounds)."""
+    from audio_rag_amd.retrieval.shards import (MAX_QUERY_TERMS, pack_rows, pad_csr, unpack_rows,
+                                                unpad_csr)
+
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 40, 1300)
+    lens[[0, 7, 8]] = 0
+    lens[3] = MAX_QUERY_TERMS
+    lens[5] = MAX_QUERY_TERMS + 9  # truncated by both forms
+    indptr = np.zeros(len(lens) + 1, np.int32)
+    indptr[1:] = np.cumsum(lens)
+    idx = rng.integers(0, 250002, indptr[-1] + 50).astype(np.int32)  # 50 trailing entries
+    val = rng.random(indptr[-1] + 50).astype(np.float32)
+    host = pad_csr(*(torch.from_numpy(a) for a in (indptr, idx, val)))
+    dev = pad_csr(*(torch.from_numpy(a).to(gpu) for a in (indptr, idx, val)))
+    for h, d in zip(host, dev):
+        assert torch.equal(h, d.cpu())
+    # unpack from a packed, gathered-shaped buffer with a leading dense part (odd byte width)
+    dense = torch.randint(0, 255, (len(lens), 6), dtype=torch.uint8)
+    buf, layout = pack_rows([dense.to(gpu), *dev])
+    from audio_rag_amd._armi import call, ptr, stream_handle
+    n = len(lens)
+    ip = torch.empty(n + 1, dtype=torch.int32, device=gpu)
+    ix = torch.empty(n * MAX_QUERY_TERMS, dtype=torch.int32, device=gpu)
+    vx = torch.empty(n * MAX_QUERY_TERMS, dtype=torch.float32, device=gpu)
+    lc, li, lv = layout[1:]
+    call("armi_query_slots_unpack", buf.data_ptr(), int(buf.stride(0)), lc[0], li[0], lv[0], n,
+         MAX_QUERY_TERMS, ptr(ip), ptr(ix), ptr(vx), stream_handle())
+    want = unpad_csr(*unpack_rows(buf.cpu(), layout)[1:])
+    m = int(want[0][-1])
+    assert torch.equal(ip.cpu(), want[0])
+    assert torch.equal(ix.cpu()[:m], want[1][:m]) and torch.equal(vx.cpu()[:m], want[2][:m])
