@@ -2164,6 +2164,21 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
 
+  // One memory round trip for everything the selection needs: the pool (8 entries per thread;
+  // pool <= kMaxPool = 8 * 512, so one round), the workgroup lists' bounds and the query are all
+  // in flight before anything waits. Entry g * kKW is workgroup g's maximum (its list is sorted).
+  constexpr int kFilterBatch = 8;
+  static_assert(kFilterBatch * kDenseMergeThreads >= kMaxPool, "one filter round");
+  float kk[kFilterBatch];
+  int32_t rw[kFilterBatch];
+#pragma unroll
+  for (int j = 0; j < kFilterBatch; ++j) {
+    const int e = tid + j * kDenseMergeThreads;
+    const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
+    kk[j] = e < pool ? cand_key[src] : kNegInf;
+    rw[j] = e < pool ? cand_row[src] : 0;
+  }
+  float b = tid < n_wg ? cand_bound[(size_t)tid * q_stride + qg] : kNegInf;
   // exact query norm (every wave holds the fixed-point query for the rescore anyway)
   int32_t qf[DIM / 64];
   load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
@@ -2177,24 +2192,32 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (tid == 0) {
     inv_q_out[qg] = inv_q;
     qnorm_out[qg] = qnorm_real;
+    ctr[0] = 0;
   }
+  // workgroup maxima and bound partials to LDS (rkey is free until the rescore)
+  uint32_t* umax = reinterpret_cast<uint32_t*>(rkey);         // [256]
+  float* bpart = reinterpret_cast<float*>(rkey) + 256;        // [kDenseMergeThreads / 64]
+#pragma unroll
+  for (int j = 0; j < kFilterBatch; ++j) {
+    const int e = tid + j * kDenseMergeThreads;
+    if (e < pool && e % kKW == 0) umax[e / kKW] = ord_key(kk[j]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+  if (lane == 0) bpart[wave] = b;
+  __syncthreads();
 
   // wave 0: t0 = kc-th largest workgroup maximum, and the workgroup lists' own bounds
   if (wave == 0) {
-    float b = kNegInf;
+    float bb = kNegInf;
+#pragma unroll
+    for (int w = 0; w < kDenseMergeThreads / 64; ++w) bb = fmaxf(bb, bpart[w]);
     uint32_t u[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int g = lane + 64 * i;
-      float m = kNegInf;
-      if (g < n_wg) {
-        m = cand_key[((size_t)g * q_stride + qg) * kKW];
-        b = fmaxf(b, cand_bound[(size_t)g * q_stride + qg]);
-      }
-      u[i] = ord_key(m);
+      u[i] = g < n_wg ? umax[g] : ord_key(kNegInf);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
     float t0 = kNegInf;
     if (n_wg >= kc) {
       uint32_t prefix = 0;  // largest v with #{u >= v} >= kc, i.e. the kc-th largest key
@@ -2208,40 +2231,26 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
       t0 = from_ord_key(prefix);
     }
     if (lane == 0) {
-      red[8] = b;
+      red[8] = bb;
       red[9] = t0;
-      ctr[0] = 0;
     }
   }
   __syncthreads();
   const float t0 = red[9];
 
-  // filter the pool: 8 entries per thread per round, all loads issued before any is used (a
-  // latency-bound kernel: one memory round trip per round, not per entry)
+  // filter the pool held in registers
   float dmax = kNegInf;
-  constexpr int kFilterBatch = 8;
-  for (int e0 = tid; e0 < pool; e0 += kFilterBatch * kDenseMergeThreads) {
-    float kk[kFilterBatch];
-    int32_t rw[kFilterBatch];
 #pragma unroll
-    for (int j = 0; j < kFilterBatch; ++j) {
-      const int e = e0 + j * kDenseMergeThreads;
-      const size_t src = ((size_t)(e / kKW) * q_stride + qg) * kKW + (e % kKW);
-      kk[j] = e < pool ? cand_key[src] : kNegInf;
-      rw[j] = e < pool ? cand_row[src] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < kFilterBatch; ++j) {
-      if (kk[j] == kNegInf) continue;
-      if (kk[j] >= t0) {
-        const int slot = atomicAdd(&ctr[0], 1);
-        if (slot < kSelCap) {
-          skey[slot] = kk[j];
-          srow[slot] = rw[j];
-        }
-      } else {
-        dmax = fmaxf(dmax, kk[j]);
+  for (int j = 0; j < kFilterBatch; ++j) {
+    if (kk[j] == kNegInf) continue;
+    if (kk[j] >= t0) {
+      const int slot = atomicAdd(&ctr[0], 1);
+      if (slot < kSelCap) {
+        skey[slot] = kk[j];
+        srow[slot] = rw[j];
       }
+    } else {
+      dmax = fmaxf(dmax, kk[j]);
     }
   }
 #pragma unroll
@@ -2926,6 +2935,8 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
+  ARMI_REQUIRE(n_wg >= 1 && n_wg * kKW <= kMaxPool,
+               "dense merge: the candidate pool must fit one filter round (<= 256 lists)");
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
