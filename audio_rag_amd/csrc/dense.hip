@@ -2194,6 +2194,10 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     qnorm_out[qg] = qnorm_real;
     ctr[0] = 0;
   }
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_MERGE_ABL) && ARMI_MERGE_ABL == 3
+  if (kk[0] == 12345.f && rw[kFilterBatch - 1] == -7 && b == 1.f) out_flags[qg] = 0;  // keep loads
+  return;  // probe: loads + query norm only
+#endif
   // workgroup maxima and bound partials to LDS (rkey is free until the rescore)
   uint32_t* umax = reinterpret_cast<uint32_t*>(rkey);         // [256]
   float* bpart = reinterpret_cast<float*>(rkey) + 256;        // [kDenseMergeThreads / 64]
@@ -2319,6 +2323,10 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     }
     armi::lds_sort_approx_desc(skey, srow, n2);
   }
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_MERGE_ABL) && ARMI_MERGE_ABL == 2
+  if (tid == 0) out_flags[qg] = 0;
+  return;  // probe: up to the sorted selection
+#endif
   float bound = red[8];
 #pragma unroll
   for (int w = 0; w < kDenseMergeThreads / 64; ++w) bound = fmaxf(bound, red[w]);
@@ -2336,7 +2344,11 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
       const int c = wave + kMW * (i0 + j);
       const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
       rr[j] = live ? srow[c] : -1;
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_MERGE_ABL) && ARMI_MERGE_ABL == 1
+      load_raw<DIM>(rows, lane, raw[j]);  // probe: every rescore load hits one cached row
+#else
       load_raw<DIM>(rows + (size_t)(live ? rr[j] : 0) * DIM, lane, raw[j]);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
