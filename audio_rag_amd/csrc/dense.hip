@@ -2333,12 +2333,17 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (n_keep > 64 && n_keep <= 4 * 64 && kc <= 64) bound = fmaxf(bound, red[10]);
   if (kc < n2) bound = fmaxf(bound, skey[kc]);
 
-  // exact rescore of the kc best, kRescoreBatch rows in flight per wave
+  // exact rescore of the kc best, kRescoreBatch rows in flight per wave; each row's inverse norm
+  // is loaded with the row (same round trip), and the 8 per-lane partial dots are reduced
+  // together (a halving butterfly: 10 int64 shuffles for 8 rows instead of 48); lane 8r ends
+  // with row r's exact dot (integer sums: any order gives the same bits).
+  static_assert(kRescoreBatch == 8, "the butterfly below reduces 8 rows");
   constexpr int kMW = kDenseMergeThreads / 64;
   const int per_wave = (kc + kMW - 1) / kMW;
   for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
     u32x2 raw[kRescoreBatch][DIM / 256];
     int32_t rr[kRescoreBatch];
+    double inv[kRescoreBatch];
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
       const int c = wave + kMW * (i0 + j);
@@ -2349,22 +2354,49 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #else
       load_raw<DIM>(rows + (size_t)(live ? rr[j] : 0) * DIM, lane, raw[j]);
 #endif
+      inv[j] = inv_norm[live ? rr[j] : 0];
     }
+    int64_t v[kRescoreBatch];
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
-      if (i0 + j >= per_wave) break;
-      const int c = wave + kMW * (i0 + j);
-      double key = kNegInfD;
-      int64_t ord = kNoOrd;
-      const int64_t dot = dot_fixed<DIM>(qf, raw[j]);
-      if (rr[j] >= 0) {
-        key = (double)dot * inv_norm[rr[j]];
-        ord = ordinal_base + rr[j];
+      int32_t xf[DIM / 64];
+      raw_to_fixed<DIM>(raw[j], xf);
+      int64_t acc = 0;
+#pragma unroll
+      for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)xf[i];
+      v[j] = acc;
+    }
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // lanes with bit 5 keep rows 4..7, the others rows 0..3
+      const int64_t mine = b5 ? v[4 + m] : v[m];
+      const int64_t give = b5 ? v[m] : v[4 + m];
+      v[m] = mine + __shfl_xor(give, 32);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int64_t mine = b4 ? v[2 + m] : v[m];
+      const int64_t give = b4 ? v[m] : v[2 + m];
+      v[m] = mine + __shfl_xor(give, 16);
+    }
+    int64_t dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
+    dot += __shfl_xor(dot, 4);
+    dot += __shfl_xor(dot, 2);
+    dot += __shfl_xor(dot, 1);
+    const int r = (lane >> 3) & 7;  // = 4 b5 + 2 b4 + b3
+    int32_t myrow = -1;
+    double myinv = 0.0;
+#pragma unroll
+    for (int j = 0; j < kRescoreBatch; ++j) {
+      if (j == r) {
+        myrow = rr[j];
+        myinv = inv[j];
       }
-      if (lane == 0) {
-        rkey[c] = key;
-        rord[c] = ord;
-      }
+    }
+    if ((lane & 7) == 0 && i0 + r < per_wave) {
+      const int c = wave + kMW * (i0 + r);
+      rkey[c] = myrow >= 0 ? (double)dot * myinv : kNegInfD;
+      rord[c] = myrow >= 0 ? ordinal_base + myrow : kNoOrd;
     }
   }
   __syncthreads();
