@@ -41,6 +41,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # 1/16 of the bf16 rate (cdna_hip_programming.md §3 'FP32-input MFMA')
 MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.0}
 
+# measured fp16 MFMA ceiling under the chip's clock management (back-to-back MFMAs on random
+# operands hold ~1.63 GHz, not 2.4): profiles/r02o_mfma_ceiling.txt; reported beside the spec peak
+MFMA_PRACTICAL_TFLOPS = {"fp16": 1674.0}
+
 
 def cpu_model() -> str:
     try:
@@ -498,6 +502,8 @@ def main() -> None:
             "peak": MFMA_PEAK_TFLOPS["fp16"],
             "unit": "TFLOP/s",
             "frac": alg_flops / (scan_avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["fp16"],
+            "frac_of_measured_ceiling": (alg_flops / (scan_avg_ms * 1e-3) / 1e12
+                                         / MFMA_PRACTICAL_TFLOPS["fp16"]),
             "traffic": None,
             "algorithmic_flops_per_launch": alg_flops,
             "algorithmic_bytes_per_launch": alg_bytes,
@@ -519,6 +525,8 @@ def main() -> None:
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": rr_tflops / peak,
+            "frac_of_measured_ceiling": (rr_tflops / MFMA_PRACTICAL_TFLOPS[args.rerank_dtype]
+                                         if args.rerank_dtype in MFMA_PRACTICAL_TFLOPS else None),
             "traffic": None,
             "algorithmic_flops_per_step": rr_timing["flops"] / max(len(rr_timing["events"]), 1),
             "avg_forward_ms": rr_ms / max(len(rr_timing["events"]), 1),
