@@ -416,43 +416,61 @@ __global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
 // Attention of one query token per sequence (the <s> token, position 0) over all its keys: the
 // last encoder layer of the cross-encoder, whose only consumer is the classification head on the
 // <s> row (XLMRobertaClassificationHead reads features[:, 0, :]), needs no other query row.
-// One workgroup per (head, sequence), 4 waves: scores of the keys (one key per thread per round,
-// its 128-B K row as 8 x 16-B loads), masked softmax in fp32, then P.V with thread (channel c,
-// key group g) summing keys j = g mod 4 (each V row read as 64 consecutive halves: coalesced).
+// One workgroup per (head, sequence), 4 waves. A key's 64 channels are 8 chunks of 16 B, so a wave
+// covers 8 keys per load instruction (lane = key slot (lane >> 3) x chunk (lane & 7)): every load
+// is a full 128-B line. Scores: chunk partial dots reduced over the 8 chunk lanes, masked softmax
+// in fp32; P.V: each lane accumulates its chunk's 8 channels over its keys, then the key slots
+// (shuffles) and the waves (LDS) are summed.
 // Layout as attention_f16_kernel: qkv [n_seq][L][3][H][64]; ctx [n_seq][H][64] (= [n_seq][d]).
 constexpr int kClsThreads = 256;
+constexpr int kClsKeySlots = kClsThreads / 8;             // keys per round (8 lanes per key)
+constexpr int kClsRounds = kMaxL / kClsKeySlots;          // rounds at L = kMaxL
 __global__ __launch_bounds__(kClsThreads) void attention_cls_f16_kernel(
     const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
     int L, int heads, float scale) {
-  __shared__ float qs[kDh];
   __shared__ float p[kMaxL];
   __shared__ float red[kClsThreads / 64];
   __shared__ float part[kClsThreads / 64][kDh];
   const int head = blockIdx.x, seq = blockIdx.y, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  const int ch = lane & 7;                   // 16-B chunk: channels 8 ch .. 8 ch + 7
+  const int slot = wave * 8 + (lane >> 3);   // key slot: keys slot, slot + 32, ...
   const int d3 = 3 * heads * kDh;
   const uint16_t* __restrict__ base = qkv + (size_t)seq * L * d3;
-  if (tid < kDh) qs[tid] = (float)__builtin_bit_cast(_Float16, base[head * kDh + tid]) * scale;
-  __syncthreads();
+  float qv[8];
+  {
+    const half8 hq = __builtin_bit_cast(half8, *reinterpret_cast<const u32x4*>(
+                                                   base + head * kDh + 8 * ch));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[e] = (float)hq[e] * scale;
+  }
+  const int rounds = (L + kClsKeySlots - 1) / kClsKeySlots;
+  // scores: all of this lane's K chunks in flight before any is used
+  u32x4 kc[kClsRounds];
+#pragma unroll
+  for (int r = 0; r < kClsRounds; ++r) {
+    const int j = slot + r * kClsKeySlots;
+    if (r < rounds && j < L)
+      kc[r] = *reinterpret_cast<const u32x4*>(base + (size_t)j * d3 + (heads + head) * kDh + 8 * ch);
+  }
   float m = -INFINITY;
-  for (int j = tid; j < L; j += kClsThreads) {
-    float sc = -INFINITY;
-    if (mask[(size_t)seq * L + j] != 0) {
-      const u32x4* krow =
-          reinterpret_cast<const u32x4*>(base + (size_t)j * d3 + (heads + head) * kDh);
-      u32x4 kv[kDh / 8];
 #pragma unroll
-      for (int t = 0; t < kDh / 8; ++t) kv[t] = krow[t];
-      sc = 0.f;
+  for (int r = 0; r < kClsRounds; ++r) {
+    const int j = slot + r * kClsKeySlots;
+    float sc = 0.f;
+    if (r < rounds && j < L) {
+      const half8 hk = __builtin_bit_cast(half8, kc[r]);
 #pragma unroll
-      for (int t = 0; t < kDh / 8; ++t) {
-        const half8 hk = __builtin_bit_cast(half8, kv[t]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sc += qs[8 * t + e] * (float)hk[e];
-      }
+      for (int e = 0; e < 8; ++e) sc += qv[e] * (float)hk[e];
     }
-    p[j] = sc;
-    m = fmaxf(m, sc);
+    sc += __shfl_xor(sc, 1);
+    sc += __shfl_xor(sc, 2);
+    sc += __shfl_xor(sc, 4);
+    if (r < rounds && j < L) {
+      sc = mask[(size_t)seq * L + j] != 0 ? sc : -INFINITY;
+      if (ch == 0) p[j] = sc;
+      m = fmaxf(m, sc);
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
@@ -471,11 +489,33 @@ __global__ __launch_bounds__(kClsThreads) void attention_cls_f16_kernel(
   if (lane == 0) red[wave] = sum;
   __syncthreads();
   const float total = red[0] + red[1] + red[2] + red[3];
-  const uint16_t* __restrict__ vcol = base + (2 * heads + head) * kDh + lane;
-  float acc = 0.f;
-  for (int j = wave; j < L; j += kClsThreads / 64)
-    acc += p[j] * (float)__builtin_bit_cast(_Float16, vcol[(size_t)j * d3]);
-  part[wave][lane] = acc;
+  // P.V: this lane's chunk of its keys' V rows, all loads in flight first
+  u32x4 vc[kClsRounds];
+#pragma unroll
+  for (int r = 0; r < kClsRounds; ++r) {
+    const int j = slot + r * kClsKeySlots;
+    if (r < rounds && j < L)
+      vc[r] = *reinterpret_cast<const u32x4*>(base + (size_t)j * d3 + (2 * heads + head) * kDh +
+                                              8 * ch);
+  }
+  float acc[8] = {};
+#pragma unroll
+  for (int r = 0; r < kClsRounds; ++r) {
+    const int j = slot + r * kClsKeySlots;
+    if (r < rounds && j < L) {
+      const float w = p[j];
+      const half8 hv = __builtin_bit_cast(half8, vc[r]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += w * (float)hv[e];
+    }
+  }
+#pragma unroll
+  for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off);
+  if (lane < 8)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[wave][8 * ch + e] = acc[e];
   __syncthreads();
   if (tid < kDh) {
     const float o = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
