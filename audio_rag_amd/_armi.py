@@ -62,6 +62,7 @@ SIGNATURES: dict[str, tuple] = {
     "armi_stream_create_hybrid": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_double,
                                           ctypes.POINTER(c_void_p)]),
     "armi_stream_destroy": (c_int, [c_void_p]),
+    "armi_stream_stop": (c_int, [c_void_p]),
     "armi_stream_submit": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int64)]),
     "armi_stream_submit_hybrid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                           ctypes.POINTER(c_int64)]),

@@ -23,7 +23,25 @@ struct armi_index {
                                  // padding): 16-B chunk c of row r at tile r/32, chunk c, lane r%32
   float* a32 = nullptr;          // [n_tiles*32] s_r / |x_r| (score scale; NaN = invalid / padding)
   float* e32 = nullptr;          // [n_tiles*32] >= ||x_r - s_r rows8[r]||_2 / |x_r| (per unit |q|)
+  // The int8 image (rows8, a32, e32) is stored in a SCATTERED row order: ordinal i sits at image
+  // position img_pos(i) = 32 * ((i % T) * perm_mul % T) + i / T (T = n_tiles), so consecutive
+  // ordinals (overlapping chunks of one recording: near-duplicate vectors) land in tiles about
+  // 0.618 T apart, i.e. in different scan workgroups and lane lists, and a run of near-duplicates
+  // never crowds one lane list. perm_inv = perm_mul^-1 mod T.
+  int64_t perm_mul = 1;
+  int64_t perm_inv = 1;
 };
+
+namespace armi {
+// image position -> ordinal (may be >= n_rows for padding positions)
+__host__ __device__ inline int64_t img_to_ord(int64_t pos, int64_t T, int64_t perm_inv) {
+  const int64_t tau = pos >> 5;
+  return (pos & 31) * T + (tau * perm_inv) % T;
+}
+__host__ __device__ inline int64_t ord_to_img(int64_t i, int64_t T, int64_t perm_mul) {
+  return 32 * (((i % T) * perm_mul) % T) + i / T;
+}
+}  // namespace armi
 
 // Sparse store: a device inverted index built at create time from the caller's CSR (which may
 // be freed afterwards). Term t's postings (row, value) sit in [term_ptr[t], term_ptr[t+1]),

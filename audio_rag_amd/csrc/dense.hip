@@ -350,13 +350,22 @@ __device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
-template <int DIM, bool QI8>
+// COLLECT: the second pass for the queries the merge could not certify (replaces the per-query
+// exhaustive exact scan of round 2). The call's uncertified queries, in query order, are dealt
+// 64 per block; each gets its merge-computed threshold thr[q] = (k-th exact key found) - delta,
+// rounded down. Every row whose key (the same upper bound as the scan's, exact <= key + delta)
+// reaches it is appended to the query's list: a row of the true top-k has exact >= k-th found,
+// hence key >= thr, so the list holds the whole top-k whatever the corpus looks like (runs of
+// near-duplicates, one-ulp neighbours, exact duplicates). dense_collect_merge_kernel rescores it.
+template <int DIM, bool QI8, bool COLLECT>
 __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
-    int guard) {
+    int guard, const uint32_t* __restrict__ flags, const float* __restrict__ thr,
+    int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap) {
+  static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
   constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
   constexpr int DEPTH = GROUPS % 4 == 0 ? 4 : 2;  // groups in flight per lane
@@ -368,18 +377,56 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   }
   if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
   const int q0 = qb * kQB;
-  const int nq = min(kQB, q_stride - q0);
+  int nq = min(kQB, q_stride - q0);
   const uint16_t* __restrict__ queries = queries_all + (size_t)q0 * DIM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
   float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
   float* qscale = qnorm + kQB;  // [kQB] t_q (QI8)
   float* qerr = qscale + kQB;   // [kQB] e_q (QI8); [8][kQB] norm partials (fp16 queries)
+  int32_t* qsel = reinterpret_cast<int32_t*>(qerr + kQB * (kThreads / kQB));  // [kQB] COLLECT
+  float* qthr = reinterpret_cast<float*>(qsel + kQB);                        // [kQB] COLLECT
+  int32_t* wcnt = reinterpret_cast<int32_t*>(qthr + kQB);                    // [kWaves]
 
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
+  if constexpr (COLLECT) {
+    // this block's slice [q0, q0 + 64) of the ordered list of uncertified queries
+    for (int e = threadIdx.x; e < kQB; e += kThreads) {
+      qsel[e] = 0;
+      qthr[e] = __builtin_inff();
+    }
+    int base = 0;
+    for (int c0 = 0; c0 < q_stride; c0 += kThreads) {
+      const int q = c0 + (int)threadIdx.x;
+      const bool u = q < q_stride && !(flags[q] & ARMI_FLAG_CERTIFIED);
+      const uint64_t bal = __ballot(u);
+      if (lane == 0) wcnt[wave] = __popcll(bal);
+      __syncthreads();
+      int pre = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const int c = wcnt[w];
+        pre += w < wave ? c : 0;
+        tot += c;
+      }
+      const int p = base + pre + __popcll(bal & ((1ull << lane) - 1ull));
+      if (u && p >= q0 && p < q0 + kQB) {
+        qsel[p - q0] = q;
+        qthr[p - q0] = thr[q];
+      }
+      base += tot;
+      __syncthreads();
+    }
+    nq = min(kQB, base - q0);
+    if (nq <= 0) return;  // workgroup-uniform
+  }
+  auto qrow = [&](int q) -> const uint16_t* {
+    if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
+    return queries + (size_t)q * DIM;
+  };
   const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
   int64_t t = t_begin + wave;
@@ -414,8 +461,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       const int sh = sh0 + (kThreads / kQB) * i;
       const int s = sh >> 1, hh = sh & 1;
       const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
-      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off)
-                    : u32x4{0u, 0u, 0u, 0u};
+      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(qrow(q) + off) : u32x4{0u, 0u, 0u, 0u};
     }
     float ss = 0.0f;
 #pragma unroll
@@ -503,6 +549,14 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   }
   __syncthreads();
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
+  float th0 = __builtin_inff(), th1 = __builtin_inff();
+  int qi0 = 0, qi1 = 0;
+  if constexpr (COLLECT) {
+    th0 = qthr[r];
+    th1 = qthr[32 + r];
+    qi0 = qsel[r];
+    qi1 = qsel[32 + r];
+  }
   float qt0 = 1.0f, qt1 = 1.0f, qe0 = 0.0f, qe1 = 0.0f;
   if constexpr (QI8) {
     qt0 = qscale[r]; qt1 = qscale[32 + r];
@@ -615,6 +669,25 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         mx1 = fmaxf(mx1, x1[j]);
       }
       const int32_t rbase = (int32_t)row0 + 4 * h;
+      if constexpr (COLLECT) {
+        // append every image position whose key reaches the query's threshold (NaN keys of
+        // invalid / filtered rows never do)
+        if (__any(mx0 >= th0 || mx1 >= th1)) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int32_t pos = rbase + (j & 3) + 8 * (j >> 2);
+            if (x0[j] >= th0) {
+              const int s = atomicAdd(col_cnt + qi0, 1);
+              if (s < col_cap) col_list[(size_t)qi0 * col_cap + s] = pos;
+            }
+            if (x1[j] >= th1) {
+              const int s = atomicAdd(col_cnt + qi1, 1);
+              if (s < col_cap) col_list[(size_t)qi1 * col_cap + s] = pos;
+            }
+          }
+        }
+        continue;
+      }
       if (__any(mx0 > s0[kLaneList - 1])) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -642,6 +715,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     }
   }
 
+  if constexpr (COLLECT) return;
   // 2. Workgroup merge (as dense_scan_kernel; the query image is dead: overlay it).
   __syncthreads();
   float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][64]
@@ -691,7 +765,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
 template <int DIM>
 constexpr int scan_i8_lds_bytes() {
-  return scan_lds_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB);
+  return scan_lds_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB) + kQB * 8 + kWaves * 4;
 }
 
 // Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
@@ -2141,15 +2215,94 @@ __device__ __forceinline__ float from_ord_key(uint32_t k) {
 constexpr int kSelCap = 1024;  // kept entries per query; overflow -> uncertified (exact fallback)
 constexpr int kRescoreBatch = 8;
 
+// Exact keys of 8 rows at once by one wave: each row's inverse norm is loaded with the row (same
+// round trip), and the 8 per-lane partial dots are reduced together (a halving butterfly: 10 int64
+// shuffles for 8 rows instead of 48). rr[j] = ordinal of row j or -1. Lane 8r (r = 0..7) ends
+// with row r's exact key in `key` (-inf for rr[r] < 0) and its ordinal in `row` (integer sums:
+// any order gives the same bits).
+template <int DIM>
+__device__ __forceinline__ void exact_keys8(const int32_t (&qf)[DIM / 64],
+                                            const uint16_t* __restrict__ rows,
+                                            const double* __restrict__ inv_norm,
+                                            const int32_t (&rr)[8], int lane, double& key,
+                                            int32_t& row) {
+  u32x2 raw[8][DIM / 256];
+  double inv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int32_t src = rr[j] >= 0 ? rr[j] : 0;
+    load_raw<DIM>(rows + (size_t)src * DIM, lane, raw[j]);
+    inv[j] = inv_norm[src];
+  }
+  int64_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int32_t xf[DIM / 64];
+    raw_to_fixed<DIM>(raw[j], xf);
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)xf[i];
+    v[j] = acc;
+  }
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {  // lanes with bit 5 keep rows 4..7, the others rows 0..3
+    const int64_t mine = b5 ? v[4 + m] : v[m];
+    const int64_t give = b5 ? v[m] : v[4 + m];
+    v[m] = mine + __shfl_xor(give, 32);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int64_t mine = b4 ? v[2 + m] : v[m];
+    const int64_t give = b4 ? v[m] : v[2 + m];
+    v[m] = mine + __shfl_xor(give, 16);
+  }
+  int64_t dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
+  dot += __shfl_xor(dot, 4);
+  dot += __shfl_xor(dot, 2);
+  dot += __shfl_xor(dot, 1);
+  const int r = (lane >> 3) & 7;  // = 4 b5 + 2 b4 + b3
+  row = -1;
+  double myinv = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j == r) {
+      row = rr[j];
+      myinv = inv[j];
+    }
+  }
+  key = row >= 0 ? (double)dot * myinv : kNegInfD;
+}
+
+// Ordinal of a candidate row: the int8 pass reports image positions (scattered order,
+// armi_index.h), the fp16 passes ordinals (perm_T == 0).
+__device__ __forceinline__ int32_t cand_ordinal(int32_t row, int64_t perm_T, int64_t perm_inv) {
+  return perm_T ? (int32_t)armi::img_to_ord(row, perm_T, perm_inv) : row;
+}
+
+// Largest float <= x (x finite or infinite).
+__device__ __forceinline__ float f32_round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) {  // one ulp toward -inf (f is finite here)
+    const uint32_t u = __float_as_uint(f);
+    f = f > 0.0f ? __uint_as_float(u - 1u) : (f == 0.0f ? -1.17549435e-38f : __uint_as_float(u + 1u));
+  }
+  return f;
+}
+
+// sel_col (J) / sel_rank (r): t0 = the r-th largest of the workgroup lists' J-th entries. r lists
+// hold >= J entries >= t0 each, so the pool holds >= r J >= kc entries >= t0 and its kc-th best is
+// >= t0 (host: the smallest J with r = ceil(kc / J) <= n_wg; with r > n_wg, t0 = -inf).
 template <int DIM>
 __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
     const float* __restrict__ cand_bound, int n_wg, int q_stride, const uint16_t* __restrict__ rows,
     const double* __restrict__ inv_norm, const uint16_t* __restrict__ queries,
-    double* __restrict__ inv_q_out, double* __restrict__ qnorm_out, int k, int kc,
-    int64_t ordinal_base, float* __restrict__ out_scores, int64_t* __restrict__ out_ids,
-    double* __restrict__ out_rank, int32_t* __restrict__ out_count,
-    uint32_t* __restrict__ out_flags) {
+    double* __restrict__ inv_q_out, double* __restrict__ qnorm_out, int k, int kc, int sel_col,
+    int sel_rank, int64_t perm_T, int64_t perm_inv, int64_t ordinal_base,
+    float* __restrict__ out_scores, int64_t* __restrict__ out_ids, double* __restrict__ out_rank,
+    int32_t* __restrict__ out_count, uint32_t* __restrict__ out_flags, float* __restrict__ thr_out,
+    int32_t* __restrict__ col_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* skey = reinterpret_cast<float*>(smem);                              // [kSelCap]
   int32_t* srow = reinterpret_cast<int32_t*>(smem + kSelCap * 4);            // [kSelCap]
@@ -2204,7 +2357,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #pragma unroll
   for (int j = 0; j < kFilterBatch; ++j) {
     const int e = tid + j * kDenseMergeThreads;
-    if (e < pool && e % kKW == 0) umax[e / kKW] = ord_key(kk[j]);
+    if (e < pool && e % kKW == sel_col - 1) umax[e / kKW] = ord_key(kk[j]);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
@@ -2223,14 +2376,14 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
       u[i] = g < n_wg ? umax[g] : ord_key(kNegInf);
     }
     float t0 = kNegInf;
-    if (n_wg >= kc) {
-      uint32_t prefix = 0;  // largest v with #{u >= v} >= kc, i.e. the kc-th largest key
+    if (n_wg >= sel_rank) {
+      uint32_t prefix = 0;  // largest v with #{u >= v} >= r, i.e. the r-th largest key
       for (int bit = 31; bit >= 0; --bit) {
         const uint32_t cand = prefix | (1u << bit);
         int cnt = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(u[i] >= cand));
-        if (cnt >= kc) prefix = cand;
+        if (cnt >= sel_rank) prefix = cand;
       }
       t0 = from_ord_key(prefix);
     }
@@ -2333,69 +2486,25 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (n_keep > 64 && n_keep <= 4 * 64 && kc <= 64) bound = fmaxf(bound, red[10]);
   if (kc < n2) bound = fmaxf(bound, skey[kc]);
 
-  // exact rescore of the kc best, kRescoreBatch rows in flight per wave; each row's inverse norm
-  // is loaded with the row (same round trip), and the 8 per-lane partial dots are reduced
-  // together (a halving butterfly: 10 int64 shuffles for 8 rows instead of 48); lane 8r ends
-  // with row r's exact dot (integer sums: any order gives the same bits).
-  static_assert(kRescoreBatch == 8, "the butterfly below reduces 8 rows");
+  // exact rescore of the kc best, kRescoreBatch rows in flight per wave (exact_keys8)
+  static_assert(kRescoreBatch == 8, "exact_keys8 reduces 8 rows");
   constexpr int kMW = kDenseMergeThreads / 64;
   const int per_wave = (kc + kMW - 1) / kMW;
   for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
-    u32x2 raw[kRescoreBatch][DIM / 256];
     int32_t rr[kRescoreBatch];
-    double inv[kRescoreBatch];
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
       const int c = wave + kMW * (i0 + j);
       const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
-      rr[j] = live ? srow[c] : -1;
-#if defined(ARMI_PROBE_BUILD) && defined(ARMI_MERGE_ABL) && ARMI_MERGE_ABL == 1
-      load_raw<DIM>(rows, lane, raw[j]);  // probe: every rescore load hits one cached row
-#else
-      load_raw<DIM>(rows + (size_t)(live ? rr[j] : 0) * DIM, lane, raw[j]);
-#endif
-      inv[j] = inv_norm[live ? rr[j] : 0];
+      rr[j] = live ? cand_ordinal(srow[c], perm_T, perm_inv) : -1;
     }
-    int64_t v[kRescoreBatch];
-#pragma unroll
-    for (int j = 0; j < kRescoreBatch; ++j) {
-      int32_t xf[DIM / 64];
-      raw_to_fixed<DIM>(raw[j], xf);
-      int64_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)xf[i];
-      v[j] = acc;
-    }
-    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {  // lanes with bit 5 keep rows 4..7, the others rows 0..3
-      const int64_t mine = b5 ? v[4 + m] : v[m];
-      const int64_t give = b5 ? v[m] : v[4 + m];
-      v[m] = mine + __shfl_xor(give, 32);
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int64_t mine = b4 ? v[2 + m] : v[m];
-      const int64_t give = b4 ? v[m] : v[2 + m];
-      v[m] = mine + __shfl_xor(give, 16);
-    }
-    int64_t dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
-    dot += __shfl_xor(dot, 4);
-    dot += __shfl_xor(dot, 2);
-    dot += __shfl_xor(dot, 1);
-    const int r = (lane >> 3) & 7;  // = 4 b5 + 2 b4 + b3
-    int32_t myrow = -1;
-    double myinv = 0.0;
-#pragma unroll
-    for (int j = 0; j < kRescoreBatch; ++j) {
-      if (j == r) {
-        myrow = rr[j];
-        myinv = inv[j];
-      }
-    }
+    double key;
+    int32_t myrow;
+    exact_keys8<DIM>(qf, rows, inv_norm, rr, lane, key, myrow);
+    const int r = (lane >> 3) & 7;
     if ((lane & 7) == 0 && i0 + r < per_wave) {
       const int c = wave + kMW * (i0 + r);
-      rkey[c] = myrow >= 0 ? (double)dot * myinv : kNegInfD;
+      rkey[c] = key;
       rord[c] = myrow >= 0 ? ordinal_base + myrow : kNoOrd;
     }
   }
@@ -2421,11 +2530,15 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
   bool certified;
   int n_out;
+  const double delta =
+      (kDeltaSafety * (double)DIM * (1.0 / 16777216.0) + kEncodeSlack) * qnorm_real;
+  // second-pass threshold: every row of the true top-k has exact >= this k-th exact key (found
+  // rows are real rows), hence int8 key >= kth - delta; fewer than k valid rows: collect them all
+  float thr = kNegInf;
   if (n_valid >= k) {
     const double kth = rkey[k - 1] * (1.0 / 16777216.0);
-    const double delta =
-        (kDeltaSafety * (double)DIM * (1.0 / 16777216.0) + kEncodeSlack) * qnorm_real;
     certified = kth > (double)bound + delta;
+    thr = f32_round_down(kth - delta);
     n_out = k;
   } else {
     certified = (bound == kNegInf);
@@ -2449,10 +2562,120 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (lane == 0) {
     out_count[qg] = certified ? n_out : 0;
     out_flags[qg] = certified ? ARMI_FLAG_CERTIFIED : 0u;
+    thr_out[qg] = certified ? __builtin_inff() : thr;
+    col_cnt[qg] = 0;
   }
 }
 
 constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16;
+
+// Second-pass merge, one workgroup per query (certified queries exit at once): exact keys of the
+// rows dense_scan_i8_kernel<COLLECT> appended (image positions -> ordinals), top-k by (key desc,
+// ordinal asc). The list holds every row of the true top-k (see the collect pass), so this top-k
+// is the exact answer. More appends than the list holds (> cap rows within delta + the int8 slack
+// of the k-th key: a pathological pile of duplicates) -> this workgroup scores every row itself.
+// Rows go through LDS 512 at a time: [0, 512) the best so far, [512, 1024) the next chunk, one
+// bitonic sort per chunk; a list of <= 512 rows is scored and sorted once.
+constexpr int kColChunk = 512;
+constexpr size_t kColMergeLds = 2 * kColChunk * 16;
+
+template <int DIM>
+__global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel(
+    const int32_t* __restrict__ col_cnt, const int32_t* __restrict__ col_list, int col_cap,
+    int64_t perm_T, int64_t perm_inv, const uint16_t* __restrict__ rows,
+    const double* __restrict__ inv_norm, const int64_t* __restrict__ norm2,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, const uint16_t* __restrict__ queries,
+    const double* __restrict__ inv_q, int k, int64_t ordinal_base, float* __restrict__ out_scores,
+    int64_t* __restrict__ out_ids, double* __restrict__ out_rank, int32_t* __restrict__ out_count,
+    uint32_t* __restrict__ flags) {
+  const int qg = blockIdx.x;
+  if (flags[qg] & ARMI_FLAG_CERTIFIED) return;  // workgroup-uniform
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* key = reinterpret_cast<double*>(smem);                            // [2 * kColChunk]
+  int64_t* ord = reinterpret_cast<int64_t*>(smem + 2 * kColChunk * 8);       // [2 * kColChunk]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = armi::wave_id();
+  const int cnt = col_cnt[qg];
+  const bool exhaustive = cnt > col_cap;
+  const int64_t n = exhaustive ? n_rows : cnt;
+  for (int e = tid; e < 2 * kColChunk; e += kDenseMergeThreads) {
+    key[e] = kNegInfD;
+    ord[e] = kNoOrd;
+  }
+  int32_t qf[DIM / 64];
+  load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
+  const int32_t* list = col_list + (size_t)qg * col_cap;
+  const bool single = n <= kColChunk;
+  constexpr int kPerWave = kColChunk / (kDenseMergeThreads / 64);  // 64 rows per wave and chunk
+  for (int64_t c0 = 0; c0 < n; c0 += kColChunk) {
+    const int base = single ? 0 : kColChunk;
+    const int m = (int)min<int64_t>(kColChunk, n - c0);
+    __syncthreads();  // the previous sort is done with [base, base + kColChunk)
+    for (int b = 0; b < kPerWave; b += 8) {
+      int32_t rr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = kPerWave * wave + b + j;
+        int32_t o = -1;
+        if (e < m) {
+          if (exhaustive) {
+            const int64_t row = c0 + e;
+            const bool on = norm2[row] >= 0 &&
+                            (!row_mask || ((row_mask[row >> 6] >> (row & 63)) & 1ull));
+            o = on ? (int32_t)row : -1;
+          } else {
+            o = cand_ordinal(list[c0 + e], perm_T, perm_inv);
+          }
+        }
+        rr[j] = o;
+      }
+      double kk;
+      int32_t myrow;
+      exact_keys8<DIM>(qf, rows, inv_norm, rr, lane, kk, myrow);
+      if ((lane & 7) == 0) {
+        const int e = base + kPerWave * wave + b + ((lane >> 3) & 7);
+        key[e] = kk;
+        ord[e] = myrow >= 0 ? ordinal_base + myrow : kNoOrd;
+      }
+    }
+    armi::lds_sort_rank_desc(key, ord,
+                             single ? armi::pow2_at_least(m > k ? m : k) : 2 * kColChunk);
+  }
+  if (wave != 0) return;
+  int n_valid = 0;
+  for (int c = lane; c < k; c += 64) n_valid += ord[c] != kNoOrd;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
+  const double iq = inv_q[qg];
+  for (int c = lane; c < k; c += 64) {
+    const size_t o = (size_t)qg * k + c;
+    const bool v = ord[c] != kNoOrd;
+    out_scores[o] = v ? (float)(key[c] * iq) : kNegInf;
+    out_ids[o] = v ? ord[c] : -1;
+    out_rank[o] = v ? key[c] : kNegInfD;
+  }
+  if (lane == 0) {
+    out_count[qg] = n_valid;
+    flags[qg] = ARMI_FLAG_FALLBACK;
+  }
+}
+
+// Int8 image order of a row filter: bit p of the output = bit img_to_ord(p) of the caller's
+// ordinal mask (0 for padding positions). One wave per 64 image positions.
+__global__ __launch_bounds__(256) void mask_to_img_kernel(const uint64_t* __restrict__ mask,
+                                                          int64_t n_rows, int64_t T,
+                                                          int64_t perm_inv,
+                                                          uint64_t* __restrict__ out) {
+  const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool bit = false;
+  if (pos < T * 32) {
+    const int64_t i = armi::img_to_ord(pos, T, perm_inv);
+    bit = i < n_rows && ((mask[i >> 6] >> (i & 63)) & 1ull);
+  }
+  const uint64_t b = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && pos < T * 32) out[pos >> 6] = b;
+}
 
 // Exhaustive exact scan: grid (n_blocks, nq); block b scores rows [b*rpb, (b+1)*rpb) and keeps
 // its best `cap` (power of two) entries. Queries whose flag says CERTIFIED are skipped.
@@ -2716,10 +2939,11 @@ GemmForm gemm_form() {
   return f;
 }
 
-// The 64-query scan reads the int8 filter image (dense_scan_i8_kernel) for k <= 16, with the
+// The 64-query scan reads the int8 filter image (dense_scan_i8_kernel) for k <= 64, with the
 // merge rescoring the kc_i8 best upper bounds; ARMI_DENSE_FILTER=fp16 forces the fp16 scan (A/B).
-// Beyond k = 16 the looser keys would need rescoring pools past the merge's 256 rows.
-constexpr int kI8MaxK = 16;
+// k = 40 is the reference's default hybrid prefetch (QueryPipeline.query -> search(top_k=20) ->
+// dense prefetch limit 2 * 20, src/audio_rag/retrieval/qdrant.py:281-293).
+constexpr int kI8MaxK = 64;
 bool use_i8_filter(const armi_index* idx, int k) {
   static const bool off = [] {
     const char* e = getenv("ARMI_DENSE_FILTER");
@@ -2745,11 +2969,26 @@ bool use_q8(int k) {
 // 0.255 vs 0.273 ms with 128, tools/probes/kc_ab.sh); a query whose k-th cosine sits among more
 // near-equal bounds takes the exact fallback, so only its time depends on this choice.
 // ARMI_DENSE_KC=64|128 forces either (A/B).
+// k = 40 at 1M random unit rows: ~110 rows reach the 40th cosine (bound slack 0.26 sigma at
+// 3.94 sigma), so 256; the collect pass catches whatever a smaller pool misses.
 int kc_i8(int k) {
   static const int forced = getenv("ARMI_DENSE_KC") ? atoi(getenv("ARMI_DENSE_KC")) : 0;
-  if (forced == 64 || forced == 128) return forced;
-  return use_q8(k) ? 128 : (k <= 10 ? 64 : 128);
+  if (forced == 64 || forced == 128 || forced == 256) return forced;
+  return use_q8(k) ? 128 : (k <= 10 ? 64 : (k <= 20 ? 128 : 256));
 }
+
+// Threshold column of the merge's pool selection (dense_merge_kernel): the smallest J (power of
+// two, <= kKW) with r = ceil(kc / J) <= n_wg.
+void merge_select(int kc, int n_wg, int& col, int& rank) {
+  int j = 1;
+  while (j < kKW && (kc + j - 1) / j > n_wg) j <<= 1;
+  col = j;
+  rank = (kc + j - 1) / j;
+}
+
+// Per-query capacity of the collect pass's row list (beyond it the second-pass merge scores every
+// row itself: a pathological pile of > 4096 rows within the bound slack of the k-th key).
+constexpr int kCollectCap = 4096;
 
 struct GemmPlan {
   int n_qb = 0;
@@ -2798,6 +3037,10 @@ struct Workspace {
   double* qnorm;
   double* ex_key;
   int64_t* ex_ord;
+  float* thr;          // [nq] collect threshold (+inf: certified)
+  int32_t* col_cnt;    // [nq] rows appended by the collect pass
+  int32_t* col_list;   // [nq][kCollectCap] image positions
+  uint64_t* mask_img;  // row filter in int8 image order
   size_t bytes;
 };
 
@@ -2809,12 +3052,18 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.cand_key = cv.take<float>((size_t)n_wg * nq * kKW);
     w.cand_row = cv.take<int32_t>((size_t)n_wg * nq * kKW);
     w.cand_bound = cv.take<float>((size_t)n_wg * nq);
+    w.thr = cv.take<float>(nq);
+    w.col_cnt = cv.take<int32_t>(nq);
+    w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
+    w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
-  const ExactPlan ep = plan_exact(idx, k);
-  w.ex_key = cv.take<double>((size_t)nq * ep.n_blocks * ep.cap);
-  w.ex_ord = cv.take<int64_t>((size_t)nq * ep.n_blocks * ep.cap);
+  if (!fast) {
+    const ExactPlan ep = plan_exact(idx, k);
+    w.ex_key = cv.take<double>((size_t)nq * ep.n_blocks * ep.cap);
+    w.ex_ord = cv.take<int64_t>((size_t)nq * ep.n_blocks * ep.cap);
+  }
   w.bytes = cv.off + 256;
   return w;
 }
@@ -2859,6 +3108,16 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   const ScanPlan sp = plan_scan(idx, k, nq);
   int n_wg = sp.n_wg;
   int kc = sp.kc;
+  const int64_t T = std::max<int64_t>(idx->n_tiles, 1);
+  // the int8 passes (first pass and collect pass) read the filter in image order
+  const uint64_t* mask_i8 = nullptr;
+  if (row_mask) {
+    mask_to_img_kernel<<<dim3((unsigned)((T * 32 + 255) / 256)), dim3(256), 0, stream>>>(
+        row_mask, idx->n_rows, T, idx->perm_inv, w.mask_img);
+    ARMI_LAUNCHED("mask_to_img_kernel");
+    mask_i8 = w.mask_img;
+  }
+  bool i8_first = false;
   if (use_gemm_scan(nq)) {
     const GemmPlan gp = plan_gemm(idx, nq);
     n_wg = gp.n_ranges;
@@ -2956,15 +3215,17 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (int rc = tl.end()) return rc;
   } else if (use_i8_filter(idx, k)) {
     kc = kc_i8(k);
+    i8_first = true;
     const bool qi8 = use_q8(k);
-    auto kern = qi8 ? dense_scan_i8_kernel<DIM, true> : dense_scan_i8_kernel<DIM, false>;
-    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, true>, scan_i8_lds_bytes<DIM>())) return rc;
-    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, false>, scan_i8_lds_bytes<DIM>())) return rc;
+    auto kern = qi8 ? dense_scan_i8_kernel<DIM, true, false> : dense_scan_i8_kernel<DIM, false, false>;
+    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, true, false>, scan_i8_lds_bytes<DIM>())) return rc;
+    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, false, false>, scan_i8_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
-        idx->rows8, idx->a32, idx->e32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
+        idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
+        nullptr, nullptr, nullptr, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -2981,13 +3242,34 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
   ARMI_REQUIRE(n_wg >= 1 && n_wg * kKW <= kMaxPool,
                "dense merge: the candidate pool must fit one filter round (<= 256 lists)");
+  int sel_col = 1, sel_rank = kc;
+  merge_select(kc, n_wg, sel_col, sel_rank);
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
-      w.inv_q, w.qnorm, k, kc, idx->ordinal_base, out_scores, out_ids, out_rank, out_count,
-      out_flags);
+      w.inv_q, w.qnorm, k, kc, sel_col, sel_rank, i8_first ? T : 0, idx->perm_inv,
+      idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt);
   ARMI_LAUNCHED("dense_merge_kernel");
-  return launch_exact<DIM>(idx, queries, nq, k, row_mask, out_scores, out_ids, out_rank,
-                           out_count, out_flags, 1, w, stream);
+  // second pass for the uncertified queries (both kernels exit at once when every query of the
+  // call is certified): int8 collect over the whole shard, then exact rescore of the lists
+  {
+    const ScanPlan cp = plan_scan(idx, k, 1);  // one block's ranges; blocks of one range share an XCD
+    const int n_qb = (nq + kQB - 1) / kQB;
+    const int grid = n_qb == 1 ? cp.n_wg : n_qb * 8 * ((cp.n_wg + 7) / 8);
+    auto kern = dense_scan_i8_kernel<DIM, false, true>;
+    if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
+    kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
+        idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
+        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, out_flags, w.thr, w.col_cnt,
+        w.col_list, kCollectCap);
+    ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
+  }
+  if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
+  dense_collect_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kColMergeLds, stream>>>(
+      w.col_cnt, w.col_list, kCollectCap, T, idx->perm_inv, idx->rows, idx->inv_norm, idx->norm2,
+      row_mask, idx->n_rows, queries, w.inv_q, k, idx->ordinal_base, out_scores, out_ids,
+      out_rank, out_count, out_flags);
+  ARMI_LAUNCHED("dense_collect_merge_kernel");
+  return ARMI_OK;
 }
 
 template <typename F>

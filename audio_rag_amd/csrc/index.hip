@@ -57,12 +57,14 @@ __global__ __launch_bounds__(256) void row_norms_kernel(const uint16_t* __restri
   }
 }
 
-// One wave per row: the int8 filter image. s = max |x_i| / 127 (fp32), q_i = rint(x_i / s),
-// a32 = s / |x|, e32 = ||x - s q||_2 / |x| rounded up (the quantisation term of the filter's
-// score bound: |q.(x - s q)| / |x| <= |q| e32 by Cauchy-Schwarz).
+// One wave per image position: the int8 filter image. s = max |x_i| / 127 (fp32),
+// q_i = rint(x_i / s), a32 = s / |x|, e32 = ||x - s q||_2 / |x| rounded up (the quantisation term
+// of the filter's score bound: |q.(x - s q)| / |x| <= |q| e32 by Cauchy-Schwarz). Image position
+// pos holds ordinal img_to_ord(pos) (armi_index.h: the scattered order).
 template <int DIM>
 __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restrict__ rows,
                                                          int64_t n_rows, int64_t n_padded,
+                                                         int64_t n_tiles, int64_t perm_inv,
                                                          const double* __restrict__ inv_norm,
                                                          const int64_t* __restrict__ norm2,
                                                          int8_t* __restrict__ rows8,
@@ -70,18 +72,20 @@ __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restr
                                                          float* __restrict__ e32) {
   constexpr int E = DIM / 64;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + armi::wave_id();
-  if (row >= n_padded) return;
-  // tile-blocked layout: 16-B chunk c of row r sits at (r / 32) * 32 * DIM + c * 512 + (r % 32) * 16,
-  // so the scan's wave-wide chunk loads (32 rows x 16 B per lane half) are contiguous 512-B runs
-  int8_t* tile = rows8 + (row >> 5) * 32 * DIM + (row & 31) * 16;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + armi::wave_id();
+  if (pos >= n_padded) return;
+  const int64_t row = n_tiles > 0 ? armi::img_to_ord(pos, n_tiles, perm_inv) : n_rows;
+  // tile-blocked layout: 16-B chunk c of image row p sits at (p / 32) * 32 * DIM + c * 512 +
+  // (p % 32) * 16, so the scan's wave-wide chunk loads (32 rows x 16 B per lane half) are
+  // contiguous 512-B runs
+  int8_t* tile = rows8 + (pos >> 5) * 32 * DIM + (pos & 31) * 16;
   auto dst_at = [&](int i) -> int8_t& { return tile[(i >> 4) * 512 + (i & 15)]; };
   if (row >= n_rows || norm2[row] < 0) {  // padding or invalid: never a result
 #pragma unroll
     for (int i = 0; i < E; ++i) dst_at(lane + 64 * i) = 0;
     if (lane == 0) {
-      a32[row] = __builtin_nanf("");
-      e32[row] = 0.0f;
+      a32[pos] = __builtin_nanf("");
+      e32[pos] = 0.0f;
     }
     return;
   }
@@ -108,9 +112,30 @@ __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restr
   for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
   if (lane == 0) {
     const double inv = inv_norm[row] * 16777216.0;  // 1 / |x|
-    a32[row] = (float)((double)s * inv);
-    e32[row] = (float)(sqrt(err) * inv * (1.0 + 1.0 / 1048576.0)) ;
+    a32[pos] = (float)((double)s * inv);
+    e32[pos] = (float)(sqrt(err) * inv * (1.0 + 1.0 / 1048576.0)) ;
   }
+}
+
+int64_t gcd64(int64_t a, int64_t b) {
+  while (b) {
+    const int64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// Modular inverse of a mod m (gcd(a, m) = 1), extended Euclid.
+int64_t inv_mod(int64_t a, int64_t m) {
+  if (m == 1) return 0;
+  int64_t t = 0, nt = 1, r = m, nr = a % m;
+  while (nr) {
+    const int64_t q = r / nr;
+    int64_t tmp = t - q * nt; t = nt; nt = tmp;
+    tmp = r - q * nr; r = nr; nr = tmp;
+  }
+  return t < 0 ? t + m : t;
 }
 
 }  // namespace
@@ -138,6 +163,16 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
   hipError_t e = hipGetDeviceProperties(&prop, device);
   if (e != hipSuccess) { delete idx; return armi::hip_fail(e, "hipGetDeviceProperties"); }
   idx->num_cus = prop.multiProcessorCount;
+  // scattered image order: multiplier ~ 0.618 T, coprime with T (armi_index.h)
+  if (idx->n_tiles > 1) {
+    const int64_t T = idx->n_tiles;
+    int64_t p = std::max<int64_t>(1, (int64_t)((double)T * 0.6180339887498949));
+    while (gcd64(p, T) != 1) ++p;
+    idx->perm_mul = p % T;
+    idx->perm_inv = inv_mod(idx->perm_mul, T);
+  } else {
+    idx->perm_mul = idx->perm_inv = 1;
+  }
   const int64_t padded = std::max<int64_t>(idx->n_tiles * armi::TILE_ROWS, 1);
   e = hipMalloc(&idx->norm2, padded * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&idx->inv_norm, padded * sizeof(double));
@@ -157,7 +192,8 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
   if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "row_norms_kernel"); }
   auto filt = [&](auto D) {
     row_filter_kernel<decltype(D)::value><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
-        rows, n_rows, padded, idx->inv_norm, idx->norm2, idx->rows8, idx->a32, idx->e32);
+        rows, n_rows, padded, idx->n_tiles, idx->perm_inv, idx->inv_norm, idx->norm2, idx->rows8,
+        idx->a32, idx->e32);
   };
   switch (dim) {
     case 256: filt(std::integral_constant<int, 256>{}); break;

@@ -44,7 +44,13 @@ inline int64_t now_ns() {
 
 constexpr int kSlots = 3;           // batches in flight (GPU running / collected / collecting)
 constexpr int kMaxTerms = 256;      // sparse terms per query (armi_sparse_topk's limit)
-constexpr int64_t kRing = 1 << 20;  // result ring entries (tickets alive at once)
+// Result ring entries (tickets whose results stay readable): max(2^14, 64 * max_batch) rounded up
+// to a power of two, i.e. 3.9 MB of host memory at k = 10, max_batch 64 (include/armi.h).
+int64_t ring_entries(int max_batch) {
+  int64_t r = 1 << 14;
+  while (r < 64 * (int64_t)max_batch) r <<= 1;
+  return r;
+}
 
 struct Slot {
   int n = 0;                         // queries in the batch
@@ -127,6 +133,8 @@ struct armi_stream {
   std::atomic<int64_t> batches{0}, queries{0};
   std::thread dispatcher, completer;
   int device = 0;
+  int64_t ring_n = 0;                    // ring entries (a power of two)
+  std::atomic<int> active{0};            // callers inside submit / wait / stats / loadgen
 };
 
 namespace {
@@ -223,9 +231,9 @@ void completer_main(armi_stream* s) {
     const int64_t t = now_ns();
     for (int i = 0; i < sl.n; ++i) {
       const int64_t tk = sl.first_ticket + i;
-      Entry& e = s->ring[tk % kRing];
-      const size_t o = (size_t)(tk % kRing) * s->k;
-      if (status == ARMI_OK && s->sidx && s->nnz_of[tk % kRing] > 0) {
+      Entry& e = s->ring[tk % s->ring_n];
+      const size_t o = (size_t)(tk % s->ring_n) * s->k;
+      if (status == ARMI_OK && s->sidx && s->nnz_of[tk % s->ring_n] > 0) {
         // hybrid branch: the fused list, hit.score = the RRF score (rank holds it in fp64)
         const size_t f = (size_t)i * s->k;
         e.count = sl.h_f_count[i];
@@ -364,11 +372,12 @@ int create_impl(const armi_index* idx, const armi_sparse_index* sidx, int k, int
   s->device = idx->device;
   s->ws_bytes = armi_dense_workspace_bytes(idx, max_batch, s->kp);
   if (sidx) s->sws_bytes = armi_sparse_workspace_bytes(sidx, max_batch, s->kp);
-  s->ring = std::vector<Entry>(kRing);
-  s->nnz_of.assign(kRing, 0);
-  s->r_scores.assign((size_t)kRing * k, 0.f);
-  s->r_ids.assign((size_t)kRing * k, -1);
-  s->r_rank.assign((size_t)kRing * k, 0.0);
+  s->ring_n = ring_entries(max_batch);
+  s->ring = std::vector<Entry>(s->ring_n);
+  s->nnz_of.assign(s->ring_n, 0);
+  s->r_scores.assign((size_t)s->ring_n * k, 0.f);
+  s->r_ids.assign((size_t)s->ring_n * k, -1);
+  s->r_rank.assign((size_t)s->ring_n * k, 0.0);
   int rc = ARMI_OK;
   if (hipSetDevice(s->device) != hipSuccess ||
       hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -384,6 +393,26 @@ int create_impl(const armi_index* idx, const armi_sparse_index* sidx, int k, int
   s->completer = std::thread(completer_main, s);
   *out = s;
   return ARMI_OK;
+}
+
+// Counts a caller inside the server's entry points; armi_stream_destroy waits for the count to
+// drop to zero before it frees anything.
+struct Active {
+  armi_stream* s;
+  explicit Active(armi_stream* s_) : s(s_) { if (s) s->active.fetch_add(1); }
+  ~Active() { if (s) s->active.fetch_sub(1); }
+};
+
+// Stops the server: no new batches, every waiter and blocked submitter wakes and returns.
+void stop_impl(armi_stream* s) {
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->stop = true;
+  }
+  s->cv_dispatch.notify_all();
+  s->cv_complete.notify_all();
+  s->cv_space.notify_all();
+  s->cv_done.notify_all();
 }
 
 int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
@@ -412,9 +441,9 @@ int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
     }
     c.nnz += nnz;
     c.h_sp_ptr[c.n + 1] = c.nnz;
-    s->nnz_of[tk % kRing] = nnz;
+    s->nnz_of[tk % s->ring_n] = nnz;
   }
-  Entry& e = s->ring[tk % kRing];
+  Entry& e = s->ring[tk % s->ring_n];
   e.t_submit = now_ns();
   ++c.n;
   const bool wake = c.n == 1 || c.n == s->max_batch;
@@ -439,19 +468,37 @@ int armi_stream_create_hybrid(const armi_index* idx, const armi_sparse_index* si
   return create_impl(idx, sidx, k, rrf_k, max_batch, max_wait_us, out);
 }
 
+int armi_stream_stop(armi_stream* s) {
+  ARMI_REQUIRE(s, "armi_stream_stop: null server");
+  stop_impl(s);
+  return ARMI_OK;
+}
+
 int armi_stream_destroy(armi_stream* s) {
   if (!s) return ARMI_OK;
+  stop_impl(s);
+  // callers still inside wait / submit (woken by the stop) leave before anything is freed
+  while (s->active.load() > 0) {
+    {
+      std::lock_guard<std::mutex> g(s->mu);
+      s->cv_done.notify_all();
+      s->cv_space.notify_all();
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
   shutdown(s);
   delete s;
   return ARMI_OK;
 }
 
 int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
+  Active a(s);
   return submit_impl(s, query, nullptr, nullptr, 0, ticket);
 }
 
 int armi_stream_submit_hybrid(armi_stream* s, const uint16_t* query, const int32_t* sp_indices,
                               const float* sp_values, int nnz, int64_t* ticket) {
+  Active a(s);
   return submit_impl(s, query, sp_indices, sp_values, nnz, ticket);
 }
 
@@ -459,7 +506,8 @@ int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids
                      int32_t* count, int32_t* mode, double timeout_us) {
   ARMI_REQUIRE(s && count, "armi_stream_wait: null pointer argument");
   ARMI_REQUIRE(ticket >= 0, "armi_stream_wait: bad ticket");
-  Entry& e = s->ring[ticket % kRing];
+  Active a(s);
+  Entry& e = s->ring[ticket % s->ring_n];
   if (e.ticket.load(std::memory_order_acquire) != ticket) {
     std::unique_lock<std::mutex> lk(s->mu);
     const auto until = Clock::now() + std::chrono::nanoseconds((int64_t)(timeout_us * 1e3));
@@ -474,7 +522,7 @@ int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids
     }
   }
   if (e.status != ARMI_OK) return armi::fail(e.status, "armi_stream_wait: the batch failed");
-  const size_t o = (size_t)(ticket % kRing) * s->k;
+  const size_t o = (size_t)(ticket % s->ring_n) * s->k;
   if (scores) std::memcpy(scores, &s->r_scores[o], s->k * sizeof(float));
   if (ids) std::memcpy(ids, &s->r_ids[o], s->k * sizeof(int64_t));
   if (rank) std::memcpy(rank, &s->r_rank[o], s->k * sizeof(double));
@@ -485,6 +533,7 @@ int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids
 
 int armi_stream_stats(armi_stream* s, int64_t* batches, int64_t* queries) {
   ARMI_REQUIRE(s && batches && queries, "armi_stream_stats: null pointer argument");
+  Active a(s);
   *batches = s->batches.load();
   *queries = s->queries.load();
   return ARMI_OK;
@@ -497,14 +546,39 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* 
   ARMI_REQUIRE(s && queries && latency_us && elapsed_s && completed,
                "armi_stream_loadgen: null pointer argument");
   ARMI_REQUIRE(n_vectors >= 1, "armi_stream_loadgen: n_vectors < 1");
-  ARMI_REQUIRE(n_queries >= 1 && n_queries <= kRing / 2, "armi_stream_loadgen: n_queries range");
+  ARMI_REQUIRE(n_queries >= 1, "armi_stream_loadgen: n_queries < 1");
   ARMI_REQUIRE(qps > 0.0, "armi_stream_loadgen: qps must be > 0");
+  Active a(s);
   std::mt19937_64 rng(seed);
   std::exponential_distribution<double> gap(qps);
   std::vector<int64_t> tickets((size_t)n_queries);
+  std::atomic<int64_t> n_sub{0};
+  // results are collected in ticket order while arrivals continue, so only the tickets in flight
+  // (<= kSlots batches plus the collector's lag) need to stay in the result ring
+  int64_t t_last = 0, t_first = -1;
+  std::atomic<int> rc_col{ARMI_OK};
+  std::thread collector([&] {
+    int32_t cnt = 0;
+    for (int64_t i = 0; i < n_queries; ++i) {
+      while (n_sub.load(std::memory_order_acquire) <= i) {
+        if (rc_col.load() != ARMI_OK) return;
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
+      }
+      const int64_t tk = tickets[(size_t)i];
+      if (int rc = armi_stream_wait(s, tk, nullptr, nullptr, nullptr, &cnt, nullptr, 60e6)) {
+        rc_col.store(rc);
+        return;
+      }
+      const Entry& e = s->ring[tk % s->ring_n];
+      latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;
+      t_last = std::max(t_last, e.t_done);
+      if (t_first < 0) t_first = e.t_submit;
+    }
+  });
   const int64_t t0 = now_ns();
   double due = 0.0;  // seconds since t0
-  for (int64_t i = 0; i < n_queries; ++i) {
+  int rc = ARMI_OK;
+  for (int64_t i = 0; i < n_queries && rc == ARMI_OK && rc_col.load() == ARMI_OK; ++i) {
     due += gap(rng);
     const int64_t due_ns = t0 + (int64_t)(due * 1e9);
     for (;;) {  // open-loop arrivals: sleep to ~50 us before the due time, then spin
@@ -514,23 +588,15 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* 
     }
     const int64_t v = i % n_vectors;
     const int nnz = q_indptr ? q_indptr[v + 1] - q_indptr[v] : 0;
-    if (int rc = submit_impl(s, queries + (size_t)v * s->dim,
-                             q_indptr ? q_indices + q_indptr[v] : nullptr,
-                             q_indptr ? q_values + q_indptr[v] : nullptr, nnz,
-                             &tickets[(size_t)i]))
-      return rc;
+    rc = submit_impl(s, queries + (size_t)v * s->dim, q_indptr ? q_indices + q_indptr[v] : nullptr,
+                     q_indptr ? q_values + q_indptr[v] : nullptr, nnz, &tickets[(size_t)i]);
+    if (rc == ARMI_OK) n_sub.store(i + 1, std::memory_order_release);
   }
-  int64_t t_last = t0, t_first = -1;
-  int32_t cnt = 0;
-  for (int64_t i = 0; i < n_queries; ++i) {
-    if (int rc = armi_stream_wait(s, tickets[(size_t)i], nullptr, nullptr, nullptr, &cnt, nullptr,
-                                  60e6))
-      return rc;
-    const Entry& e = s->ring[tickets[(size_t)i] % kRing];
-    latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;
-    t_last = std::max(t_last, e.t_done);
-    if (t_first < 0) t_first = e.t_submit;
-  }
+  if (rc != ARMI_OK) rc_col.store(rc);  // stops the collector
+  collector.join();
+  if (rc != ARMI_OK) return rc;
+  if (rc_col.load() != ARMI_OK)
+    return armi::fail(rc_col.load(), "armi_stream_loadgen: waiting for a result failed");
   *elapsed_s = (double)(t_last - t_first) * 1e-9;
   *completed = n_queries;
   return ARMI_OK;

@@ -18,6 +18,7 @@ import logging
 import queue
 import threading
 import time
+import weakref
 from concurrent.futures import Future
 from dataclasses import dataclass, field
 
@@ -42,6 +43,35 @@ class _Request:
 
 def _filter_key(f: dict | None):
     return None if not f else tuple(sorted((k, repr(v)) for k, v in f.items()))
+
+
+def _sorted_terms(indices, values) -> tuple[np.ndarray, np.ndarray]:
+    """A query's sparse terms as the device search needs them: ascending unique int32 indices
+    (Qdrant stores sparse vectors sorted by index and rejects duplicates)."""
+    idx = np.asarray(indices, dtype=np.int64).reshape(-1)
+    val = np.asarray(values, dtype=np.float32).reshape(-1)
+    if idx.shape != val.shape:
+        raise RetrievalError("sparse query indices and values differ in length")
+    order = np.argsort(idx, kind="stable")
+    idx, val = idx[order], val[order]
+    if idx.size and (np.any(idx[1:] == idx[:-1]) or idx[0] < 0 or idx[-1] >= 2**31):
+        raise RetrievalError("sparse query indices must be unique non-negative int32")
+    return np.ascontiguousarray(idx, dtype=np.int32), np.ascontiguousarray(val)
+
+
+def _sorted_csr(indptr, indices, values) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """_sorted_terms for every row of a query CSR at once."""
+    indptr = np.asarray(indptr, dtype=np.int64)
+    idx = np.asarray(indices, dtype=np.int64)
+    val = np.asarray(values, dtype=np.float32)
+    row = np.repeat(np.arange(indptr.size - 1), np.diff(indptr))
+    order = np.lexsort((idx, row))
+    idx, val = idx[order], val[order]
+    if idx.size and (np.any((idx[1:] == idx[:-1]) & (row[1:] == row[:-1])) or idx.min() < 0
+                     or idx.max() >= 2**31):
+        raise RetrievalError("sparse query indices must be unique non-negative int32 per query")
+    return (np.ascontiguousarray(indptr, dtype=np.int32), np.ascontiguousarray(idx, dtype=np.int32),
+            np.ascontiguousarray(val))
 
 
 class QueryBatcher:
@@ -73,6 +103,8 @@ class QueryBatcher:
             raise RetrievalError("QueryBatcher is closed")
         fut: Future = Future()
         d = np.ascontiguousarray(dense, dtype=np.float16).reshape(-1)
+        if sparse is not None:
+            sparse = _sorted_terms(*sparse)
         self._q.put(_Request(d, sparse, filter_metadata, fut))
         return fut
 
@@ -180,7 +212,11 @@ class StreamServer:
     (qdrant.py:316-323); "hybrid" (a hybrid collection) answers a query that carries sparse
     terms by the hybrid branch (qdrant.py:272-298: prefetch 2k + 2k, RRF, hit.score = the RRF
     score) and one without by the dense branch, as search() chooses. Filters and the sparse-only
-    mode go through QueryBatcher."""
+    mode go through QueryBatcher.
+
+    Lifetime: the collection knows its open servers and closes them before it frees its device
+    indexes (ChunkCollection.close: delete_collection, load_collection, attach_collection); close()
+    stops the native server, waits for the callers still inside it, then destroys it."""
 
     def __init__(self, retriever: MI355XRetriever, collection_name: str | None = None,
                  top_k: int | None = None, max_batch: int = 64, max_wait_ms: float = 2.0,
@@ -199,6 +235,10 @@ class StreamServer:
         self.k = top_k or retriever.config.top_k
         self.dim = retriever.embedding_dim
         self._handle = _armi.ctypes.c_void_p()
+        self._lock = threading.Lock()
+        self._idle = threading.Condition(self._lock)
+        self._inflight = 0
+        self._closed = False
         if self.hybrid:
             _armi.call("armi_stream_create_hybrid", self.index.handle, self.sparse_index.handle,
                        self.k, retriever.config.rrf_k, max_batch, float(max_wait_ms) * 1e3,
@@ -206,6 +246,28 @@ class StreamServer:
         else:
             _armi.call("armi_stream_create", self.index.handle, self.k, max_batch,
                        float(max_wait_ms) * 1e3, _armi.ctypes.byref(self._handle))
+        self.collection.attach_server(self)
+        # QdrantRetriever.search applies score_threshold to legacy dense-only collections only
+        # (qdrant.py:331), as MI355XRetriever.search does
+        thr = retriever.config.score_threshold
+        self.threshold = thr if (not self.collection.hybrid and thr > 0) else None
+
+    def _call(self, fn: str, *args):
+        """One native call on the live server (refused once close() has begun)."""
+        with self._lock:
+            if self._closed:
+                raise RetrievalError("StreamServer is closed")
+            self._inflight += 1
+            h = self._handle
+        try:
+            return self._armi.call(fn, h, *args)
+        except self._armi.ArmiError as e:  # retriever failures surface as RetrievalError
+            raise RetrievalError(str(e)) from e
+        finally:
+            with self._lock:
+                self._inflight -= 1
+                if self._inflight == 0:
+                    self._idle.notify_all()
 
     def submit_arrays(self, dense: np.ndarray,
                       sparse: tuple[np.ndarray, np.ndarray] | None = None) -> int:
@@ -215,16 +277,13 @@ class StreamServer:
             raise RetrievalError(f"query has {q.size} components, the store {self.dim}")
         ticket = self._armi.ctypes.c_int64()
         if sparse is not None and self.hybrid and len(sparse[0]) > 0:
-            idx = np.ascontiguousarray(sparse[0], dtype=np.int32)
-            val = np.ascontiguousarray(sparse[1], dtype=np.float32)
+            idx, val = _sorted_terms(*sparse)
             if idx.size > 256:
                 raise RetrievalError("a sparse query may hold at most 256 terms")
-            self._armi.call("armi_stream_submit_hybrid", self._handle, q.ctypes.data,
-                            idx.ctypes.data, val.ctypes.data, idx.size,
-                            self._armi.ctypes.byref(ticket))
+            self._call("armi_stream_submit_hybrid", q.ctypes.data, idx.ctypes.data,
+                       val.ctypes.data, idx.size, self._armi.ctypes.byref(ticket))
         else:
-            self._armi.call("armi_stream_submit", self._handle, q.ctypes.data,
-                            self._armi.ctypes.byref(ticket))
+            self._call("armi_stream_submit", q.ctypes.data, self._armi.ctypes.byref(ticket))
         return ticket.value
 
     def submit(self, query: EmbeddingResult) -> int:
@@ -239,9 +298,9 @@ class StreamServer:
         ids = np.empty(self.k, dtype=np.int64)
         count = self._armi.ctypes.c_int32()
         mode = self._armi.ctypes.c_int32()
-        self._armi.call("armi_stream_wait", self._handle, ticket, scores.ctypes.data,
-                        ids.ctypes.data, rank.ctypes.data, self._armi.ctypes.byref(count),
-                        self._armi.ctypes.byref(mode), timeout * 1e6)
+        self._call("armi_stream_wait", ticket, scores.ctypes.data, ids.ctypes.data,
+                   rank.ctypes.data, self._armi.ctypes.byref(count),
+                   self._armi.ctypes.byref(mode), timeout * 1e6)
         return (rank if mode.value == 1 else scores), ids, count.value
 
     def result(self, ticket: int, timeout: float = 60.0) -> list[RetrievalResult]:
@@ -251,6 +310,8 @@ class StreamServer:
         scores, ids, c = self.raw_result(ticket, timeout)
         out = []
         for pid, score in zip(ids[:c].tolist(), scores[:c].tolist()):
+            if self.threshold is not None and score < self.threshold:
+                continue
             p = self.collection.payloads[pid]
             chunk = AudioChunk(text=p.get("text", ""), start=p.get("start", 0.0),
                                end=p.get("end", 0.0), speaker=p.get("speaker"),
@@ -263,8 +324,7 @@ class StreamServer:
 
     def stats(self) -> tuple[int, int]:
         b, q = self._armi.ctypes.c_int64(), self._armi.ctypes.c_int64()
-        self._armi.call("armi_stream_stats", self._handle, self._armi.ctypes.byref(b),
-                        self._armi.ctypes.byref(q))
+        self._call("armi_stream_stats", self._armi.ctypes.byref(b), self._armi.ctypes.byref(q))
         return b.value, q.value
 
     def loadgen(self, queries: np.ndarray, n_queries: int, qps: float, seed: int = 0,
@@ -280,20 +340,31 @@ class StreamServer:
         ptrs = (None, None, None)
         keep = None
         if sparse_csr is not None and self.hybrid:
-            keep = tuple(np.ascontiguousarray(a, dtype=t)
-                         for a, t in zip(sparse_csr, (np.int32, np.int32, np.float32)))
+            keep = _sorted_csr(*sparse_csr)
             if keep[0].size != q.shape[0] + 1:
                 raise ValueError("one CSR row per query vector is required")
+            if np.diff(keep[0]).max(initial=0) > 256:
+                raise RetrievalError("a sparse query may hold at most 256 terms")
             ptrs = tuple(a.ctypes.data for a in keep)
-        self._armi.call("armi_stream_loadgen", self._handle, q.ctypes.data, *ptrs, q.shape[0],
-                        n_queries, float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
-                        self._armi.ctypes.byref(done))
+        self._call("armi_stream_loadgen", q.ctypes.data, *ptrs, q.shape[0], n_queries,
+                   float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
+                   self._armi.ctypes.byref(done))
         return lat * 1e-6, el.value
 
     def close(self) -> None:
-        if self._handle and self._handle.value:
-            self._armi.call("armi_stream_destroy", self._handle)
-            self._handle = self._armi.ctypes.c_void_p()
+        with self._lock:
+            if self._closed:
+                return
+            self._closed = True
+            h = self._handle
+        if h and h.value:
+            # wake every caller blocked inside the server, let them leave, then free it
+            self._armi.call("armi_stream_stop", h)
+            with self._lock:
+                while self._inflight:
+                    self._idle.wait()
+            self._armi.call("armi_stream_destroy", h)
+        self._handle = self._armi.ctypes.c_void_p()
 
     def __enter__(self):
         return self

@@ -15,6 +15,7 @@ reference).
 from __future__ import annotations
 
 import threading
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -73,6 +74,7 @@ class ChunkCollection:
     _key_index: dict = field(default_factory=dict)   # metadata key -> (count, {canon: ordinals})
     _lock: threading.Lock = field(default_factory=threading.Lock)
     _frozen: bool = False
+    _servers: weakref.WeakSet = field(default_factory=weakref.WeakSet)  # open StreamServers
 
     @property
     def count(self) -> int:
@@ -239,7 +241,15 @@ class ChunkCollection:
                     sh.payloads)
         return coll
 
+    def attach_server(self, server) -> None:
+        """Registers a StreamServer over this collection's indexes: close() stops it first."""
+        self._servers.add(server)
+
     def close(self) -> None:
+        # the native servers' dispatcher threads launch searches on these indexes: stop them
+        # before the indexes are freed
+        for srv in list(self._servers):
+            srv.close()
         for ix in (self._dense, self._sparse):
             if ix is not None:
                 ix.close()

@@ -268,9 +268,15 @@ class MI355XRetriever(BaseRetriever):
         """Row b of a device TopK -> fresh RetrievalResult objects from the payload table
         (qdrant.py:334-346)."""
         coll = self._collections[resolved]
-        count = int(out.count[b].item())
-        ids = out.ids[b, :count].cpu().tolist()
-        scores = (out.rank if mode == "hybrid" else out.scores)[b, :count].cpu().tolist()
+        # one packed device-to-host copy (count, ids, scores as fp64: ordinals < 2^31 and fp32
+        # scores convert exactly) instead of three synchronising copies
+        sc = out.rank if mode == "hybrid" else out.scores
+        packed = torch.cat([out.count[b:b + 1].double(), out.ids[b].double(),
+                            sc[b].double()]).cpu().numpy()
+        k = out.ids.shape[1]
+        count = int(packed[0])
+        ids = packed[1:1 + count].astype(np.int64).tolist()
+        scores = packed[1 + k:1 + k + count].tolist()
         results = []
         for pid, score in zip(ids, scores):
             if threshold is not None and score < threshold:

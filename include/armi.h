@@ -183,6 +183,11 @@ int armi_stream_create(const armi_index* index, int k, int max_batch, double max
  * dense branch (dense top-k, cosine scores). k <= 120. Both indexes must outlive the server. */
 int armi_stream_create_hybrid(const armi_index* index, const armi_sparse_index* sparse, int k,
                               int rrf_k, int max_batch, double max_wait_us, armi_stream** out);
+/* Stops the server (no new batches; blocked submitters and waiters wake and return an error);
+ * the server stays allocated until armi_stream_destroy. */
+int armi_stream_stop(armi_stream* server);
+/* Stops the server, waits for every caller still inside submit / wait / stats / loadgen to
+ * return, then frees it. */
 int armi_stream_destroy(armi_stream* server);
 /* query: host fp16 [dim], copied before return; *ticket identifies its result. */
 int armi_stream_submit(armi_stream* server, const uint16_t* query, int64_t* ticket);
@@ -193,8 +198,10 @@ int armi_stream_submit_hybrid(armi_stream* server, const uint16_t* query,
                               int64_t* ticket);
 /* Blocks until the ticket's result is published (at most timeout_us), then copies its k
  * scores / ids / rank keys (each nullable), the valid count and the branch taken (mode:
- * 0 dense, 1 hybrid; nullable). Results stay readable until 2^20 later tickets have been
- * submitted. */
+ * 0 dense, 1 hybrid; nullable). Results stay readable until R later tickets have been
+ * submitted, R = max(2^14, 64 max_batch) rounded up to a power of two (the result ring: R k
+ * (4 + 8 + 8) B + 48 R B of host memory, 3.9 MB at k = 10, max_batch 64); an older ticket fails
+ * with "result overwritten". */
 int armi_stream_wait(armi_stream* server, int64_t ticket, float* scores, int64_t* ids,
                      double* rank, int32_t* count, int32_t* mode, double timeout_us);
 int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);
@@ -202,7 +209,8 @@ int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);
  * Poisson process at `qps` from one thread, query i = row (i % n_vectors) of `queries` (host
  * fp16 [n_vectors][dim]) with, when q_indptr is non-null, the sparse terms of CSR row
  * (i % n_vectors); latency_us[i] = completion - submit of query i; elapsed_s = last
- * completion - first submit. n_queries <= 2^19. */
+ * completion - first submit. Results are collected by a second thread while arrivals continue,
+ * so n_queries is unbounded. */
 int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, const int32_t* q_indptr,
                         const int32_t* q_indices, const float* q_values, int64_t n_vectors,
                         int64_t n_queries, double qps, uint64_t seed, double* latency_us,

@@ -97,3 +97,21 @@ def test_failures_reach_every_caller_and_close_is_final():
     qb.close()
     with pytest.raises(RetrievalError, match="closed"):
         qb.submit_arrays(_vec(1))
+
+
+def test_sparse_terms_sorted_and_validated():
+    import numpy as np
+
+    from audio_rag_amd.core.exceptions import RetrievalError
+    from audio_rag_amd.retrieval.batcher import _sorted_csr, _sorted_terms
+
+    idx, val = _sorted_terms([9, 3, 7], [0.9, 0.3, 0.7])
+    assert idx.tolist() == [3, 7, 9] and idx.dtype == np.int32
+    assert np.allclose(val, [0.3, 0.7, 0.9])
+    with pytest.raises(RetrievalError):
+        _sorted_terms([4, 4], [1.0, 2.0])
+    p, i, v = _sorted_csr([0, 3, 3, 5], [8, 2, 5, 1, 0], [8.0, 2.0, 5.0, 1.0, 0.0])
+    assert p.tolist() == [0, 3, 3, 5] and i.tolist() == [2, 5, 8, 0, 1]
+    assert v.tolist() == [2.0, 5.0, 8.0, 0.0, 1.0]
+    with pytest.raises(RetrievalError):
+        _sorted_csr([0, 2], [6, 6], [1.0, 1.0])

@@ -178,3 +178,73 @@ def test_stream_server_loadgen_and_filtered_edge(gpu, oracle_mod, store):
     want = oracle_mod.dense_topk(rows3, qd[:1], K)
     assert want.count[0] == 3
     assert [r.chunk.text for r in res] == [f"s{p}" for p in want.ids[0, :3]]
+
+
+def test_stream_server_survives_collection_delete_and_concurrent_close(gpu, oracle_mod, store):
+    """Deleting the collection under an open server stops the server first (no search on a freed
+    index); closing a server while another thread waits in it wakes that thread with an error
+    instead of freeing the memory under it."""
+    import time
+
+    from audio_rag_amd.core.exceptions import RetrievalError
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    _, _, _, qd = store
+    srv = StreamServer(ret, max_batch=8, max_wait_ms=0.5)
+    t = srv.submit_arrays(qd[0].view(np.float16))
+    assert len(srv.result(t)) == K
+    ret.delete_collection()
+    with pytest.raises(RetrievalError):
+        srv.submit_arrays(qd[1].view(np.float16))
+
+    ret = _retriever(store)
+    srv = StreamServer(ret, max_batch=64, max_wait_ms=200.0)  # the batch waits 200 ms
+    t = srv.submit_arrays(qd[2].view(np.float16))
+    errs = []
+
+    def waiter():
+        try:
+            srv.raw_result(t, timeout=30.0)
+        except RetrievalError as e:  # woken by close()
+            errs.append(e)
+        except Exception as e:  # noqa: BLE001 - any other failure is a test failure
+            errs.append(e)
+
+    th = threading.Thread(target=waiter)
+    th.start()
+    time.sleep(0.02)
+    srv.close()
+    th.join(10.0)
+    assert not th.is_alive()
+    assert len(errs) <= 1 and all(isinstance(e, RetrievalError) for e in errs)
+    srv.close()  # idempotent
+
+
+def test_stream_server_threshold_and_unsorted_terms(gpu, oracle_mod, store):
+    """score_threshold applies to a legacy dense-only collection (qdrant.py:331) as in
+    MI355XRetriever.search; sparse terms submitted in any order answer as sorted ones."""
+    from audio_rag_amd.config import RetrievalConfig
+    from audio_rag_amd.core import EmbeddingResult
+    from audio_rag_amd.retrieval.batcher import StreamServer
+    from audio_rag_amd.retrieval.mi355x import MI355XRetriever
+
+    rows, _, (qi, qx, qv), qd = store
+    legacy = MI355XRetriever(RetrievalConfig(top_k=K, score_threshold=0.05), 1024)
+    legacy.add_arrays(rows.view(np.float16), [{"text": f"c{r}", "metadata": {}} for r in range(N)])
+    qf = qd.view(np.float16).astype(np.float32)
+    with StreamServer(legacy, max_batch=8, max_wait_ms=0.5) as srv:
+        for i in range(6):
+            want = legacy.search(EmbeddingResult(dense=qf[i].tolist()))
+            got = srv.result(srv.submit_arrays(qd[i].view(np.float16)))
+            assert [(r.chunk.text, r.score) for r in got] == [(r.chunk.text, r.score) for r in want]
+            assert all(r.score >= 0.05 for r in got)
+    ret = _retriever(store)
+    with StreamServer(ret, max_batch=8, max_wait_ms=0.5, search_type="hybrid") as srv:
+        for i in range(1, 8):
+            if not i % 4:
+                continue
+            idx, val = qx[qi[i]:qi[i + 1]], qv[qi[i]:qi[i + 1]]
+            rev = srv.result(srv.submit_arrays(qd[i].view(np.float16), (idx[::-1], val[::-1])))
+            want = _expected(oracle_mod, store, i, "hybrid", None)
+            assert [(r.chunk.text, r.score) for r in rev] == want, i

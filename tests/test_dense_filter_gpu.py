@@ -8,8 +8,8 @@ src/audio_rag/retrieval/qdrant.py:284-288, 316-332) on inputs built to stress th
 whose components span a wide dynamic range (a few large components, the rest tiny: a large
 quantisation error), near-duplicate rows (ties broken by ordinal), zero rows (key 0), and a row
 filter.
-The int8-query form (k <= 6), the fp16-query form (7 <= k <= 16) and the fp16 scan (k > 16) all
-run, and at 100k random unit rows every query must be certified (no exact fallback).
+The int8 first pass serves k <= 64 (fp16 scan beyond), and at 100k random unit rows every query
+must be certified (no second pass).
 """
 
 import numpy as np
@@ -68,11 +68,13 @@ def test_scan_form_by_k(gpu, oracle_mod):
     idx = _index(oracle_mod.unit_fp16(500, 1024, seed=1), gpu)
     assert idx.scan_form(64, 5) == _armi.SCAN_INT8_FILTER
     assert idx.scan_form(64, 16) == _armi.SCAN_INT8_FILTER
-    assert idx.scan_form(64, 17) == _armi.SCAN_FP16
+    assert idx.scan_form(64, 40) == _armi.SCAN_INT8_FILTER  # the reference's hybrid prefetch
+    assert idx.scan_form(64, 64) == _armi.SCAN_INT8_FILTER
+    assert idx.scan_form(64, 65) == _armi.SCAN_FP16
     assert idx.scan_form(300, 5) == _armi.SCAN_TILED_FP16
 
 
-@pytest.mark.parametrize("k", [1, 5, 6, 7, 10, 16, 17])
+@pytest.mark.parametrize("k", [1, 5, 6, 7, 10, 16, 17, 40, 65])
 def test_filter_forms_match_oracle(gpu, oracle_mod, k):
     rows = oracle_mod.unit_fp16(30000, 1024, seed=300 + k)
     qs = oracle_mod.unit_fp16(64, 1024, seed=301 + k)

@@ -8,7 +8,7 @@ configs[2] (1 x MI355X, 1M chunks, hybrid dense + BM25 with RRF, top-20 -> cross
     L = 256 tokens, all 12 layers, fp16 path) within 1e-3 of transformers' fp32 forward.
 configs[3]'s arithmetic on one GPU (10M chunks sharded 8-way -> 8 shards of 1.25M rows, the
 all-gathered batch of 512 queries, i.e. exactly one rank's scan shape at N = 8):
-  * per-shard tiled scans (dense_gemm_scan_glds_kernel) at k = 5 and k = 40, merged over the 8
+  * per-shard tiled scans (dense_gemm_scan_w4_kernel, the default tiled form) at k = 5 and k = 40, merged over the 8
     shards by armi_topk_merge_shards: 8 sampled queries against the oracle over all 10M rows,
     all 512 against the exhaustive exact scan;
   * the hybrid step: dense + sparse prefetch 40 per shard, merged, RRF 20, against the oracle.
