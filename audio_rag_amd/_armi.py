@@ -71,7 +71,8 @@ SIGNATURES: dict[str, tuple] = {
     "armi_stream_stats": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
     "armi_stream_loadgen": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                     ctypes.c_double, ctypes.c_uint64, c_void_p,
-                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64)]),
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
+                                    c_void_p, c_void_p]),
     "armi_sparse_index_create": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                          c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_sparse_index_destroy": (c_int, [c_void_p]),

@@ -542,7 +542,8 @@ int armi_stream_stats(armi_stream* s, int64_t* batches, int64_t* queries) {
 int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* q_indptr,
                         const int32_t* q_indices, const float* q_values, int64_t n_vectors,
                         int64_t n_queries, double qps, uint64_t seed, double* latency_us,
-                        double* elapsed_s, int64_t* completed) {
+                        double* elapsed_s, int64_t* completed, int64_t* out_ids,
+                        int32_t* out_count) {
   ARMI_REQUIRE(s && queries && latency_us && elapsed_s && completed,
                "armi_stream_loadgen: null pointer argument");
   ARMI_REQUIRE(n_vectors >= 1, "armi_stream_loadgen: n_vectors < 1");
@@ -565,10 +566,12 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* 
         std::this_thread::sleep_for(std::chrono::microseconds(5));
       }
       const int64_t tk = tickets[(size_t)i];
-      if (int rc = armi_stream_wait(s, tk, nullptr, nullptr, nullptr, &cnt, nullptr, 60e6)) {
+      int64_t* ids = out_ids ? out_ids + (size_t)i * s->k : nullptr;
+      if (int rc = armi_stream_wait(s, tk, nullptr, ids, nullptr, &cnt, nullptr, 60e6)) {
         rc_col.store(rc);
         return;
       }
+      if (out_count) out_count[i] = cnt;
       const Entry& e = s->ring[tk % s->ring_n];
       latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;
       t_last = std::max(t_last, e.t_done);

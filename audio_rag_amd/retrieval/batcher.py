@@ -328,11 +328,12 @@ class StreamServer:
         return b.value, q.value
 
     def loadgen(self, queries: np.ndarray, n_queries: int, qps: float, seed: int = 0,
-                sparse_csr: tuple[np.ndarray, np.ndarray, np.ndarray] | None = None):
+                sparse_csr: tuple[np.ndarray, np.ndarray, np.ndarray] | None = None,
+                answers: bool = False):
         """Native open-loop Poisson load at `qps` (armi_stream_loadgen): query i = row
         (i % len(queries)) with, on a hybrid server, the terms of CSR row (i % len(queries)).
         Returns per-query latency in seconds and the elapsed time from the first submit to the
-        last completion."""
+        last completion; with answers=True also every query's ids [n_queries, k] and count."""
         q = np.ascontiguousarray(queries, dtype=np.float16).reshape(-1, self.dim)
         lat = np.empty(n_queries, dtype=np.float64)
         el = self._armi.ctypes.c_double()
@@ -346,9 +347,14 @@ class StreamServer:
             if np.diff(keep[0]).max(initial=0) > 256:
                 raise RetrievalError("a sparse query may hold at most 256 terms")
             ptrs = tuple(a.ctypes.data for a in keep)
+        ids = np.empty((n_queries, self.k), dtype=np.int64) if answers else None
+        cnt = np.empty(n_queries, dtype=np.int32) if answers else None
         self._call("armi_stream_loadgen", q.ctypes.data, *ptrs, q.shape[0], n_queries,
                    float(qps), seed, lat.ctypes.data, self._armi.ctypes.byref(el),
-                   self._armi.ctypes.byref(done))
+                   self._armi.ctypes.byref(done), None if ids is None else ids.ctypes.data,
+                   None if cnt is None else cnt.ctypes.data)
+        if answers:
+            return lat * 1e-6, el.value, ids, cnt
         return lat * 1e-6, el.value
 
     def close(self) -> None:

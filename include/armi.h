@@ -210,11 +210,13 @@ int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);
  * fp16 [n_vectors][dim]) with, when q_indptr is non-null, the sparse terms of CSR row
  * (i % n_vectors); latency_us[i] = completion - submit of query i; elapsed_s = last
  * completion - first submit. Results are collected by a second thread while arrivals continue,
- * so n_queries is unbounded. */
+ * so n_queries is unbounded; out_ids [n_queries][k] / out_count [n_queries] (nullable) receive
+ * every query's answer (ids of the branch taken, as armi_stream_wait). */
 int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, const int32_t* q_indptr,
                         const int32_t* q_indices, const float* q_values, int64_t n_vectors,
                         int64_t n_queries, double qps, uint64_t seed, double* latency_us,
-                        double* elapsed_s, int64_t* completed);
+                        double* elapsed_s, int64_t* completed, int64_t* out_ids,
+                        int32_t* out_count);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Sparse (lexical-weight) store                                                              */
