@@ -234,6 +234,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="dense headline at N=1 only: skip the secondary configs1 / configs2 "
+                         "objects (each measured by a child bench.py run)")
     ap.add_argument("--latency-iters", type=int, default=30)
     ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
                                            "ingest"],
@@ -592,10 +595,44 @@ def main() -> None:
                                              doc_tokens(ords, 236).to(torch.int64), eos], dim=2))
         result["cpu_baseline"] = cpu_baseline(wl, ref, qn, q_csr, k, search_k, pairs)
         del ref
+    if wl == "dense" and world == 1 and not args.no_extras and args.corpus == "random":
+        result.update(secondary_configs(args))
     print(json.dumps(result), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary_configs(args) -> dict:
+    """BASELINE configs[1] and configs[2] measured beside the headline (the driver runs only the
+    default bench line): each is a child bench.py run on the same GPU, its JSON line attached
+    under "configs1" / "configs2" (value, ms_per_step, p50, rooflines)."""
+    import subprocess
+
+    runs = {
+        "configs1": ["--chunks", "100000", "--steps", "200", "--warmup", "10",
+                     "--latency-iters", "20"],
+        "configs2": ["--workload", "hybrid_rerank", "--chunks", str(args.chunks), "--steps", "10",
+                     "--warmup", "2", "--latency-iters", "3"],
+    }
+    out = {}
+    for key, extra in runs.items():
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--no-extras", "--no-cpu-baseline", *extra]
+        try:
+            res = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            line = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else ""
+            d = json.loads(line) if res.returncode == 0 and line.startswith("{") else None
+        except (subprocess.TimeoutExpired, json.JSONDecodeError):
+            d = None
+        if d is None:
+            out[key] = {"error": "child bench run failed", "cmd": " ".join(cmd[1:])}
+            continue
+        keep = ("value", "unit", "ms_per_step", "steps", "p50_ms", "p50_single_query_ms",
+                "certified_frac", "config", "roofline", "roofline_scan", "roofline_sparse",
+                "rerank_share_of_step", "dtype")
+        out[key] = {kk: d[kk] for kk in keep if kk in d}
+        out[key]["baseline_config"] = {"configs1": 1, "configs2": 2}[key]
+    return out
 
 
 WORDS = ("gradient descent learning rate loss function model training data neural network layer "
