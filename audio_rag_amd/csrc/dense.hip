@@ -350,6 +350,20 @@ __device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
+// Probe builds only (-DARMI_PROBE_BUILD -DARMI_I8_STAMPS): per (workgroup, wave) s_memrealtime
+// (100 MHz, chip-wide) at kernel entry, after the query image, after the tile loop and at the
+// end of the workgroup merge, read back by armi_probe_i8_stamps (not part of the ABI).
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_STAMPS)
+__device__ uint64_t g_i8_stamps[256 * kWaves * 4];
+#define I8_STAMP(slot)                                                                \
+  do {                                                                                \
+    if (!COLLECT && lane == 0 && blockIdx.x < 256)                                    \
+      g_i8_stamps[(blockIdx.x * kWaves + wave) * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define I8_STAMP(slot) do {} while (0)
+#endif
+
 // COLLECT: the second pass for the queries the merge could not certify (replaces the per-query
 // exhaustive exact scan of round 2). The call's uncertified queries, in query order, are dealt
 // 64 per block; each gets its merge-computed threshold thr[q] = (k-th exact key found) - delta,
@@ -392,6 +406,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   const int lane = threadIdx.x & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
+  I8_STAMP(0);
   if constexpr (COLLECT) {
     // this block's slice [q0, q0 + 64) of the ordered list of uncertified queries
     for (int e = threadIdx.x; e < kQB; e += kThreads) {
@@ -548,6 +563,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   }
   }
   __syncthreads();
+  I8_STAMP(1);
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
   float th0 = __builtin_inff(), th1 = __builtin_inff();
   int qi0 = 0, qi1 = 0;
@@ -715,6 +731,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     }
   }
 
+  I8_STAMP(2);
   if constexpr (COLLECT) return;
   // 2. Workgroup merge (as dense_scan_kernel; the query image is dead: overlay it).
   __syncthreads();
@@ -761,6 +778,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     }
     if (lane == 0) cand_bound[base] = b[qq];
   }
+  I8_STAMP(3);
 }
 
 template <int DIM>
@@ -3373,6 +3391,13 @@ int armi_dense_exact_topk(const armi_index* idx, const uint16_t* queries, int n_
                              out_count, flags, 0, w, stream);
   });
 }
+
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_STAMPS)
+int armi_probe_i8_stamps(uint64_t* out) {
+  ARMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_i8_stamps), sizeof(g_i8_stamps)));
+  return ARMI_OK;
+}
+#endif
 
 int armi_topk_merge_shards(const double* in_rank, const float* in_scores, const int64_t* in_ids,
                            const int32_t* in_count, int n_shards, int n_queries, int k_in,

@@ -1,0 +1,64 @@
+"""Phase timeline of dense_scan_i8_kernel from a probe build (-DARMI_PROBE_BUILD -DARMI_I8_STAMPS):
+per (workgroup, wave) s_memrealtime stamps at entry, after the query image, after the tile loop
+and at the end of the workgroup merge, for one 64-query launch over `--chunks` rows. Prints the
+launch's phase spans (chip-wide, 10 ns ticks -> us)."""
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from audio_rag_amd import _armi  # noqa: E402
+from audio_rag_amd.retrieval.device import DenseIndex  # noqa: E402
+from audio_rag_amd.synthetic import make_queries, make_rows  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rows = make_rows(0, a.chunks, 1024, dev)
+    idx = DenseIndex(rows)
+    qs = make_queries(1, 64, 1024, dev, seed=1)[0]
+    ws = torch.empty(idx.workspace_bytes(64, 5), dtype=torch.uint8, device=dev)
+    lib = _armi.load()
+    fn = lib.armi_probe_i8_stamps
+    fn.argtypes = [ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    buf = np.zeros(256 * 8 * 4, dtype=np.uint64)
+    spans = []
+    for r in range(a.reps):
+        idx.topk(qs, 5, workspace=ws)
+        torch.cuda.synchronize()
+        assert fn(buf.ctypes.data) == 0
+        st = buf.reshape(256, 8, 4).astype(np.int64)
+        live = st[:, :, 0] > 0
+        t0 = st[:, :, 0][live].min()
+        rel = (st - t0) / 100.0  # us
+        e = rel[..., 0][live]
+        img = (rel[..., 1] - rel[..., 0])[live]
+        loop = (rel[..., 2] - rel[..., 1])[live]
+        merge = (rel[..., 3] - rel[..., 2])[live]
+        end = rel[..., 3][live]
+        loop_end = rel[..., 2][live]
+        spans.append(dict(entry_spread=float(e.max()), image_mean=float(img.mean()),
+                          image_max=float(img.max()), loop_mean=float(loop.mean()),
+                          loop_max=float(loop.max()), loop_end_min=float(loop_end.min()),
+                          loop_end_max=float(loop_end.max()), merge_mean=float(merge.mean()),
+                          merge_max=float(merge.max()), total=float(end.max())))
+        buf[:] = 0
+    keys = spans[0].keys()
+    med = {k: float(np.median([s[k] for s in spans[2:]])) for k in keys}
+    print(json.dumps({"chunks": a.chunks, "median_us": med}))
+
+
+if __name__ == "__main__":
+    main()
