@@ -30,6 +30,7 @@ struct armi_index {
   // never crowds one lane list. perm_inv = perm_mul^-1 mod T.
   int64_t perm_mul = 1;
   int64_t perm_inv = 1;
+  int32_t* tile_ord = nullptr;   // [n_tiles] ordinal of image tile tau's row 0 = tau * perm_inv mod T
 };
 
 namespace armi {

@@ -377,7 +377,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
-    int guard, const uint32_t* __restrict__ flags, const float* __restrict__ thr,
+    int guard, const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
+    const float* __restrict__ thr,
     int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap) {
   static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
   constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
@@ -591,6 +592,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     for (; t < t_end; t += kWaves) {
       const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
       const u32x4* nxt = row_ptr(tn);
+      const int32_t tord = tile_ord[t];  // ordinal of the tile's image row 0 (wave-uniform)
       int qoff = h * kQB + r;
       asm volatile("" : "+v"(qoff));
       const u32x4* qv = qimg + qoff;
@@ -684,14 +686,17 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         mx0 = fmaxf(mx0, x0[j]);
         mx1 = fmaxf(mx1, x1[j]);
       }
-      const int32_t rbase = (int32_t)row0 + 4 * h;
+      // image row p of the tile holds ordinal tord + p * T (armi_index.h): lists and the collect
+      // lists carry ordinals
+      const int32_t T32 = (int32_t)n_tiles;
+      const int32_t obase = tord + 4 * h * T32;
       if constexpr (COLLECT) {
         // append every image position whose key reaches the query's threshold (NaN keys of
         // invalid / filtered rows never do)
         if (__any(mx0 >= th0 || mx1 >= th1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            const int32_t pos = rbase + (j & 3) + 8 * (j >> 2);
+            const int32_t pos = obase + ((j & 3) + 8 * (j >> 2)) * T32;
             if (x0[j] >= th0) {
               const int s = atomicAdd(col_cnt + qi0, 1);
               if (s < col_cap) col_list[(size_t)qi0 * col_cap + s] = pos;
@@ -711,7 +716,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
             d0 = fmaxf(d0, x0[j]);
             continue;
           }
-          topm_insert<kLaneList>(x0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
+          topm_insert<kLaneList>(x0[j], obase + ((j & 3) + 8 * (j >> 2)) * T32, s0, i0, d0);
         }
       } else {
         d0 = fmaxf(d0, mx0);
@@ -723,7 +728,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
             d1 = fmaxf(d1, x1[j]);
             continue;
           }
-          topm_insert<kLaneList>(x1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
+          topm_insert<kLaneList>(x1[j], obase + ((j & 3) + 8 * (j >> 2)) * T32, s1, i1, d1);
         }
       } else {
         d1 = fmaxf(d1, mx1);
@@ -2292,12 +2297,6 @@ __device__ __forceinline__ void exact_keys8(const int32_t (&qf)[DIM / 64],
   key = row >= 0 ? (double)dot * myinv : kNegInfD;
 }
 
-// Ordinal of a candidate row: the int8 pass reports image positions (scattered order,
-// armi_index.h), the fp16 passes ordinals (perm_T == 0).
-__device__ __forceinline__ int32_t cand_ordinal(int32_t row, int64_t perm_T, int64_t perm_inv) {
-  return perm_T ? (int32_t)armi::img_to_ord(row, perm_T, perm_inv) : row;
-}
-
 // Largest float <= x (x finite or infinite).
 __device__ __forceinline__ float f32_round_down(double x) {
   float f = (float)x;
@@ -2317,7 +2316,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     const float* __restrict__ cand_bound, int n_wg, int q_stride, const uint16_t* __restrict__ rows,
     const double* __restrict__ inv_norm, const uint16_t* __restrict__ queries,
     double* __restrict__ inv_q_out, double* __restrict__ qnorm_out, int k, int kc, int sel_col,
-    int sel_rank, int64_t perm_T, int64_t perm_inv, int64_t ordinal_base,
+    int sel_rank, int64_t ordinal_base,
     float* __restrict__ out_scores, int64_t* __restrict__ out_ids, double* __restrict__ out_rank,
     int32_t* __restrict__ out_count, uint32_t* __restrict__ out_flags, float* __restrict__ thr_out,
     int32_t* __restrict__ col_cnt) {
@@ -2514,7 +2513,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     for (int j = 0; j < kRescoreBatch; ++j) {
       const int c = wave + kMW * (i0 + j);
       const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
-      rr[j] = live ? cand_ordinal(srow[c], perm_T, perm_inv) : -1;
+      rr[j] = live ? srow[c] : -1;
     }
     double key;
     int32_t myrow;
@@ -2600,7 +2599,7 @@ constexpr size_t kColMergeLds = 2 * kColChunk * 16;
 template <int DIM>
 __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel(
     const int32_t* __restrict__ col_cnt, const int32_t* __restrict__ col_list, int col_cap,
-    int64_t perm_T, int64_t perm_inv, const uint16_t* __restrict__ rows,
+    const uint16_t* __restrict__ rows,
     const double* __restrict__ inv_norm, const int64_t* __restrict__ norm2,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, const uint16_t* __restrict__ queries,
     const double* __restrict__ inv_q, int k, int64_t ordinal_base, float* __restrict__ out_scores,
@@ -2643,7 +2642,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
                             (!row_mask || ((row_mask[row >> 6] >> (row & 63)) & 1ull));
             o = on ? (int32_t)row : -1;
           } else {
-            o = cand_ordinal(list[c0 + e], perm_T, perm_inv);
+            o = list[c0 + e];
           }
         }
         rr[j] = o;
@@ -2683,12 +2682,12 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
 // ordinal mask (0 for padding positions). One wave per 64 image positions.
 __global__ __launch_bounds__(256) void mask_to_img_kernel(const uint64_t* __restrict__ mask,
                                                           int64_t n_rows, int64_t T,
-                                                          int64_t perm_inv,
+                                                          const int32_t* __restrict__ tile_ord,
                                                           uint64_t* __restrict__ out) {
   const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool bit = false;
   if (pos < T * 32) {
-    const int64_t i = armi::img_to_ord(pos, T, perm_inv);
+    const int64_t i = (pos & 31) * T + tile_ord[pos >> 5];
     bit = i < n_rows && ((mask[i >> 6] >> (i & 63)) & 1ull);
   }
   const uint64_t b = __ballot(bit);
@@ -3131,7 +3130,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   const uint64_t* mask_i8 = nullptr;
   if (row_mask) {
     mask_to_img_kernel<<<dim3((unsigned)((T * 32 + 255) / 256)), dim3(256), 0, stream>>>(
-        row_mask, idx->n_rows, T, idx->perm_inv, w.mask_img);
+        row_mask, idx->n_rows, T, idx->tile_ord, w.mask_img);
     ARMI_LAUNCHED("mask_to_img_kernel");
     mask_i8 = w.mask_img;
   }
@@ -3243,7 +3242,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-        nullptr, nullptr, nullptr, nullptr, 0);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -3264,7 +3263,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   merge_select(kc, n_wg, sel_col, sel_rank);
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
-      w.inv_q, w.qnorm, k, kc, sel_col, sel_rank, i8_first ? T : 0, idx->perm_inv,
+      w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
       idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt);
   ARMI_LAUNCHED("dense_merge_kernel");
   // second pass for the uncertified queries (both kernels exit at once when every query of the
@@ -3277,13 +3276,13 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
-        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, out_flags, w.thr, w.col_cnt,
-        w.col_list, kCollectCap);
+        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
+        w.col_cnt, w.col_list, kCollectCap);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
   dense_collect_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kColMergeLds, stream>>>(
-      w.col_cnt, w.col_list, kCollectCap, T, idx->perm_inv, idx->rows, idx->inv_norm, idx->norm2,
+      w.col_cnt, w.col_list, kCollectCap, idx->rows, idx->inv_norm, idx->norm2,
       row_mask, idx->n_rows, queries, w.inv_q, k, idx->ordinal_base, out_scores, out_ids,
       out_rank, out_count, out_flags);
   ARMI_LAUNCHED("dense_collect_merge_kernel");

@@ -117,6 +117,12 @@ __global__ __launch_bounds__(256) void row_filter_kernel(const uint16_t* __restr
   }
 }
 
+__global__ __launch_bounds__(256) void tile_ord_kernel(int64_t T, int64_t perm_inv,
+                                                       int32_t* __restrict__ out) {
+  const int64_t tau = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (tau < T) out[tau] = (int32_t)((tau * perm_inv) % T);
+}
+
 int64_t gcd64(int64_t a, int64_t b) {
   while (b) {
     const int64_t t = a % b;
@@ -183,8 +189,16 @@ int armi_index_create(int device, const uint16_t* rows, int64_t n_rows, int dim,
   if (e == hipSuccess) e = hipMalloc(&idx->rows8, tiled * dim);
   if (e == hipSuccess) e = hipMalloc(&idx->a32, padded * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&idx->e32, padded * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&idx->tile_ord, std::max<int64_t>(idx->n_tiles, 1) * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemsetAsync(idx->invalid, 0, sizeof(unsigned long long), stream);
   if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "armi_index_create alloc"); }
+  {
+    const int64_t T = std::max<int64_t>(idx->n_tiles, 1);
+    tile_ord_kernel<<<dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream>>>(
+        idx->n_tiles > 0 ? T : 1, idx->perm_inv, idx->tile_ord);
+    e = hipGetLastError();
+    if (e != hipSuccess) { armi_index_destroy(idx); return armi::hip_fail(e, "tile_ord_kernel"); }
+  }
   const int64_t blocks = (padded + 3) / 4;
   row_norms_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
       rows, n_rows, padded, dim, idx->norm2, idx->inv_norm, idx->inv_norm32, idx->invalid);
@@ -216,6 +230,7 @@ int armi_index_destroy(armi_index* idx) {
   hipFree(idx->rows8);
   hipFree(idx->a32);
   hipFree(idx->e32);
+  hipFree(idx->tile_ord);
   delete idx;
   return ARMI_OK;
 }
