@@ -23,7 +23,7 @@ LIB = OUT_DIR / "libarmi.so"
 OBJ_DIR = ROOT / "build" / "armi_obj"
 
 SOURCES = ["armi_common.cpp", "index.hip", "dense.hip", "sparse.hip", "rrf.hip", "encoder.hip",
-           "attention.hip", "stream.cpp"]
+           "attention.hip", "gemm.hip", "stream.cpp"]
 ARCH = os.environ.get("ARMI_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-ffp-contract=off",

@@ -367,31 +367,6 @@ __global__ __launch_bounds__(256) void add_layernorm_f16_kernel(
   }
 }
 
-// erf in fp32 without branches (|error| <= 1.2 ulp, 6.9e-8 absolute over [-10, 10], checked
-// against float64 erf): the minimax fits of the well-known branch-split erff (|x| <= 0.9277:
-// odd polynomial in x; above: 1 - exp(-(|x| + poly(|x|) |x|))), both evaluated and selected, so the
-// 8 values of a thread never diverge. The library erff spends ~3x the instructions in branches;
-// the GELU pass was instruction-bound on it.
-__device__ __forceinline__ float erf_f32(float a) {
-  const float t = fabsf(a), s = a * a;
-  float r = fmaf(-1.72853470e-5f, t, 3.83197126e-4f);
-  const float u = fmaf(-3.88396438e-3f, t, 2.42546219e-2f);
-  r = fmaf(r, s, u);
-  r = fmaf(r, t, -1.06777877e-1f);
-  r = fmaf(r, t, -6.34846687e-1f);
-  r = fmaf(r, t, -1.28717512e-1f);
-  r = fmaf(r, t, -t);
-  const float big = copysignf(1.0f - __expf(r), a);
-  float q = -5.96761703e-4f;
-  q = fmaf(q, s, 4.99119423e-3f);
-  q = fmaf(q, s, -2.67681349e-2f);
-  q = fmaf(q, s, 1.12819925e-1f);
-  q = fmaf(q, s, -3.76125336e-1f);
-  q = fmaf(q, s, 1.28379166e-1f);
-  q = fmaf(q, a, a);
-  return t > 0.927734375f ? big : q;
-}
-
 // in-place exact-erf GELU of fp16 x (+ fp32 bias[col], nullable), computed in fp32
 __global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
                                                        const float* __restrict__ bias, int64_t n,
@@ -406,8 +381,8 @@ __global__ __launch_bounds__(256) void gelu_f16_kernel(uint16_t* __restrict__ x,
     const half2v hv = __builtin_bit_cast(half2v, word);
     float t0 = (float)hv[0] + (bias ? bias[c0 + 2 * w] : 0.f);
     float t1 = (float)hv[1] + (bias ? bias[c0 + 2 * w + 1] : 0.f);
-    t0 = 0.5f * t0 * (1.0f + erf_f32(t0 * 0.70710678118654752440f));
-    t1 = 0.5f * t1 * (1.0f + erf_f32(t1 * 0.70710678118654752440f));
+    t0 = 0.5f * t0 * (1.0f + armi::erf_f32(t0 * 0.70710678118654752440f));
+    t1 = 0.5f * t1 * (1.0f + armi::erf_f32(t1 * 0.70710678118654752440f));
     v[w] = pack_h2(t0, t1);
   }
   *reinterpret_cast<u32x4*>(x + i8) = v;

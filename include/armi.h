@@ -153,7 +153,7 @@ int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
  * _read synchronises on the recorded events of one slot, returns the summed kernel time and the
  * launch count, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
  * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (sparse_scan_kernel of armi_sparse_topk),
- * ARMI_TIMING_ENCODER_GEMM (the cross-encoder GEMMs of armi_enc_gemm_f16).
+ * ARMI_TIMING_ENCODER_GEMM (the cross-encoder GEMMs of armi_enc_linear_f16).
  * armi_scan_timing_read = armi_kernel_timing_read(ARMI_TIMING_DENSE_SCAN, ...). */
 #define ARMI_TIMING_DENSE_SCAN 0
 #define ARMI_TIMING_SPARSE_SCAN 1
@@ -331,6 +331,16 @@ int armi_enc_add_layernorm_f16(const uint16_t* x, const uint16_t* res, const flo
  * width must be a multiple of 8. */
 int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
                       hipStream_t stream);
+/* out = epi(x . w^T + bias): the nn.Linear layers of the cross-encoder (XLMRobertaLayer as
+ * CrossEncoder.predict runs it, reranking/bge.py:119-123) on the hand-written gfx950 MFMA GEMM,
+ * with the intermediate dense's exact-erf GELU (XLMRobertaIntermediate) fused into the epilogue.
+ *   x [m][k] fp16, w [n][k] fp16 (nn.Linear weight layout), bias [n] fp32, out [m][n] fp16;
+ *   fp32 accumulate; n % 256 == 0, k % 64 == 0, k <= 8192.
+ * Timed under ARMI_TIMING_ENCODER_GEMM when live timing is on. */
+#define ARMI_EPI_BIAS 0
+#define ARMI_EPI_BIAS_GELU 1
+int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out,
+                        int64_t m, int n, int k, int epilogue, hipStream_t stream);
 
 #ifdef __cplusplus
 }

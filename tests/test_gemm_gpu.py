@@ -1,0 +1,43 @@
+"""armi_enc_linear_f16 (the hand-written gfx950 GEMM of the cross-encoder's linear layers, fused
+bias / bias + exact-erf GELU epilogues; include/armi.h) against a torch fp32 reference of the same
+op: out = x . w^T + b (nn.Linear, XLMRobertaLayer as CrossEncoder.predict runs it,
+src/audio_rag/reranking/bge.py:119-123), GELU(out) for the intermediate dense. fp16 operands,
+fp32 accumulate, fp16 output: tolerance = fp16 output rounding (2^-10 relative) + 1e-3 absolute.
+Shapes cover full and partial 256-token blocks, every XLM-R base width and a K of 3072, with
+asymmetric operands (a transposed or mis-ordered output fails)."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(256, 256, 128, 0), (1000, 768, 768, 0),
+                                       (2048, 3072, 768, 1), (517, 768, 3072, 0),
+                                       (300, 2304, 768, 0), (4096, 768, 768, 1),
+                                       (77, 512, 192, 1)])
+def test_linear_f16_matches_fp32(gpu, m, n, k, epi):
+    from audio_rag_amd._armi import call, ptr, stream_handle
+
+    g = torch.Generator(device=gpu).manual_seed(m + n + k)
+    x = torch.randn((m, k), generator=g, device=gpu).half()
+    w = (torch.randn((n, k), generator=g, device=gpu) / k ** 0.5).half()
+    w[:, 0] += torch.arange(n, device=gpu).half() * 1e-3  # asymmetric in (feature, k)
+    b = torch.randn(n, generator=g, device=gpu) * 0.1
+    out = torch.full((m, n), float("nan"), dtype=torch.float16, device=gpu)
+    call("armi_enc_linear_f16", ptr(x), ptr(w), ptr(b), ptr(out), m, n, k, epi, stream_handle())
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t() + b
+    if epi:
+        ref = torch.nn.functional.gelu(ref)  # exact erf GELU
+    assert not torch.isnan(out).any()
+    torch.testing.assert_close(out.float(), ref, rtol=2 ** -10, atol=1e-3)
+
+
+def test_linear_f16_rejects_bad_shapes(gpu):
+    from audio_rag_amd._armi import ArmiError, call, stream_handle
+
+    with pytest.raises(ArmiError):
+        call("armi_enc_linear_f16", None, None, None, None, 10, 100, 768, 0, stream_handle())
+    with pytest.raises(ArmiError):
+        call("armi_enc_linear_f16", None, None, None, None, 10, 256, 100, 0, stream_handle())
