@@ -344,20 +344,18 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
     const char* e = getenv("ARMI_GEMM_BARRIERS");
     return (e && e[0] == '2') ? 2 : 4;
   }();
-  auto launch = [&](auto kern) -> int {
-    static bool raised = false;
-    (void)raised;
-    ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-    armi::TimedLaunch tl;
-    if (tl.begin(ARMI_TIMING_ENCODER_GEMM, stream) < 0) return ARMI_ERR_HIP;
-    kern<<<dim3(grid), dim3(kThreads), kLds, stream>>>(x, w, bias, out, m, n, k, n_tp, n_tiles);
-    ARMI_LAUNCHED("linear_f16_kernel");
-    return tl.end();
-  };
+  auto kern = linear_f16_kernel<0, 4>;
   if (epilogue == ARMI_EPI_BIAS_GELU)
-    return nbar == 4 ? launch(linear_f16_kernel<1, 4>) : launch(linear_f16_kernel<1, 2>);
-  return nbar == 4 ? launch(linear_f16_kernel<0, 4>) : launch(linear_f16_kernel<0, 2>);
+    kern = nbar == 4 ? linear_f16_kernel<1, 4> : linear_f16_kernel<1, 2>;
+  else if (nbar == 2)
+    kern = linear_f16_kernel<0, 2>;
+  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
+  armi::TimedLaunch tl;
+  if (tl.begin(ARMI_TIMING_ENCODER_GEMM, stream) < 0) return ARMI_ERR_HIP;
+  kern<<<dim3(grid), dim3(kThreads), kLds, stream>>>(x, w, bias, out, m, n, k, n_tp, n_tiles);
+  ARMI_LAUNCHED("linear_f16_kernel");
+  return tl.end();
 }
 
 }  // extern "C"
