@@ -61,6 +61,15 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + armi::erf_f32(x * 0.70710678118654752440f));
 }
 
+// sources of one tile of a workgroup's stream (linear_f16_kernel)
+struct TileSrc {
+  const unsigned char* p;  // feature block of w (scalar base)
+  const unsigned char* q;  // token block of x
+  uint32_t oq[2][2];       // per-lane token row offsets [half][piece] (clamped for a partial block)
+  int tp;                  // feature block index
+  int64_t q0;              // first token row
+};
+
 template <int EPI, int NBAR>
 __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
@@ -108,13 +117,6 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
   // belong to one of the two: nK >= 2). Per tile: scalar bases of its operand blocks and, for a
   // partial token block, the per-lane row offsets clamped to the last row (rows past m are read
   // from row m - 1 and never stored).
-  struct TileSrc {
-    const unsigned char* p;
-    const unsigned char* q;
-    uint32_t oq[2][2];
-    int tp;      // feature block
-    int64_t q0;  // first token row
-  };
   auto tile_src = [&](int64_t j) {
     TileSrc ts;
     const int64_t t = (int64_t)slot + j * G;
@@ -131,7 +133,8 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
       for (int jj = 0; jj < 2; ++jj) {
         const int i = 2 * wave + jj;
         const int bq = 64 * (i >> 2) + 32 * h + 8 * (i & 3);
-        const int row = (int)min<int64_t>(bq + prow, qlim);
+        const int64_t rq = bq + prow;
+        const int row = (int)(rq < qlim ? rq : qlim);
         ts.oq[h][jj] = (uint32_t)((row * k + 8 * pchunk) * 2);
       }
     return ts;
