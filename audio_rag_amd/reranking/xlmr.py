@@ -133,6 +133,26 @@ class CrossEncoderXLMR:
              ptr(self.head[2]), ptr(self.head[3]), ptr(probs), n, L, d, s)
         return probs
 
+    # Linear layers of the fp16 forward: "armi" = armi_enc_linear_f16 (hand-written gfx950 GEMM,
+    # bias / bias + exact-erf GELU fused into the epilogue: no separate GELU pass), "torch" = torch's
+    # hipBLASLt linear + armi_enc_gelu_f16 (A/B). ARMI_RERANK_GEMM selects.
+    gemm_impl = os.environ.get("ARMI_RERANK_GEMM", "armi")
+
+    def _lin(self, x: torch.Tensor, ly: dict, name: str, gelu: bool = False) -> torch.Tensor:
+        """y = x . W^T + b (+ exact GELU) for weight `name` of layer ly, fp16 in / out."""
+        w, b = ly[name + "_h"], ly[{"wqkv": "bqkv", "wo": "bo", "wi": "bi", "wo2": "bo2"}[name]]
+        n, k = w.shape
+        if self.gemm_impl == "armi" and n % 256 == 0 and k % 64 == 0 and k >= 128:
+            out = torch.empty((x.shape[0], n), dtype=torch.float16, device=self.device)
+            call("armi_enc_linear_f16", ptr(x), ptr(w), ptr(b), ptr(out), x.shape[0], n, k,
+                 1 if gelu else 0, stream_handle())
+            return out
+        y = torch.nn.functional.linear(x, w, ly[{"wqkv": "bqkv", "wo": "bo", "wi": "bi",
+                                                 "wo2": "bo2"}[name] + "_h"])
+        if gelu:
+            call("armi_enc_gelu_f16", ptr(y), None, y.shape[0], y.shape[1], stream_handle())
+        return y
+
     # Two-stream form (A/B, off by default): at or above this many tokens the sequences split into
     # two halves whose layer ops interleave on two streams. Measured slower at the configs[2]
     # shape (912 vs 929 q/s, profiles/r02h_rerank_ab.txt): the GEMMs hold every CU, so the other
@@ -183,11 +203,10 @@ class CrossEncoderXLMR:
         d, H, dh = self.d, self.heads, self.dh
         s = stream_handle()
         rows = n * L
-        lin = torch.nn.functional.linear
         scale = 1.0 / math.sqrt(dh)
         last = len(self.layers) - 1
         for i, ly in enumerate(self.layers):
-            qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])
+            qkv = self._lin(h16, ly, "wqkv")
             yield
             if i == last:
                 # The head reads only the <s> row of the last layer's output, and every op after
@@ -204,18 +223,16 @@ class CrossEncoderXLMR:
                      s)
             del qkv
             yield
-            attn = lin(ctx, ly["wo_h"], ly["bo_h"])
+            attn = self._lin(ctx, ly, "wo")
             yield
             h1 = torch.empty_like(h16)
             call("armi_enc_add_layernorm_f16", ptr(attn), ptr(h16), ptr(ly["ln1"][0]),
                  ptr(ly["ln1"][1]), ptr(h1), rows, d, self.eps, s)
             del attn
             yield
-            inter = lin(h1, ly["wi_h"], ly["bi_h"])
+            inter = self._lin(h1, ly, "wi", gelu=True)  # exact-erf GELU in the epilogue
             yield
-            call("armi_enc_gelu_f16", ptr(inter), None, rows, inter.shape[1], s)
-            yield
-            out = lin(inter, ly["wo2_h"], ly["bo2_h"])
+            out = self._lin(inter, ly, "wo2")
             del inter
             yield
             h16 = torch.empty_like(h1)
