@@ -305,7 +305,9 @@ def main() -> None:
 
     n, dim, batch, k = args.chunks, args.dim, args.batch, args.top_k
     wl = args.workload
-    search_k = k if wl == "dense" else (args.initial_k if wl == "hybrid_rerank" else k)
+    # hybrid and hybrid_rerank search configs[2]'s shape: top initial_k (20) fused from dense +
+    # sparse prefetches of 2 * 20 (QueryPipeline.query -> search(top_k=20), qdrant.py:281-298)
+    search_k = k if wl == "dense" else args.initial_k
     pre_k = search_k if wl == "dense" else 2 * search_k
     lo, hi = shard_range(n, rank, world)
     n_q_batches = 8
@@ -490,8 +492,9 @@ def main() -> None:
                 "dense": (f"dense cosine top-{k} over {n} x {dim} fp16 chunks sharded by ordinal over "
                           f"{world} GPU(s), {batch} queries per GPU per step (RCCL all-gather of "
                           f"queries and per-shard top-{k} when N>1)"),
-                "hybrid": (f"hybrid top-{k}: dense cosine + sparse lexical prefetch {pre_k} each, RRF "
-                           f"(1/(2+pos)), {n} chunks, {batch} queries per GPU per step"),
+                "hybrid": (f"hybrid top-{search_k}: dense cosine + sparse lexical prefetch {pre_k} "
+                           f"each, RRF (1/(2+pos)), {n} chunks, {batch} queries per GPU per step "
+                           f"(configs[2]'s retrieval, no rerank)"),
                 "hybrid_rerank": (f"hybrid top-{search_k} (prefetch {pre_k}+{pre_k}, RRF) -> "
                                   f"cross-encoder (XLM-R base, 12 layers, L=256, "
                                   f"{args.rerank_dtype} GEMMs) -> top-{k}, {n} chunks, {batch} "
