@@ -2145,6 +2145,357 @@ void dense_gemm_scan_w4_kernel(
   }
 }
 
+// Tiled scan on the GEMM mainloop of gemm.hip (armi_enc_linear_f16): the > 128-query form
+// (round 3, ARMI_GEMM_FORM=g8 / default once measured). Workgroup = (256-query block, row range),
+// 512 threads = 8 waves as 2 (rows, 128 each) x 4 (queries, 64 each), tiles of 256 rows x 256
+// queries, v_mfma_f32_16x16x32_f16 (lane (l & 15) = row / query of a 16-block, 8 k values per
+// lane): per wave 8 x 4 accumulator blocks, the accumulator register j of lane l is
+// D[row 4 (l >> 4) + j][query l & 15]. K-tiles of 64, four quadrant phases each, operand halves
+// staged by LDS-DMA (one half-tile per phase, >= 4 phases ahead, one counted vmcnt per K-tile;
+// see gemm.hip). The K-tile stream runs across the range's tiles, so the next tile's first
+// K-tiles are in flight during a tile's epilogue.
+// Tile epilogue (per lane and query, over its 32 rows of the tile): score = fma(acc, inv_norm,
+// bias) with (0, -FLT_MAX) for dead rows (past the range, filtered, invalid), row code pm*4 + j in
+// the 5 low mantissa bits (<= 2^-18 relative: kEncodeSlack), compare-free best-two + third chain;
+// the best two enter a 2-deep lane list, the third and every eviction the lane's discarded bound.
+// Per query 8 lanes (2 waves x 4 lane groups) x 2 entries = the workgroup's 16 candidates.
+constexpr int kG8Threads = 512;
+constexpr int kG8Img = 256 * 64 * 2;       // one operand image of a K-tile (32 KB)
+constexpr int kG8Buf = 2 * kG8Img;         // rows + queries
+constexpr int kG8Norm = 2 * kG8Buf;        // two 1-KB inverse-norm slots (tile parity)
+constexpr size_t kG8Lds = 2 * kG8Buf + 2 * 1024;
+
+struct G8Src {
+  const unsigned char* p;  // first row of the tile (scalar base)
+  int32_t last;            // last row of the store relative to the tile (clamp of the DMA rows)
+  int64_t r0;              // first row of the tile
+};
+
+template <int DIM>
+__global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
+    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
+    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+  constexpr int nK = DIM / 64;
+  static_assert(nK >= 2, "the stream needs >= 2 K-tiles per tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int id = blockIdx.x;
+  int qb, rp;
+  if (n_qb == 2) {
+    qb = (id >> 3) & 1;
+    rp = (id >> 4) * 8 + (id & 7);
+  } else {
+    qb = id % n_qb;
+    rp = id / n_qb;
+  }
+  if (rp >= n_ranges) return;  // workgroup-uniform
+  const int64_t lo = (int64_t)rp * rows_per_range;
+  const int64_t hi = min(lo + rows_per_range, n_rows);
+  const int q_base = qb * 256;
+  const int n_tiles = (int)((hi - lo + 255) / 256);
+  const int64_t total = (int64_t)n_tiles * nK;
+  const int64_t n_pad = (n_rows + 31) / 32 * 32;  // inverse norms are padded to 32-row tiles
+
+  const int tid = threadIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = tid & 63;
+  const int wp = wave >> 2;
+  const int wq = wave & 3;
+  const int prow = lane >> 3;
+  const int pchunk = (lane & 7) ^ prow;
+  // piece geometry (wave-uniform) of half h, piece jj: first image row of the 8-row piece
+  auto bp_of = [&](int h, int jj) {
+    const int i = 2 * wave + jj;
+    return i < 8 ? 64 * h + 8 * i : 128 + 64 * h + 8 * (i - 8);
+  };
+  auto bq_of = [&](int h, int jj) {
+    const int i = 2 * wave + jj;
+    return 64 * (i >> 2) + 32 * h + 8 * (i & 3);
+  };
+  const int qlast = nq - 1 - q_base;
+  const unsigned char* qsrc = reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
+  auto tile_src = [&](int j) {
+    G8Src ts;
+    ts.r0 = lo + (int64_t)j * 256;
+    ts.p = reinterpret_cast<const unsigned char*>(rows + (size_t)ts.r0 * DIM);
+    const int64_t last = n_rows - 1 - ts.r0;
+    ts.last = (int32_t)(last < 255 ? last : 255);
+    return ts;
+  };
+  G8Src cur = tile_src(0), nxt = tile_src(1);
+  // DMA offsets are formed at issue time (a few VALU) instead of held in registers
+  auto issue_half = [&](int64_t sidx, int kt_s, int d, int op, int h) {
+    if (sidx >= total) return;  // uniform
+    int kt2 = kt_s + d;
+    const bool next = kt2 >= nK;
+    kt2 -= next ? nK : 0;
+    unsigned char* buf = smem + (sidx & 1) * kG8Buf + op * kG8Img;
+    if (op == 0) {
+      const unsigned char* src = (next ? nxt.p : cur.p) + kt2 * 128;
+      const int32_t lim = next ? nxt.last : cur.last;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int bp = bp_of(h, jj);
+        const int row = min(bp + prow, lim);
+        __builtin_amdgcn_global_load_lds(src + (uint32_t)((row * DIM + 8 * pchunk) * 2),
+                                         (lds_ptr_t)(buf + bp * 128), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int bq = bq_of(h, jj);
+        const int row = min(bq + prow, qlast);
+        __builtin_amdgcn_global_load_lds(qsrc + kt2 * 128 + (uint32_t)((row * DIM + 8 * pchunk) * 2),
+                                         (lds_ptr_t)(buf + bq * 128), 16, 0, 0);
+      }
+    }
+  };
+  // inverse norms of tile j's 256 rows -> LDS slot j & 1 (wave 0; clamped to the padded array,
+  // rows past the range are dead anyway)
+  auto issue_norms = [&](int j, int64_t r0) {
+    if (wave == 0 && j < n_tiles) {
+      const int64_t src = min(r0 + 4 * lane, n_pad - 4);
+      __builtin_amdgcn_global_load_lds(inv_norm32 + src,
+                                       (lds_ptr_t)(smem + kG8Norm + (j & 1) * 1024), 16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  const uint32_t co0 = (uint32_t)((((lane >> 4)) ^ (lane & 7)) << 4);
+  const uint32_t co1 = co0 ^ 64u;
+  const uint32_t rowP = (uint32_t)(128 * wp + (lane & 15)) * 128u;
+  const uint32_t rowQ = (uint32_t)(64 * wq + (lane & 15)) * 128u + kG8Img;
+  u32x4 pf[4][2], qf[2][2];
+  auto read_p = [&](int par, int ph) {
+    const uint32_t a0 = lds0 + par * kG8Buf + rowP + co0 + ph * 64 * 128;
+    const uint32_t a1 = lds0 + par * kG8Buf + rowP + co1 + ph * 64 * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pf[i][0]) : "v"(a0), "i"(i * 2048));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pf[i][1]) : "v"(a1), "i"(i * 2048));
+    }
+  };
+  auto read_q = [&](int par, int qh) {
+    const uint32_t a0 = lds0 + par * kG8Buf + rowQ + co0 + qh * 32 * 128;
+    const uint32_t a1 = lds0 + par * kG8Buf + rowQ + co1 + qh * 32 * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(qf[i][0]) : "v"(a0), "i"(i * 2048));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(qf[i][1]) : "v"(a1), "i"(i * 2048));
+    }
+  };
+  auto frags_ready = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(pf[0][0]), "+v"(pf[0][1]), "+v"(pf[1][0]), "+v"(pf[1][1]),
+                   "+v"(pf[2][0]), "+v"(pf[2][1]), "+v"(pf[3][0]), "+v"(pf[3][1]),
+                   "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1])::"memory");
+  };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  auto quadrant = [&](int ph, int qh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[4 * ph + i][2 * qh + jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              __builtin_bit_cast(half8, pf[i][s2]), __builtin_bit_cast(half8, qf[jj][s2]),
+              acc[4 * ph + i][2 * qh + jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // per lane and query block qn (query 64 wq + 16 qn + (l & 15)): 2-deep list + discarded bound
+  float sl[4][2], dl[4];
+  int32_t il[4][2];
+#pragma unroll
+  for (int qn = 0; qn < 4; ++qn) {
+    dl[qn] = kNegInf;
+    sl[qn][0] = sl[qn][1] = kNegInf;
+    il[qn][0] = il[qn][1] = -1;
+  }
+  constexpr float kDead = -1.0e38f;
+  const uint32_t norm_lane = lds0 + kG8Norm + (uint32_t)(128 * wp + 4 * (lane >> 4)) * 4u;
+  auto epilogue = [&](int j) {
+    const int64_t r0 = cur.r0;
+    const int64_t live_rows = hi - r0;  // rows of the tile inside the range
+    uint64_t mw0 = ~0ull, mw1 = ~0ull;  // filter bits of rows r0 + 128 wp + [0, 128)
+    if (row_mask) {
+      const int64_t rb = r0 + 128 * wp;  // a multiple of 32 (ranges start on 32-row tiles)
+      const int64_t w0 = rb >> 6;
+      const int sh = (int)(rb & 63);
+      const int64_t n_words = (n_rows + 63) >> 6;
+      const uint64_t a = w0 < n_words ? row_mask[w0] : 0ull;
+      const uint64_t b = w0 + 1 < n_words ? row_mask[w0 + 1] : 0ull;
+      const uint64_t c = w0 + 2 < n_words ? row_mask[w0 + 2] : 0ull;
+      mw0 = sh ? (a >> sh) | (b << (64 - sh)) : a;
+      mw1 = sh ? (b >> sh) | (c << (64 - sh)) : b;
+    }
+    const uint32_t na = norm_lane + (uint32_t)(j & 1) * 1024u;
+    const int32_t rbase = (int32_t)(r0 + 128 * wp + 4 * (lane >> 4));
+    auto row_of = [&](float b) {
+      const int32_t code = (int32_t)(__float_as_uint(b) & 31u);
+      return rbase + 16 * (code >> 2) + (code & 3);
+    };
+    // live bit pm*4 + e of the lane's 32 rows (range end, filter); NaN norms are checked per read
+    uint32_t lbits = 0;
+#pragma unroll
+    for (int pm = 0; pm < 8; ++pm) {
+      const int rl = 128 * wp + 16 * pm + 4 * (lane >> 4);  // tile row of register 0
+      const uint64_t mw = pm < 4 ? mw0 : mw1;
+      const int sh = 16 * (pm & 3) + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        lbits |= ((rl + e < live_rows) && ((mw >> (sh + e)) & 1ull)) ? (1u << (pm * 4 + e)) : 0u;
+    }
+    // one query block at a time (3 chain registers live, not 12); the 8 inverse-norm reads per
+    // block are repeated per block (LDS, cheap). The opaque copy of the live bits keeps the
+    // compiler from hoisting 32 per-row (scale, bias) selects out of the qn loop (register spill).
+#pragma unroll
+    for (int qn = 0; qn < 4; ++qn) {
+      float b1 = kNegInf, b2 = kNegInf, b3 = kNegInf;
+      uint32_t lq = lbits;
+      asm volatile("" : "+v"(lq));
+#pragma unroll
+      for (int pm = 0; pm < 8; ++pm) {
+        f32x4v iv;
+        asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(iv) : "v"(na), "i"(pm * 64) : "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = iv[e];
+          const bool live = ((lq >> (pm * 4 + e)) & 1u) && x == x;
+          const float y = __builtin_fmaf(acc[pm][qn][e], live ? x : 0.0f,
+                                         live ? 0.0f : -3.4028234663852886e38f);
+          const float en = __uint_as_float((__float_as_uint(y) & ~31u) | (uint32_t)(pm * 4 + e));
+          const float t = fminf(b1, en);
+          b1 = fmaxf(b1, en);
+          const float t2 = fminf(b2, t);
+          b2 = fmaxf(b2, t);
+          b3 = fmaxf(b3, t2);
+        }
+        acc[pm][qn] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+      if (b1 > kDead) topm_insert<2>(b1, row_of(b1), sl[qn], il[qn], dl[qn]);
+      if (b2 > kDead) topm_insert<2>(b2, row_of(b2), sl[qn], il[qn], dl[qn]);
+      if (b3 > kDead) dl[qn] = fmaxf(dl[qn], b3);
+    }
+  };
+
+  issue_norms(0, cur.r0);
+  issue_half(0, 0, 0, 0, 0);
+  issue_half(0, 0, 0, 1, 0);
+  issue_half(0, 0, 0, 1, 1);
+  issue_half(0, 0, 0, 0, 1);
+  issue_half(1, 0, 1, 0, 0);
+  issue_half(1, 0, 1, 1, 1);
+  if (total > 1) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int j = 0, kt = 0;
+  for (int64_t st = 0; st < total; ++st) {
+    const int par = (int)(st & 1);
+    read_p(par, 0);
+    read_q(par, 0);
+    issue_half(st + 1, kt, 1, 0, 1);
+    if (kt == 1) issue_norms(j + 1, nxt.r0);  // slot (j+1)&1 was last read by epilogue(j-1)
+    __builtin_amdgcn_s_barrier();
+    frags_ready();
+    quadrant(0, 0);
+    __builtin_amdgcn_s_barrier();
+    read_q(par, 1);
+    issue_half(st + 1, kt, 1, 1, 0);
+    frags_ready();
+    quadrant(0, 1);
+    __builtin_amdgcn_s_barrier();
+    read_p(par, 1);
+    issue_half(st + 2, kt, 2, 0, 0);
+    frags_ready();
+    quadrant(1, 1);
+    __builtin_amdgcn_s_barrier();
+    read_q(par, 0);
+    issue_half(st + 2, kt, 2, 1, 1);
+    frags_ready();
+    quadrant(1, 0);
+    if (st + 2 < total) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (++kt == nK) {
+      epilogue(j);
+      kt = 0;
+      ++j;
+      cur = nxt;
+      nxt = tile_src(j + 1);
+    }
+  }
+
+  // Workgroup merge: per query the 8 lanes' 2-deep lists (16 entries) sorted descending + the
+  // largest discarded score, through LDS (buffer 0: every DMA has landed, the loop ended on a
+  // vmcnt(0) and a barrier)
+  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + 256 * 16 * 4);     // [256][16]
+  float* lbnd = reinterpret_cast<float*>(smem + 256 * 16 * 8);        // [256][8]
+  const int grp = 4 * wp + (lane >> 4);
+#pragma unroll
+  for (int qn = 0; qn < 4; ++qn) {
+    const int ql = 64 * wq + 16 * qn + (lane & 15);
+    lkey[ql * 16 + 2 * grp] = sl[qn][0];
+    lkey[ql * 16 + 2 * grp + 1] = sl[qn][1];
+    lrow[ql * 16 + 2 * grp] = il[qn][0];
+    lrow[ql * 16 + 2 * grp + 1] = il[qn][1];
+    lbnd[ql * 8 + grp] = dl[qn];
+  }
+  __syncthreads();
+  if (tid < 256 && q_base + tid < nq) {
+    float key[16];
+    int32_t row[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      key[e] = lkey[tid * 16 + e];
+      row[e] = lrow[tid * 16 + e];
+    }
+    // bitonic sort of 16 in registers: descending by (key, row ascending)
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1)
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int o = e ^ stride;
+          if (o > e) {
+            const bool desc = (e & size) == 0;
+            const bool o_better = armi::approx_better(key[o], row[o], key[e], row[e]);
+            if (o_better == desc) {
+              const float tk = key[e]; key[e] = key[o]; key[o] = tk;
+              const int32_t tr = row[e]; row[e] = row[o]; row[o] = tr;
+            }
+          }
+        }
+    float bnd = kNegInf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bnd = fmaxf(bnd, lbnd[tid * 8 + e]);
+    const size_t base = (size_t)rp * nq + q_base + tid;
+#pragma unroll
+    for (int e = 0; e < kKW; ++e) {
+      cand_key[base * kKW + e] = key[e];
+      cand_row[base * kKW + e] = row[e];
+    }
+    cand_bound[base] = bnd;
+  }
+}
+
 // This lane's DIM/64 contiguous fp16 elements of a vector, as raw 8-byte words.
 template <int DIM>
 __device__ __forceinline__ void load_raw(const uint16_t* __restrict__ v, int lane,
@@ -2945,10 +3296,11 @@ int gemm_ablate() {
 // kernel (ARMI_GEMM_FORM=glds) or the phase-pipelined one (ARMI_GEMM_FORM=p8). Measured at the
 // 10M / 8-way per-rank shape: w4 1.49 ms, glds 1.67-1.78 ms, p8 2.00 ms; at 1M rows G = 4 / 8:
 // w4 196 / 171-186 us, glds 243 / 243 us (profiles/r02_w4_scan_ab.txt, r02_p8_scan_ab.txt).
-enum class GemmForm { W4, GLDS, P8 };
+enum class GemmForm { W4, GLDS, P8, G8 };
 GemmForm gemm_form() {
   static const GemmForm f = [] {
     const char* e = getenv("ARMI_GEMM_FORM");
+    if (e && e[0] == 'g' && e[1] == '8') return GemmForm::G8;
     if (e && e[0] == 'g') return GemmForm::GLDS;
     if (e && e[0] == 'p') return GemmForm::P8;
     return GemmForm::W4;
@@ -3158,7 +3510,13 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     // the four-wave kernel addresses a range's rows with 32-bit byte offsets
     const bool w4_fits = (gp.rows_per_range + kG2Rows) * (int64_t)DIM * 2 < (int64_t(1) << 32);
-    if (glds && gemm_form() == GemmForm::W4 && w4_fits) {
+    if (glds && gemm_form() == GemmForm::G8) {
+      if (int rc = allow_lds(dense_gemm_scan_g8_kernel<DIM>, kG8Lds)) return rc;
+      dense_gemm_scan_g8_kernel<DIM><<<dim3(gp.grid), dim3(kG8Threads), kG8Lds, stream>>>(
+          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
+          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
+      ARMI_LAUNCHED("dense_gemm_scan_g8_kernel");
+    } else if (glds && gemm_form() == GemmForm::W4 && w4_fits) {
       auto kern = dense_gemm_scan_w4_kernel<DIM, 0>;
 #ifdef ARMI_PROBE_BUILD
       switch (gemm_ablate()) {
