@@ -2163,7 +2163,8 @@ constexpr int kG8Threads = 512;
 constexpr int kG8Img = 256 * 64 * 2;       // one operand image of a K-tile (32 KB)
 constexpr int kG8Buf = 2 * kG8Img;         // rows + queries
 constexpr int kG8Norm = 2 * kG8Buf;        // two 1-KB inverse-norm slots (tile parity)
-constexpr size_t kG8Lds = 2 * kG8Buf + 2 * 1024;
+constexpr int kG8List = kG8Norm + 2 * 1024;  // lane lists: [qn 4][field 3][thread 512] dwords
+constexpr size_t kG8Lds = kG8List + 4 * 3 * kG8Threads * 4;
 
 struct G8Src {
   const unsigned char* p;  // first row of the tile (scalar base)
@@ -2311,14 +2312,18 @@ __global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // per lane and query block qn (query 64 wq + 16 qn + (l & 15)): 2-deep list + discarded bound
-  float sl[4][2], dl[4];
-  int32_t il[4][2];
+  // per lane and query block qn (query 64 wq + 16 qn + (l & 15)): a 2-deep list in LDS (the
+  // lane's own dwords: key 0, key 1 with the row code in the low mantissa bits, and the two
+  // entries' tile indices as 16-bit halves; 12 live registers less than a register list, which
+  // the 128 accumulator + 48 fragment registers cannot spare) + the discarded bound in a register
+  float dl[4];
+  const uint32_t lst = lds0 + kG8List + (uint32_t)tid * 4u;
 #pragma unroll
   for (int qn = 0; qn < 4; ++qn) {
     dl[qn] = kNegInf;
-    sl[qn][0] = sl[qn][1] = kNegInf;
-    il[qn][0] = il[qn][1] = -1;
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(kNegInf), "i"((qn * 3 + 0) * 2048) : "memory");
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(kNegInf), "i"((qn * 3 + 1) * 2048) : "memory");
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(0u), "i"((qn * 3 + 2) * 2048) : "memory");
   }
   constexpr float kDead = -1.0e38f;
   const uint32_t norm_lane = lds0 + kG8Norm + (uint32_t)(128 * wp + 4 * (lane >> 4)) * 4u;
@@ -2338,11 +2343,6 @@ __global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
       mw1 = sh ? (b >> sh) | (c << (64 - sh)) : b;
     }
     const uint32_t na = norm_lane + (uint32_t)(j & 1) * 1024u;
-    const int32_t rbase = (int32_t)(r0 + 128 * wp + 4 * (lane >> 4));
-    auto row_of = [&](float b) {
-      const int32_t code = (int32_t)(__float_as_uint(b) & 31u);
-      return rbase + 16 * (code >> 2) + (code & 3);
-    };
     // live bit pm*4 + e of the lane's 32 rows (range end, filter); NaN norms are checked per read
     uint32_t lbits = 0;
 #pragma unroll
@@ -2382,9 +2382,26 @@ __global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
         }
         acc[pm][qn] = f32x4v{0.f, 0.f, 0.f, 0.f};
       }
-      if (b1 > kDead) topm_insert<2>(b1, row_of(b1), sl[qn], il[qn], dl[qn]);
-      if (b2 > kDead) topm_insert<2>(b2, row_of(b2), sl[qn], il[qn], dl[qn]);
-      if (b3 > kDead) dl[qn] = fmaxf(dl[qn], b3);
+      if (b1 > kDead) {  // (b2, b3 <= b1: nothing to do for a dead or empty b1)
+        float sl[2];
+        uint32_t pj;
+        asm volatile("ds_read_b32 %0, %3 offset:%4\n\tds_read_b32 %1, %3 offset:%5\n\t"
+                     "ds_read_b32 %2, %3 offset:%6\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(sl[0]), "=v"(sl[1]), "=v"(pj)
+                     : "v"(lst), "i"((qn * 3 + 0) * 2048), "i"((qn * 3 + 1) * 2048),
+                       "i"((qn * 3 + 2) * 2048)
+                     : "memory");
+        int32_t il[2] = {(int32_t)(pj & 0xffffu), (int32_t)(pj >> 16)};
+        topm_insert<2>(b1, j, sl, il, dl[qn]);
+        if (b2 > kDead) topm_insert<2>(b2, j, sl, il, dl[qn]);
+        if (b3 > kDead) dl[qn] = fmaxf(dl[qn], b3);
+        pj = (uint32_t)il[0] | ((uint32_t)il[1] << 16);
+        asm volatile("ds_write_b32 %0, %1 offset:%3\n\tds_write_b32 %0, %2 offset:%4\n\t"
+                     "ds_write_b32 %0, %5 offset:%6"
+                     ::"v"(lst), "v"(sl[0]), "v"(sl[1]), "i"((qn * 3 + 0) * 2048),
+                       "i"((qn * 3 + 1) * 2048), "v"(pj), "i"((qn * 3 + 2) * 2048)
+                     : "memory");
+      }
     }
   };
 
@@ -2448,13 +2465,22 @@ __global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
   int32_t* lrow = reinterpret_cast<int32_t*>(smem + 256 * 16 * 4);     // [256][16]
   float* lbnd = reinterpret_cast<float*>(smem + 256 * 16 * 8);        // [256][8]
   const int grp = 4 * wp + (lane >> 4);
+  const int64_t rbase = lo + 128 * wp + 4 * (lane >> 4);
+  const float* lsf = reinterpret_cast<const float*>(smem + kG8List);
+  const uint32_t* lsu = reinterpret_cast<const uint32_t*>(smem + kG8List);
 #pragma unroll
   for (int qn = 0; qn < 4; ++qn) {
     const int ql = 64 * wq + 16 * qn + (lane & 15);
-    lkey[ql * 16 + 2 * grp] = sl[qn][0];
-    lkey[ql * 16 + 2 * grp + 1] = sl[qn][1];
-    lrow[ql * 16 + 2 * grp] = il[qn][0];
-    lrow[ql * 16 + 2 * grp + 1] = il[qn][1];
+    const uint32_t pj = lsu[(qn * 3 + 2) * kG8Threads + tid];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float key = lsf[(qn * 3 + e) * kG8Threads + tid];
+      const uint32_t code = __float_as_uint(key) & 31u;
+      const int64_t tile = e ? (pj >> 16) : (pj & 0xffffu);
+      const int64_t row = rbase + 256 * tile + 16 * (code >> 2) + (code & 3);
+      lkey[ql * 16 + 2 * grp + e] = key;
+      lrow[ql * 16 + 2 * grp + e] = key > kDead ? (int32_t)row : -1;
+    }
     lbnd[ql * 8 + grp] = dl[qn];
   }
   __syncthreads();

@@ -135,14 +135,18 @@ class CrossEncoderXLMR:
 
     # Linear layers of the fp16 forward: "armi" = armi_enc_linear_f16 (hand-written gfx950 GEMM,
     # bias / bias + exact-erf GELU fused into the epilogue: no separate GELU pass), "torch" = torch's
-    # hipBLASLt linear + armi_enc_gelu_f16 (A/B). ARMI_RERANK_GEMM selects.
-    gemm_impl = os.environ.get("ARMI_RERANK_GEMM", "armi")
+    # hipBLASLt linear + armi_enc_gelu_f16. "mixed" (default) = armi for the FFN-up GEMM only, whose
+    # fused GELU saves the activation round trip (2.14 ms vs 2.22 + 0.55 ms per layer at 1,280 x
+    # 256 tokens), hipBLASLt for the other three, where it is 18-28 % faster than the hand-written
+    # GEMM (profiles/r03c_gemm.log). ARMI_RERANK_GEMM selects.
+    gemm_impl = os.environ.get("ARMI_RERANK_GEMM", "mixed")
 
     def _lin(self, x: torch.Tensor, ly: dict, name: str, gelu: bool = False) -> torch.Tensor:
         """y = x . W^T + b (+ exact GELU) for weight `name` of layer ly, fp16 in / out."""
         w, b = ly[name + "_h"], ly[{"wqkv": "bqkv", "wo": "bo", "wi": "bi", "wo2": "bo2"}[name]]
         n, k = w.shape
-        if self.gemm_impl == "armi" and n % 256 == 0 and k % 64 == 0 and k >= 128:
+        own = self.gemm_impl == "armi" or (self.gemm_impl == "mixed" and gelu)
+        if own and n % 256 == 0 and k % 64 == 0 and k >= 128:
             out = torch.empty((x.shape[0], n), dtype=torch.float16, device=self.device)
             call("armi_enc_linear_f16", ptr(x), ptr(w), ptr(b), ptr(out), x.shape[0], n, k,
                  1 if gelu else 0, stream_handle())
