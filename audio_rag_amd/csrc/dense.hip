@@ -379,7 +379,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     int guard, const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr,
-    int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap) {
+    int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap,
+    int32_t* __restrict__ heads) {
   static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
   constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
@@ -443,17 +444,61 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
     return queries + (size_t)q * DIM;
   };
+  // Tile schedule. Static (heads == nullptr: the collect pass, multi-block calls): workgroup rp
+  // owns tiles [rp * tiles_per_wg, ...), wave w every kWaves-th from w. Dynamic (heads, one
+  // 64-query block, round 3): the waves of a fixed static split finish up to ~15 % apart (per-CU
+  // and per-XCD bandwidth differ), which left a ~25 us tail at 1M rows; instead the tiles form 8
+  // contiguous parts, one per XCD (workgroup rp runs on XCD rp % 8), each wave takes one static
+  // tile of its XCD's part and then dequeues tiles one at a time from the part's head counter
+  // (one returning device-scope atomic per tile, issued at the top of a tile and consumed
+  // GROUPS - DEPTH groups later, when the next tile's loads start), and a wave whose part is
+  // exhausted steals from the other parts. Every tile is scanned by exactly one wave; the
+  // candidate lists and bounds of a workgroup cover whatever tiles its waves scanned.
+  const bool dyn = heads != nullptr;
   const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
-  int64_t t = t_begin + wave;
+  const int xcd = rp & 7;
+  const int64_t part = (n_tiles + 7) >> 3;
+  auto pb = [&](int y) -> int64_t {  // first tile of part y (pb(8) = n_tiles)
+    const int64_t b = (int64_t)y * part;
+    return b < n_tiles ? b : n_tiles;
+  };
+  auto nstat = [&](int y) -> int64_t {  // static tiles of part y = waves on XCD y
+    return y < n_ranges ? (int64_t)kWaves * ((n_ranges - 1 - y) / 8 + 1) : 0;
+  };
+  uint32_t gone = 0;  // parts this wave found exhausted
+  int ypref = xcd;    // part dequeued from
+  auto steal = [&]() -> int64_t {  // synchronous dequeue over the parts not yet exhausted
+    for (int d = 0; d < 8; ++d) {
+      const int y = (ypref + d) & 7;
+      if ((gone >> y) & 1u) continue;
+      int v = 0;
+      if (lane == 0) v = atomicAdd(heads + 32 * y, 1);
+      v = __builtin_amdgcn_readfirstlane(v);
+      const int64_t tt = pb(y) + nstat(y) + v;
+      if (tt < pb(y + 1)) {
+        ypref = y;
+        return tt;
+      }
+      gone |= 1u << y;
+    }
+    return -1;
+  };
+  int64_t t;
+  if (dyn) {
+    t = pb(xcd) + (int64_t)(rp >> 3) * kWaves + wave;
+    if (t >= pb(xcd + 1)) t = steal();
+  } else {
+    t = t_begin + wave < t_end ? t_begin + wave : -1;
+  }
   // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
   // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
   auto row_ptr = [&](int64_t tile) -> const u32x4* {
     return reinterpret_cast<const u32x4*>(rows8 + tile * TILE_ROWS * DIM) + r + 4 * h * 32;
   };
-  const u32x4* cur = row_ptr(t < t_end ? t : t_begin);
+  const u32x4* cur = row_ptr(t >= 0 ? t : 0);
   u32x4 buf[DEPTH][4];
-  if (t < t_end) {
+  if (t >= 0) {
 #pragma unroll
     for (int g = 0; g < DEPTH; ++g)
 #pragma unroll
@@ -588,10 +633,16 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   }
   float d0 = kNegInf, d1 = kNegInf;
 
-  if (t < t_end) {
-    for (; t < t_end; t += kWaves) {
-      const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
-      const u32x4* nxt = row_ptr(tn);
+  if (t >= 0) {
+    int64_t tn = -1;
+    for (; t >= 0; t = tn) {
+      // dynamic: this tile's dequeue, in flight during the first GROUPS - DEPTH groups
+      const int ycur = ypref;
+      const bool pend = dyn && !((gone >> ycur) & 1u);
+      int vpend = 0;
+      if (pend && lane == 0) vpend = atomicAdd(heads + 32 * ycur, 1);
+      const u32x4* nxt = cur;
+      bool has_next = false;
       const int32_t tord = tile_ord[t];  // ordinal of the tile's image row 0 (wave-uniform)
       int qoff = h * kQB + r;
       asm volatile("" : "+v"(qoff));
@@ -600,6 +651,26 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       Acc acc0 = {}, acc1 = {};
 #pragma unroll
       for (int g = 0; g < GROUPS; ++g) {
+        if (g == GROUPS - DEPTH) {  // the next tile, whose loads start now
+          if (dyn) {
+            if (pend) {
+              const int v = __builtin_amdgcn_readfirstlane(vpend);
+              const int64_t tt = pb(ycur) + nstat(ycur) + v;
+              if (tt < pb(ycur + 1)) {
+                tn = tt;
+              } else {
+                gone |= 1u << ycur;
+                tn = steal();
+              }
+            } else {
+              tn = steal();
+            }
+          } else {
+            tn = t + kWaves < t_end ? t + kWaves : -1;
+          }
+          has_next = tn >= 0;
+          nxt = row_ptr(has_next ? tn : t);
+        }
         u32x4 a[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i] = buf[g % DEPTH][i];
@@ -607,7 +678,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(cur + 32 * (8 * (g + DEPTH) + i));
-        } else {
+        } else if (has_next) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
@@ -3055,12 +3126,16 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
   }
 }
 
-// Int8 image order of a row filter: bit p of the output = bit img_to_ord(p) of the caller's
-// ordinal mask (0 for padding positions). One wave per 64 image positions.
-__global__ __launch_bounds__(256) void mask_to_img_kernel(const uint64_t* __restrict__ mask,
-                                                          int64_t n_rows, int64_t T,
-                                                          const int32_t* __restrict__ tile_ord,
-                                                          uint64_t* __restrict__ out) {
+// First kernel of an int8-scan call: zeroes the dynamic tile schedule's 8 head counters (heads,
+// one per 128-B line; nullptr = static schedule) and, with a row filter (mask), writes it in
+// int8 image order: bit p of the output = bit img_to_ord(p) of the caller's ordinal mask (0 for
+// padding positions), one wave per 64 image positions (T = 0: heads only).
+__global__ __launch_bounds__(256) void scan_prep_kernel(const uint64_t* __restrict__ mask,
+                                                        int64_t n_rows, int64_t T,
+                                                        const int32_t* __restrict__ tile_ord,
+                                                        uint64_t* __restrict__ out,
+                                                        int32_t* __restrict__ heads) {
+  if (heads && blockIdx.x == 0 && threadIdx.x < 8) heads[32 * threadIdx.x] = 0;
   const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool bit = false;
   if (pos < T * 32) {
@@ -3259,6 +3334,16 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
 // tiled); with the LDS-DMA tiled scan G=2 377 vs 459 us, G=4 357 vs 281 us
 // (profiles/r01f_scan_form_ab.txt), so the switch stays above two blocks.
 // ARMI_DENSE_SCAN=grouped|tiled forces one of them (A/B measurements).
+// Dynamic tile schedule of the one-block int8 scan (dense_scan_i8_kernel); ARMI_I8_SCHED=static
+// keeps the static split (A/B measurements).
+bool i8_dynamic_schedule() {
+  static const bool dyn = [] {
+    const char* e = getenv("ARMI_I8_SCHED");
+    return !(e && e[0] == 's');
+  }();
+  return dyn;
+}
+
 bool use_gemm_scan(int nq) {
   static const int force = [] {
     const char* e = getenv("ARMI_DENSE_SCAN");
@@ -3436,6 +3521,7 @@ struct Workspace {
   int32_t* col_cnt;    // [nq] rows appended by the collect pass
   int32_t* col_list;   // [nq][kCollectCap] image positions
   uint64_t* mask_img;  // row filter in int8 image order
+  int32_t* heads;      // [8][32] dynamic tile schedule of the int8 scan (one counter per line)
   size_t bytes;
 };
 
@@ -3451,6 +3537,7 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.col_cnt = cv.take<int32_t>(nq);
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
+    w.heads = cv.take<int32_t>(8 * 32);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -3506,11 +3593,14 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   const int64_t T = std::max<int64_t>(idx->n_tiles, 1);
   // the int8 passes (first pass and collect pass) read the filter in image order
   const uint64_t* mask_i8 = nullptr;
-  if (row_mask) {
-    mask_to_img_kernel<<<dim3((unsigned)((T * 32 + 255) / 256)), dim3(256), 0, stream>>>(
-        row_mask, idx->n_rows, T, idx->tile_ord, w.mask_img);
-    ARMI_LAUNCHED("mask_to_img_kernel");
-    mask_i8 = w.mask_img;
+  const bool i8_path = !use_gemm_scan(nq) && use_i8_filter(idx, k);
+  int32_t* heads = i8_path && sp.n_qb == 1 && i8_dynamic_schedule() ? w.heads : nullptr;
+  if (row_mask || heads) {
+    const int64_t Tm = row_mask ? T : 0;
+    scan_prep_kernel<<<dim3((unsigned)std::max<int64_t>(1, (Tm * 32 + 255) / 256)), dim3(256), 0,
+                       stream>>>(row_mask, idx->n_rows, Tm, idx->tile_ord, w.mask_img, heads);
+    ARMI_LAUNCHED("scan_prep_kernel");
+    if (row_mask) mask_i8 = w.mask_img;
   }
   bool i8_first = false;
   if (use_gemm_scan(nq)) {
@@ -3626,7 +3716,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -3661,7 +3751,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
-        w.col_cnt, w.col_list, kCollectCap);
+        w.col_cnt, w.col_list, kCollectCap, nullptr);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;

@@ -49,7 +49,11 @@ def main() -> None:
         merge = (rel[..., 3] - rel[..., 2])[live]
         end = rel[..., 3][live]
         loop_end = rel[..., 2][live]
-        spans.append(dict(entry_spread=float(e.max()), image_mean=float(img.mean()),
+        le = rel[..., 2]
+        xcd_end = [float(np.max(le[x::8][live[x::8]])) if live[x::8].any() else 0.0
+                   for x in range(8)]
+        spans.append(dict(xcd_loop_end_max_spread=float(max(xcd_end) - min(xcd_end)),
+                          entry_spread=float(e.max()), image_mean=float(img.mean()),
                           image_max=float(img.max()), loop_mean=float(loop.mean()),
                           loop_max=float(loop.max()), loop_end_min=float(loop_end.min()),
                           loop_end_max=float(loop_end.max()), merge_mean=float(merge.mean()),
