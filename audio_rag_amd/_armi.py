@@ -66,6 +66,8 @@ SIGNATURES: dict[str, tuple] = {
     "armi_stream_submit": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int64)]),
     "armi_stream_submit_hybrid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                           ctypes.POINTER(c_int64)]),
+    "armi_stream_submit_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                      c_void_p, ctypes.POINTER(c_int64)]),
     "armi_stream_wait": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  ctypes.c_double]),
     "armi_stream_stats": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),

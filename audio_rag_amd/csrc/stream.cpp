@@ -20,6 +20,10 @@
 // answers each query as QdrantRetriever.search's hybrid branch does (qdrant.py:272-298): dense and
 // sparse prefetches of 2k, RRF 1/(rrf_k + pos) with the dense list first, limit k; a query
 // submitted without sparse terms takes the dense branch (qdrant.py:316-323: its dense top-k).
+// armi_stream_submit_ex adds the sparse-only branch (qdrant.py:299-311: the first k of the
+// batch's sparse top-2k list, which is the sparse top-k: one ranking, (score desc, id asc)) and
+// the payload filter (a device row bitmask per batch: a query with another mask seals the
+// collecting batch, which the dispatcher then hands over at once).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -69,6 +73,8 @@ struct Slot {
   int32_t* h_count = nullptr;
   hipEvent_t done = nullptr;
   int status = ARMI_OK;
+  const uint64_t* mask = nullptr;    // the batch's row filter (every query of the batch)
+  bool sealed = false;               // closed early: the next query needs another mask
   // hybrid servers: the batch's sparse query CSR (pinned + device), prefetch lists, fusion
   int nnz = 0;
   int32_t* h_sp_ptr = nullptr;       // [max_batch + 1]
@@ -81,6 +87,9 @@ struct Slot {
   int64_t* d_sp_ids = nullptr;
   int32_t* d_sp_count = nullptr;
   uint32_t* d_sp_flags = nullptr;
+  float* h_sp_scores = nullptr;      // pinned sparse lists (sparse-only queries)
+  int64_t* h_sp_ids = nullptr;
+  int32_t* h_sp_count = nullptr;
   void* d_sp_ws = nullptr;
   int64_t* d_f_ids = nullptr;        // fused [max_batch][k]
   double* d_f_score = nullptr;
@@ -95,7 +104,7 @@ struct Entry {
   int64_t t_submit = 0;
   int64_t t_done = 0;
   int32_t count = 0;
-  int32_t mode = 0;                  // 0 dense branch, 1 hybrid (RRF scores in rank)
+  int32_t mode = 0;                  // 0 dense branch, 1 hybrid (RRF scores in rank), 2 sparse
   int status = ARMI_OK;
 };
 
@@ -107,7 +116,7 @@ struct armi_stream {
   int rrf_k = 2;
   int kp = 0;                               // dense prefetch limit (2k hybrid, k dense)
   size_t sws_bytes = 0;
-  std::vector<int32_t> nnz_of;              // per ring entry: sparse terms of the query
+  std::vector<int32_t> qmode;               // per ring entry: branch (0 dense, 1 hybrid, 2 sparse)
   int k = 0, max_batch = 0, dim = 0;
   int64_t max_wait_ns = 0;
   size_t ws_bytes = 0;
@@ -142,10 +151,10 @@ namespace {
 int launch_slot(armi_stream* s, Slot& sl) {
   const size_t qbytes = (size_t)sl.n * s->dim * sizeof(uint16_t);
   ARMI_HIP(hipMemcpyAsync(sl.d_queries, sl.h_queries, qbytes, hipMemcpyHostToDevice, s->stream));
-  int rc = armi_dense_topk(s->idx, sl.d_queries, sl.n, s->kp, nullptr, sl.d_scores, sl.d_ids,
+  int rc = armi_dense_topk(s->idx, sl.d_queries, sl.n, s->kp, sl.mask, sl.d_scores, sl.d_ids,
                            sl.d_rank, sl.d_count, sl.d_flags, sl.d_ws, s->ws_bytes, s->stream);
   if (rc != ARMI_OK) return rc;
-  if (s->sidx) {
+  if (s->sidx && sl.nnz > 0) {  // (no query of the batch has terms: every answer is dense)
     ARMI_HIP(hipMemcpyAsync(sl.d_sp_ptr, sl.h_sp_ptr, (size_t)(sl.n + 1) * sizeof(int32_t),
                             hipMemcpyHostToDevice, s->stream));
     if (sl.nnz > 0) {
@@ -154,7 +163,7 @@ int launch_slot(armi_stream* s, Slot& sl) {
       ARMI_HIP(hipMemcpyAsync(sl.d_sp_val, sl.h_sp_val, (size_t)sl.nnz * sizeof(float),
                               hipMemcpyHostToDevice, s->stream));
     }
-    rc = armi_sparse_topk(s->sidx, sl.d_sp_ptr, sl.d_sp_idx, sl.d_sp_val, sl.n, s->kp, nullptr,
+    rc = armi_sparse_topk(s->sidx, sl.d_sp_ptr, sl.d_sp_idx, sl.d_sp_val, sl.n, s->kp, sl.mask,
                           sl.d_sp_scores, sl.d_sp_ids, sl.d_sp_count, sl.d_sp_flags, sl.d_sp_ws,
                           s->sws_bytes, s->stream);
     if (rc != ARMI_OK) return rc;
@@ -167,6 +176,13 @@ int launch_slot(armi_stream* s, Slot& sl) {
     ARMI_HIP(hipMemcpyAsync(sl.h_f_score, sl.d_f_score, nf * sizeof(double),
                             hipMemcpyDeviceToHost, s->stream));
     ARMI_HIP(hipMemcpyAsync(sl.h_f_count, sl.d_f_count, (size_t)sl.n * sizeof(int32_t),
+                            hipMemcpyDeviceToHost, s->stream));
+    const size_t ns = (size_t)sl.n * s->kp;
+    ARMI_HIP(hipMemcpyAsync(sl.h_sp_scores, sl.d_sp_scores, ns * sizeof(float),
+                            hipMemcpyDeviceToHost, s->stream));
+    ARMI_HIP(hipMemcpyAsync(sl.h_sp_ids, sl.d_sp_ids, ns * sizeof(int64_t), hipMemcpyDeviceToHost,
+                            s->stream));
+    ARMI_HIP(hipMemcpyAsync(sl.h_sp_count, sl.d_sp_count, (size_t)sl.n * sizeof(int32_t),
                             hipMemcpyDeviceToHost, s->stream));
   }
   const size_t nk = (size_t)sl.n * s->kp;
@@ -190,7 +206,7 @@ void dispatcher_main(armi_stream* s) {
     for (;;) {
       if (s->stop) return;
       Slot& c = s->slots[s->collect];
-      if (c.n == s->max_batch) break;
+      if (c.n == s->max_batch || c.sealed) break;
       if (c.n > 0) {
         const int64_t due = s->first_submit_ns + s->max_wait_ns;
         const int64_t t = now_ns();
@@ -233,7 +249,18 @@ void completer_main(armi_stream* s) {
       const int64_t tk = sl.first_ticket + i;
       Entry& e = s->ring[tk % s->ring_n];
       const size_t o = (size_t)(tk % s->ring_n) * s->k;
-      if (status == ARMI_OK && s->sidx && s->nnz_of[tk % s->ring_n] > 0) {
+      const int qm = s->qmode[tk % s->ring_n];
+      if (status == ARMI_OK && qm == 2) {
+        // sparse-only branch: the first k of the sparse prefetch list, hit.score = the dot
+        const size_t d = (size_t)i * s->kp;
+        e.count = std::min(sl.h_sp_count[i], s->k);
+        for (int j = 0; j < s->k; ++j) {
+          s->r_ids[o + j] = sl.h_sp_ids[d + j];
+          s->r_scores[o + j] = sl.h_sp_scores[d + j];
+          s->r_rank[o + j] = (double)sl.h_sp_scores[d + j];
+        }
+        e.mode = 2;
+      } else if (status == ARMI_OK && qm == 1) {
         // hybrid branch: the fused list, hit.score = the RRF score (rank holds it in fp64)
         const size_t f = (size_t)i * s->k;
         e.count = sl.h_f_count[i];
@@ -263,6 +290,8 @@ void completer_main(armi_stream* s) {
     lk.lock();
     sl.n = 0;
     sl.nnz = 0;
+    sl.mask = nullptr;
+    sl.sealed = false;
     s->launched.pop_front();
     ++s->free_slots;
     s->cv_done.notify_all();
@@ -277,7 +306,8 @@ void free_slot(Slot& sl) {
   if (sl.h_rank) (void)hipHostFree(sl.h_rank);
   if (sl.h_count) (void)hipHostFree(sl.h_count);
   for (void* p : {(void*)sl.h_sp_ptr, (void*)sl.h_sp_idx, (void*)sl.h_sp_val, (void*)sl.h_f_ids,
-                  (void*)sl.h_f_score, (void*)sl.h_f_count})
+                  (void*)sl.h_f_score, (void*)sl.h_f_count, (void*)sl.h_sp_scores,
+                  (void*)sl.h_sp_ids, (void*)sl.h_sp_count})
     if (p) (void)hipHostFree(p);
   for (void* p : {(void*)sl.d_queries, (void*)sl.d_scores, (void*)sl.d_ids, (void*)sl.d_rank,
                   (void*)sl.d_count, (void*)sl.d_flags, sl.d_ws, (void*)sl.d_sp_ptr,
@@ -332,6 +362,9 @@ int alloc_slot(armi_stream* s, Slot& sl) {
     ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_ids), nf * sizeof(int64_t)));
     ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_score), nf * sizeof(double)));
     ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_f_count), nq * sizeof(int32_t)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_scores), nk * sizeof(float)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_ids), nk * sizeof(int64_t)));
+    ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_count), nq * sizeof(int32_t)));
     ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_ptr), (nq + 1) * sizeof(int32_t)));
     ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_idx), nt * sizeof(int32_t)));
     ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_sp_val), nt * sizeof(float)));
@@ -374,7 +407,7 @@ int create_impl(const armi_index* idx, const armi_sparse_index* sidx, int k, int
   if (sidx) s->sws_bytes = armi_sparse_workspace_bytes(sidx, max_batch, s->kp);
   s->ring_n = ring_entries(max_batch);
   s->ring = std::vector<Entry>(s->ring_n);
-  s->nnz_of.assign(s->ring_n, 0);
+  s->qmode.assign(s->ring_n, 0);
   s->r_scores.assign((size_t)s->ring_n * k, 0.f);
   s->r_ids.assign((size_t)s->ring_n * k, -1);
   s->r_rank.assign((size_t)s->ring_n * k, 0.0);
@@ -416,21 +449,32 @@ void stop_impl(armi_stream* s) {
 }
 
 int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
-                const float* sp_val, int nnz, int64_t* ticket) {
+                const float* sp_val, int nnz, int mode, const uint64_t* mask, int64_t* ticket) {
   ARMI_REQUIRE(s && query && ticket, "armi_stream_submit: null pointer argument");
   ARMI_REQUIRE(nnz >= 0 && nnz <= kMaxTerms, "armi_stream_submit: nnz must be in [0, 256]");
   ARMI_REQUIRE(nnz == 0 || (s->sidx && sp_idx && sp_val),
                "armi_stream_submit: sparse terms need a hybrid server and both arrays");
+  ARMI_REQUIRE(mode == ARMI_STREAM_AUTO || mode == ARMI_STREAM_DENSE || mode == ARMI_STREAM_SPARSE,
+               "armi_stream_submit: unknown mode");
+  // the branch (QdrantRetriever.search): terms decide between hybrid / sparse-only and dense
+  const int qm = nnz == 0 || mode == ARMI_STREAM_DENSE ? 0 : (mode == ARMI_STREAM_SPARSE ? 2 : 1);
+  if (qm == 0) nnz = 0;  // a dense-branch query adds nothing to the batch's sparse pass
   std::unique_lock<std::mutex> lk(s->mu);
   for (;;) {
     if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_submit: server stopped");
-    if (s->slots[s->collect].n < s->max_batch) break;
-    s->cv_space.wait(lk);  // collecting batch full and not yet handed over
+    Slot& c = s->slots[s->collect];
+    if (c.n > 0 && !c.sealed && c.mask != mask) {  // another filter: close the collecting batch
+      c.sealed = true;
+      s->cv_dispatch.notify_one();
+    }
+    if (!c.sealed && c.n < s->max_batch) break;
+    s->cv_space.wait(lk);  // collecting batch full (or sealed) and not yet handed over
   }
   Slot& c = s->slots[s->collect];
   const int64_t tk = s->next_ticket++;
   if (c.n == 0) {
     c.first_ticket = tk;
+    c.mask = mask;
     s->first_submit_ns = now_ns();
   }
   std::memcpy(c.h_queries + (size_t)c.n * s->dim, query, (size_t)s->dim * sizeof(uint16_t));
@@ -441,8 +485,8 @@ int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
     }
     c.nnz += nnz;
     c.h_sp_ptr[c.n + 1] = c.nnz;
-    s->nnz_of[tk % s->ring_n] = nnz;
   }
+  s->qmode[tk % s->ring_n] = qm;
   Entry& e = s->ring[tk % s->ring_n];
   e.t_submit = now_ns();
   ++c.n;
@@ -493,13 +537,20 @@ int armi_stream_destroy(armi_stream* s) {
 
 int armi_stream_submit(armi_stream* s, const uint16_t* query, int64_t* ticket) {
   Active a(s);
-  return submit_impl(s, query, nullptr, nullptr, 0, ticket);
+  return submit_impl(s, query, nullptr, nullptr, 0, ARMI_STREAM_AUTO, nullptr, ticket);
 }
 
 int armi_stream_submit_hybrid(armi_stream* s, const uint16_t* query, const int32_t* sp_indices,
                               const float* sp_values, int nnz, int64_t* ticket) {
   Active a(s);
-  return submit_impl(s, query, sp_indices, sp_values, nnz, ticket);
+  return submit_impl(s, query, sp_indices, sp_values, nnz, ARMI_STREAM_AUTO, nullptr, ticket);
+}
+
+int armi_stream_submit_ex(armi_stream* s, const uint16_t* query, const int32_t* sp_indices,
+                          const float* sp_values, int nnz, int mode, const uint64_t* row_mask,
+                          int64_t* ticket) {
+  Active a(s);
+  return submit_impl(s, query, sp_indices, sp_values, nnz, mode, row_mask, ticket);
 }
 
 int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids, double* rank,
@@ -592,7 +643,8 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* 
     const int64_t v = i % n_vectors;
     const int nnz = q_indptr ? q_indptr[v + 1] - q_indptr[v] : 0;
     rc = submit_impl(s, queries + (size_t)v * s->dim, q_indptr ? q_indices + q_indptr[v] : nullptr,
-                     q_indptr ? q_values + q_indptr[v] : nullptr, nnz, &tickets[(size_t)i]);
+                     q_indptr ? q_values + q_indptr[v] : nullptr, nnz, ARMI_STREAM_AUTO, nullptr,
+                     &tickets[(size_t)i]);
     if (rc == ARMI_OK) n_sub.store(i + 1, std::memory_order_release);
   }
   if (rc != ARMI_OK) rc_col.store(rc);  // stops the collector

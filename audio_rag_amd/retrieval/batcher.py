@@ -211,8 +211,11 @@ class StreamServer:
     search_type "dense" answers every query by the dense branch of QdrantRetriever.search
     (qdrant.py:316-323); "hybrid" (a hybrid collection) answers a query that carries sparse
     terms by the hybrid branch (qdrant.py:272-298: prefetch 2k + 2k, RRF, hit.score = the RRF
-    score) and one without by the dense branch, as search() chooses. Filters and the sparse-only
-    mode go through QueryBatcher.
+    score) and one without by the dense branch, as search() chooses; "sparse" answers a query
+    with terms by the sparse-only branch (qdrant.py:299-311: sparse top-k, hit.score = the dot).
+    submit() takes a per-query search_type and filter_metadata as search() does: the filter is
+    the collection's device row bitmask (ChunkCollection.filter_mask), held by the server until
+    the ticket's result is read; the native server batches queries of one filter together.
 
     Lifetime: the collection knows its open servers and closes them before it frees its device
     indexes (ChunkCollection.close: delete_collection, load_collection, attach_collection); close()
@@ -223,14 +226,15 @@ class StreamServer:
                  search_type: str = "dense"):
         from audio_rag_amd import _armi
 
-        if search_type not in ("dense", "hybrid"):
-            raise ValueError("StreamServer search_type must be 'dense' or 'hybrid'")
+        if search_type not in ("dense", "hybrid", "sparse"):
+            raise ValueError("StreamServer search_type must be 'dense', 'hybrid' or 'sparse'")
+        self.search_type = search_type
         self._armi = _armi
         self.retriever = retriever
         self.resolved = retriever._resolve_collection(collection_name)
         self.collection = retriever._collections[self.resolved]
         self.index = self.collection.dense_index  # kept alive for the server's lifetime
-        self.sparse_index = self.collection.sparse_index if search_type == "hybrid" else None
+        self.sparse_index = self.collection.sparse_index if search_type != "dense" else None
         self.hybrid = self.sparse_index is not None
         self.k = top_k or retriever.config.top_k
         self.dim = retriever.embedding_dim
@@ -239,6 +243,7 @@ class StreamServer:
         self._idle = threading.Condition(self._lock)
         self._inflight = 0
         self._closed = False
+        self._masks: dict[int, torch.Tensor] = {}  # ticket -> row filter the batch still reads
         if self.hybrid:
             _armi.call("armi_stream_create_hybrid", self.index.handle, self.sparse_index.handle,
                        self.k, retriever.config.rrf_k, max_batch, float(max_wait_ms) * 1e3,
@@ -269,38 +274,66 @@ class StreamServer:
                 if self._inflight == 0:
                     self._idle.notify_all()
 
+    # QdrantRetriever.search's branch per search_type (qdrant.py:272-332): native mode codes
+    _MODES = {"hybrid": 0, "dense": 1, "sparse": 2}  # ARMI_STREAM_AUTO / _DENSE / _SPARSE
+
     def submit_arrays(self, dense: np.ndarray,
-                      sparse: tuple[np.ndarray, np.ndarray] | None = None) -> int:
-        """dense: [dim] query; sparse: (ascending indices, values) or None. Returns a ticket."""
+                      sparse: tuple[np.ndarray, np.ndarray] | None = None,
+                      filter_metadata: dict | None = None, search_type: str | None = None) -> int:
+        """dense: [dim] query; sparse: (indices, values) or None; filter_metadata / search_type
+        as MI355XRetriever.search (search_type None = the server's). Returns a ticket."""
         q = np.ascontiguousarray(dense, dtype=np.float16).reshape(-1)
         if q.size != self.dim:
             raise RetrievalError(f"query has {q.size} components, the store {self.dim}")
-        ticket = self._armi.ctypes.c_int64()
-        if sparse is not None and self.hybrid and len(sparse[0]) > 0:
+        st = search_type or self.search_type
+        if st not in self._MODES:
+            raise RetrievalError(f"unknown search_type {st!r}")
+        has_terms = sparse is not None and len(sparse[0]) > 0
+        # the sparse lists exist only on a hybrid collection (else search() takes the dense
+        # branch whatever search_type says)
+        wants_sparse = st != "dense" and has_terms and self.collection.hybrid
+        if wants_sparse and not self.hybrid:
+            raise RetrievalError(f"search_type {st!r} needs a server created with search_type "
+                                 "'hybrid' or 'sparse'")
+        idx = val = None
+        nnz = 0
+        if wants_sparse:
             idx, val = _sorted_terms(*sparse)
             if idx.size > 256:
                 raise RetrievalError("a sparse query may hold at most 256 terms")
-            self._call("armi_stream_submit_hybrid", q.ctypes.data, idx.ctypes.data,
-                       val.ctypes.data, idx.size, self._armi.ctypes.byref(ticket))
-        else:
-            self._call("armi_stream_submit", q.ctypes.data, self._armi.ctypes.byref(ticket))
+            nnz = idx.size
+        mask = self.collection.filter_mask(filter_metadata)
+        ticket = self._armi.ctypes.c_int64()
+        self._call("armi_stream_submit_ex", q.ctypes.data,
+                   None if idx is None else idx.ctypes.data,
+                   None if val is None else val.ctypes.data, nnz,
+                   self._MODES[st] if wants_sparse else 1,
+                   None if mask is None else mask.data_ptr(), self._armi.ctypes.byref(ticket))
+        if mask is not None:
+            with self._lock:
+                self._masks[ticket.value] = mask
         return ticket.value
 
-    def submit(self, query: EmbeddingResult) -> int:
+    def submit(self, query: EmbeddingResult, filter_metadata: dict | None = None,
+               search_type: str | None = None) -> int:
         return self.submit_arrays(np.asarray(query.dense, dtype=np.float32),
-                                  query_sparse_arrays(query.sparse))
+                                  query_sparse_arrays(query.sparse), filter_metadata, search_type)
 
     def raw_result(self, ticket: int, timeout: float = 60.0):
-        """(scores [k] (fp64 RRF scores on the hybrid branch, else float32 cosine), ids int64
-        [k], count) of a ticket."""
+        """(scores [k] (fp64 RRF scores on the hybrid branch, else float32 cosine / sparse
+        dot), ids int64 [k], count) of a ticket."""
         scores = np.empty(self.k, dtype=np.float32)
         rank = np.empty(self.k, dtype=np.float64)
         ids = np.empty(self.k, dtype=np.int64)
         count = self._armi.ctypes.c_int32()
         mode = self._armi.ctypes.c_int32()
-        self._call("armi_stream_wait", ticket, scores.ctypes.data, ids.ctypes.data,
-                   rank.ctypes.data, self._armi.ctypes.byref(count),
-                   self._armi.ctypes.byref(mode), timeout * 1e6)
+        try:
+            self._call("armi_stream_wait", ticket, scores.ctypes.data, ids.ctypes.data,
+                       rank.ctypes.data, self._armi.ctypes.byref(count),
+                       self._armi.ctypes.byref(mode), timeout * 1e6)
+        finally:
+            with self._lock:
+                self._masks.pop(ticket, None)
         return (rank if mode.value == 1 else scores), ids, count.value
 
     def result(self, ticket: int, timeout: float = 60.0) -> list[RetrievalResult]:
@@ -319,8 +352,9 @@ class StreamServer:
             out.append(RetrievalResult(chunk=chunk, score=float(score), source=self.resolved))
         return out
 
-    def search(self, query: EmbeddingResult) -> list[RetrievalResult]:
-        return self.result(self.submit(query))
+    def search(self, query: EmbeddingResult, filter_metadata: dict | None = None,
+               search_type: str | None = None) -> list[RetrievalResult]:
+        return self.result(self.submit(query, filter_metadata, search_type))
 
     def stats(self) -> tuple[int, int]:
         b, q = self._armi.ctypes.c_int64(), self._armi.ctypes.c_int64()

@@ -196,9 +196,24 @@ int armi_stream_submit(armi_stream* server, const uint16_t* query, int64_t* tick
 int armi_stream_submit_hybrid(armi_stream* server, const uint16_t* query,
                               const int32_t* sp_indices, const float* sp_values, int nnz,
                               int64_t* ticket);
+/* Branch and filter per query (QdrantRetriever.search's choice, qdrant.py:262-332):
+ * mode ARMI_STREAM_AUTO = hybrid when the query carries terms (hybrid server), else dense;
+ * ARMI_STREAM_DENSE = the dense branch whatever the terms; ARMI_STREAM_SPARSE = sparse-only
+ * (top-k of the sparse dot, hit.score = that dot) when the query carries terms, else dense (the
+ * reference's fallback). Sparse terms need a hybrid server. row_mask (nullable) = a device
+ * bitmask over the store's ordinals (armi_dense_topk's row_mask: the Qdrant payload filter),
+ * caller-owned, unchanged and alive until the ticket's wait has returned; it applies to every
+ * list of the query (dense, sparse, both prefetches). A batch holds queries of one row_mask: a
+ * query with another mask closes the collecting batch (it leaves at once) and opens the next. */
+#define ARMI_STREAM_AUTO 0
+#define ARMI_STREAM_DENSE 1
+#define ARMI_STREAM_SPARSE 2
+int armi_stream_submit_ex(armi_stream* server, const uint16_t* query, const int32_t* sp_indices,
+                          const float* sp_values, int nnz, int mode, const uint64_t* row_mask,
+                          int64_t* ticket);
 /* Blocks until the ticket's result is published (at most timeout_us), then copies its k
  * scores / ids / rank keys (each nullable), the valid count and the branch taken (mode:
- * 0 dense, 1 hybrid; nullable). Results stay readable until R later tickets have been
+ * 0 dense, 1 hybrid, 2 sparse-only; nullable). Results stay readable until R later tickets have been
  * submitted, R = max(2^14, 64 max_batch) rounded up to a power of two (the result ring: R k
  * (4 + 8 + 8) B + 48 R B of host memory, 3.9 MB at k = 10, max_batch 64); an older ticket fails
  * with "result overwritten". */

@@ -248,3 +248,43 @@ def test_stream_server_threshold_and_unsorted_terms(gpu, oracle_mod, store):
             rev = srv.result(srv.submit_arrays(qd[i].view(np.float16), (idx[::-1], val[::-1])))
             want = _expected(oracle_mod, store, i, "hybrid", None)
             assert [(r.chunk.text, r.score) for r in rev] == want, i
+
+
+def test_stream_server_filters_and_search_types(gpu, oracle_mod, store):
+    """Native server, per-query search_type and metadata filter (armi_stream_submit_ex): every
+    branch of QdrantRetriever.search (hybrid, sparse-only, dense; the dense fallback of queries
+    without terms) under the payload filter, from concurrent callers whose filters interleave
+    (each change of filter closes the collecting batch). Answers equal the oracle's."""
+    from audio_rag_amd.core import EmbeddingResult, SparseVector
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    _, _, (qi, qx, qv), qd = store
+    qf = qd.view(np.float16).astype(np.float32)
+    queries = [EmbeddingResult(dense=qf[i].tolist(),
+                               sparse=SparseVector(qx[qi[i]:qi[i + 1]].tolist(),
+                                                   qv[qi[i]:qi[i + 1]].tolist()) if i % 4 else None)
+               for i in range(NQ)]
+    filters = [None if i % 5 else {"lecture": i % 3} for i in range(NQ)]
+    types = ["hybrid", "sparse", "dense"]
+    got = [None] * NQ
+    with StreamServer(ret, max_batch=16, max_wait_ms=3.0, search_type="hybrid") as srv:
+        def client(lo):
+            tickets = [(i, srv.submit(queries[i], filters[i], types[i % 3]))
+                       for i in range(lo, NQ, 3)]
+            for i, t in tickets:
+                got[i] = srv.result(t)
+        ts = [threading.Thread(target=client, args=(c,)) for c in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        batches, served = srv.stats()
+        assert served == NQ and batches < NQ, (batches, served)
+        assert not srv._masks  # every filter reference released with its result
+    for i in range(NQ):
+        want = _expected(oracle_mod, store, i, types[i % 3], filters[i])
+        assert [(r.chunk.text, r.score) for r in got[i]] == want, (i, types[i % 3], filters[i])
+    with StreamServer(ret, max_batch=8, max_wait_ms=0.5) as dense_srv:
+        with pytest.raises(Exception, match="needs a server"):
+            dense_srv.submit(queries[1], None, "sparse")

@@ -5,7 +5,7 @@ TAG=${1:-r03d}
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1; mkdir -p gpurun_out
 j() { tail -1 "$1" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($2)"; }
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
-  tests/test_dense_gpu.py tests/test_dense_collect_gpu.py tests/test_dense_filter_gpu.py \
+  tests/test_dense_gpu.py tests/test_dense_collect_gpu.py tests/test_dense_filter_gpu.py tests/test_batcher_gpu.py \
   > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc $(tail -1 gpurun_out/${TAG}_pytest.log)"
 [ $rc -eq 0 ] || exit $rc
