@@ -3586,7 +3586,7 @@ template <int DIM>
 int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int k,
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                    const Workspace& w, hipStream_t stream) {
+                    const Workspace& w, hipStream_t stream, hipEvent_t scan_done) {
   const ScanPlan sp = plan_scan(idx, k, nq);
   int n_wg = sp.n_wg;
   int kc = sp.kc;
@@ -3729,6 +3729,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     ARMI_LAUNCHED("dense_scan_kernel");
     if (int rc = tl.end()) return rc;
   }
+  if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
   ARMI_REQUIRE(n_wg >= 1 && n_wg * kKW <= kMaxPool,
@@ -3798,6 +3799,14 @@ int armi_dense_topk(const armi_index* idx, const uint16_t* queries, int n_querie
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
                     size_t workspace_bytes, hipStream_t stream) {
+  return armi_dense_topk_ex(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
+                            out_count, out_flags, workspace, workspace_bytes, stream, nullptr);
+}
+
+int armi_dense_topk_ex(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                       const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                       double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
+                       size_t workspace_bytes, hipStream_t stream, hipEvent_t scan_done) {
   ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
   ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
   ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
@@ -3811,6 +3820,7 @@ int armi_dense_topk(const armi_index* idx, const uint16_t* queries, int n_querie
     ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
     ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
     ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
+    if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
     return ARMI_OK;
   }
   const Workspace w = carve(workspace, idx, n_queries, k, true);
@@ -3820,7 +3830,7 @@ int armi_dense_topk(const armi_index* idx, const uint16_t* queries, int n_querie
   return dispatch_dim(idx->dim, [&](auto D) {
     constexpr int DIM = decltype(D)::value;
     return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
-                                out_count, out_flags, w, stream);
+                                out_count, out_flags, w, stream, scan_done);
   });
 }
 

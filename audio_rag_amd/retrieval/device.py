@@ -134,9 +134,11 @@ class DenseIndex:
 
     def topk(self, queries: torch.Tensor, k: int, row_mask: torch.Tensor | None = None,
              exact: bool = False, workspace: torch.Tensor | None = None,
-             out: TopK | None = None) -> TopK:
+             out: TopK | None = None, scan_done: torch.cuda.Event | None = None) -> TopK:
         """Cosine top-k of every query row. row_mask: int64 tensor holding a bitmask of enabled
-        rows (bit r of word r // 64), or None."""
+        rows (bit r of word r // 64), or None. scan_done (fast path): an event recorded on the
+        current stream after the first-pass scan, before the merge (armi_dense_topk_ex), for
+        callers that pipeline batches on two streams."""
         _check_fp16_2d(queries, "queries", self.dim)
         if not 1 <= k <= MAX_K:
             raise ValueError(f"k must be in [1, {MAX_K}]")
@@ -162,6 +164,12 @@ class DenseIndex:
                  workspace.numel(), s)
             if out.flags is not None:
                 out.flags.fill_(_armi.ARMI_FLAG_FALLBACK)
+        elif scan_done is not None:
+            if scan_done.cuda_event == 0:  # torch creates the event at its first record
+                scan_done.record()
+            call("armi_dense_topk_ex", self._handle, ptr(queries), b, k, ptr(row_mask),
+                 ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(out.flags),
+                 ptr(workspace), workspace.numel(), s, scan_done.cuda_event)
         else:
             call("armi_dense_topk", self._handle, ptr(queries), b, k, ptr(row_mask),
                  ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(out.flags),

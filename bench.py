@@ -238,6 +238,9 @@ def main() -> None:
                     help="dense headline at N=1 only: skip the secondary configs1 / configs2 "
                          "objects (each measured by a child bench.py run)")
     ap.add_argument("--latency-iters", type=int, default=30)
+    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
+                    help="dense, 1 GPU: batches in flight on their own HIP streams (2: batch i+1's "
+                         "scan starts when batch i's scan ends, batch i's merge runs beside it)")
     ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
                                            "ingest"],
                     default="dense",
@@ -376,10 +379,33 @@ def main() -> None:
                     rank=torch.gather(probs, 1, order).double(),
                     count=torch.clamp(fused.count, max=k))
 
+    # dense, one GPU: two batches in flight (armi_dense_topk_ex's scan-done event): batch i+1's
+    # stream waits for batch i's first-pass scan, so the scans run back to back while batch i's
+    # merge / second-pass launches run beside batch i+1's scan. Every batch still runs its whole
+    # call (scan, merge, exact rescore, second pass); only the overlap is new.
+    pipe = wl == "dense" and sharded is None and args.pipeline == 2
+    if pipe:
+        p_streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        p_ws = [ws, torch.empty_like(ws)]
+        p_ev = [torch.cuda.Event() for _ in range(2)]
+        p_prev = [None]
+        p_synced = [False, False]
+
     def step(i: int, q_local: torch.Tensor | None = None):
         j = i % n_q_batches
         ql = q_local if q_local is not None else queries[j]
         if wl == "dense":
+            if sharded is None and pipe:
+                st, ev = p_streams[i % 2], p_ev[i % 2]
+                if not p_synced[i % 2]:  # the inputs were made on the default stream
+                    st.wait_stream(torch.cuda.current_stream())
+                    p_synced[i % 2] = True
+                if p_prev[0] is not None:
+                    st.wait_event(p_prev[0])
+                with torch.cuda.stream(st):
+                    out = index.topk(ql, k, workspace=p_ws[i % 2], scan_done=ev)
+                p_prev[0] = ev
+                return out
             if sharded is None:
                 return index.topk(ql, k, workspace=ws)
             return sharded.dense(ql, k)
@@ -501,6 +527,7 @@ def main() -> None:
                                   f"queries per GPU per step"),
             }[wl],
             "n_chunks": n, "dim": dim, "batch_per_gpu": batch, "top_k": k, "corpus": args.corpus,
+            "batches_in_flight": 2 if pipe else 1,
             "parallelism": f"corpus-shard{world}" + ("" if backend == "nccl" or world == 1
                                                       else f" ({backend} rehearsal, shared GPUs)"),
         },

@@ -120,6 +120,16 @@ int armi_dense_topk(const armi_index* index, const uint16_t* queries, int n_quer
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
                     void* workspace, size_t workspace_bytes, hipStream_t stream);
 
+/* armi_dense_topk that also records scan_done (a hipEvent_t, nullable) on `stream` right after
+ * the call's first-pass scan kernel, before its merge / second-pass kernels: a pipelined caller
+ * (two batches on two streams) makes the next batch's stream wait on it, so the next scan starts
+ * as this one ends and this call's merge runs beside it. */
+int armi_dense_topk_ex(const armi_index* index, const uint16_t* queries, int n_queries, int k,
+                       const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                       double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                       void* workspace, size_t workspace_bytes, hipStream_t stream,
+                       hipEvent_t scan_done);
+
 size_t armi_dense_exact_workspace_bytes(const armi_index* index, int n_queries, int k);
 /* Exhaustive exact scan with the same outputs and ranking as armi_dense_topk. */
 int armi_dense_exact_topk(const armi_index* index, const uint16_t* queries, int n_queries, int k,

@@ -215,3 +215,35 @@ def test_full_size_fast_equals_exact(gpu, oracle_mod):
     ref = oracle_mod.dense_topk(rows_u16, q_u16, 5)
     np.testing.assert_array_equal(fast.ids[:2].cpu().numpy(), ref.ids)
     np.testing.assert_array_equal(fast.rank[:2].cpu().numpy(), ref.rank)
+
+
+def test_pipelined_batches_on_two_streams(gpu, oracle_mod):
+    """armi_dense_topk_ex: batches alternating over two streams, each waiting for the previous
+    batch's scan-done event (bench.py's pipelined dense step), with a row filter on every other
+    batch: every answer equals the oracle's (the dynamic tile schedule's heads live in each
+    call's own workspace)."""
+    rows = oracle_mod.unit_fp16(30000, 1024, seed=71)
+    idx = _index(rows, gpu)
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(2)]
+    evs = [torch.cuda.Event() for _ in range(2)]
+    ws = [torch.empty(idx.workspace_bytes(64, 10), dtype=torch.uint8, device=gpu) for _ in range(2)]
+    mask = np.zeros((30000 + 63) // 64, dtype=np.uint64)
+    mask[::3] = np.uint64(0xF0F0F0F0F0F0F0F0)
+    m_dev = _dev(mask.view(np.int64), gpu)
+    qs = [oracle_mod.unit_fp16(64, 1024, seed=72 + i) for i in range(6)]
+    q_dev = [_dev(q.view(np.float16), gpu) for q in qs]
+    torch.cuda.synchronize()
+    outs, prev = [], None
+    for i in range(6):
+        st = streams[i % 2]
+        if prev is not None:
+            st.wait_event(prev)
+        with torch.cuda.stream(st):
+            outs.append(idx.topk(q_dev[i], 10, row_mask=m_dev if i % 2 else None,
+                                 workspace=ws[i % 2], scan_done=evs[i % 2]))
+        prev = evs[i % 2]
+    torch.cuda.synchronize()
+    for i in range(6):
+        ref = oracle_mod.dense_topk(rows, qs[i], 10, row_mask=mask if i % 2 else None)
+        got = {f: getattr(outs[i], f).cpu().numpy() for f in ("ids", "scores", "rank", "count")}
+        _assert_same(got, ref, 10)

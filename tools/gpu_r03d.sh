@@ -10,11 +10,12 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 echo "pytest rc=$rc $(tail -1 gpurun_out/${TAG}_pytest.log)"
 [ $rc -eq 0 ] || exit $rc
 B="--no-extras --no-cpu-baseline --latency-iters 3"
-for sched in dynamic static; do
+for mode in "dynamic 2" "dynamic 1" "static 1"; do
+  set -- $mode
   for args in "" "--top-k 40" "--chunks 100000 --steps 200"; do
-    n=$(echo "$sched $args" | tr ' -' '__')
-    ARMI_I8_SCHED=$sched timeout -k 10 200 python bench.py $B $args > gpurun_out/${TAG}_$n.log 2>&1 || exit $?
-    echo "$sched [$args]: $(j gpurun_out/${TAG}_$n.log 'round(d["value"]), round(d["ms_per_step"],4), round(d["roofline"]["avg_launch_ms"],4), d["certified_frac"]')"
+    n=$(echo "$1 p$2 $args" | tr ' -' '__')
+    ARMI_I8_SCHED=$1 timeout -k 10 200 python bench.py $B --pipeline $2 $args > gpurun_out/${TAG}_$n.log 2>&1 || exit $?
+    echo "$1 pipe$2 [$args]: $(j gpurun_out/${TAG}_$n.log 'round(d["value"]), round(d["ms_per_step"],4), round(d["roofline"]["avg_launch_ms"],4), d["certified_frac"]')"
   done
 done
 bash tools/probes/i8_stamps.sh ${TAG}stp
