@@ -444,53 +444,53 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
     return queries + (size_t)q * DIM;
   };
-  // Tile schedule. Static (heads == nullptr: the collect pass, multi-block calls): workgroup rp
-  // owns tiles [rp * tiles_per_wg, ...), wave w every kWaves-th from w. Dynamic (heads, one
-  // 64-query block, round 3): the waves of a fixed static split finish up to ~15 % apart (per-CU
-  // and per-XCD bandwidth differ), which left a ~25 us tail at 1M rows; instead the tiles form 8
-  // contiguous parts, one per XCD (workgroup rp runs on XCD rp % 8), each wave takes one static
-  // tile of its XCD's part and then dequeues tiles one at a time from the part's head counter
-  // (one returning device-scope atomic per tile, issued at the top of a tile and consumed
-  // GROUPS - DEPTH groups later, when the next tile's loads start), and a wave whose part is
-  // exhausted steals from the other parts. Every tile is scanned by exactly one wave; the
-  // candidate lists and bounds of a workgroup cover whatever tiles its waves scanned.
+  // Tile schedule. Static (heads == nullptr, the default): workgroup rp owns tiles
+  // [rp * tiles_per_wg, ...), wave w every kWaves-th from w. Dynamic (heads; ARMI_I8_SCHED=
+  // dynamic, one 64-query block): each wave starts on the same static tile, then dequeues the
+  // remaining tiles of its XCD's workgroups (workgroup rp runs on XCD rp % 8) from that XCD's head
+  // counter, one returning device-scope atomic per tile (issued at the top of a tile and consumed
+  // GROUPS - DEPTH groups later, when the next tile's loads start), in an order that keeps every
+  // range advancing together (dequeue v -> range i = v % nx, position kWaves + v / nx: the same
+  // spatial spread over the image as the static split), and steals from the other XCDs' heads
+  // once its own is exhausted. Every tile is scanned by exactly one wave; a workgroup's
+  // candidate lists and bound cover whatever tiles its waves scanned.
   const bool dyn = heads != nullptr;
   const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
   const int xcd = rp & 7;
-  const int64_t part = (n_tiles + 7) >> 3;
-  auto pb = [&](int y) -> int64_t {  // first tile of part y (pb(8) = n_tiles)
-    const int64_t b = (int64_t)y * part;
-    return b < n_tiles ? b : n_tiles;
+  const int64_t dyn_per_range = tiles_per_wg > kWaves ? tiles_per_wg - kWaves : 0;
+  auto nx = [&](int y) -> int64_t {  // workgroups (ranges) on XCD y
+    return y < n_ranges ? (int64_t)((n_ranges - 1 - y) / 8 + 1) : 0;
   };
-  auto nstat = [&](int y) -> int64_t {  // static tiles of part y = waves on XCD y
-    return y < n_ranges ? (int64_t)kWaves * ((n_ranges - 1 - y) / 8 + 1) : 0;
+  uint32_t gone = 0;  // XCD heads this wave found exhausted
+  int ypref = xcd;    // head dequeued from
+  // tile of dequeue v on XCD y's head: >= 0 a tile, -1 exhausted, -2 a hole (short last range)
+  auto decode = [&](int y, int64_t v) -> int64_t {
+    const int64_t n = nx(y);
+    if (v >= n * dyn_per_range) return -1;
+    const int64_t g = y + 8 * (v % n);
+    const int64_t tt = g * tiles_per_wg + kWaves + v / n;
+    return tt < min((g + 1) * (int64_t)tiles_per_wg, n_tiles) ? tt : -2;
   };
-  uint32_t gone = 0;  // parts this wave found exhausted
-  int ypref = xcd;    // part dequeued from
-  auto steal = [&]() -> int64_t {  // synchronous dequeue over the parts not yet exhausted
+  auto steal = [&]() -> int64_t {  // synchronous dequeue over the heads not yet exhausted
     for (int d = 0; d < 8; ++d) {
       const int y = (ypref + d) & 7;
-      if ((gone >> y) & 1u) continue;
-      int v = 0;
-      if (lane == 0) v = atomicAdd(heads + 32 * y, 1);
-      v = __builtin_amdgcn_readfirstlane(v);
-      const int64_t tt = pb(y) + nstat(y) + v;
-      if (tt < pb(y + 1)) {
-        ypref = y;
-        return tt;
+      while (!((gone >> y) & 1u)) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(heads + 32 * y, 1);
+        v = __builtin_amdgcn_readfirstlane(v);
+        const int64_t tt = decode(y, v);
+        if (tt >= 0) {
+          ypref = y;
+          return tt;
+        }
+        if (tt == -1) gone |= 1u << y;
       }
-      gone |= 1u << y;
     }
     return -1;
   };
-  int64_t t;
-  if (dyn) {
-    t = pb(xcd) + (int64_t)(rp >> 3) * kWaves + wave;
-    if (t >= pb(xcd + 1)) t = steal();
-  } else {
-    t = t_begin + wave < t_end ? t_begin + wave : -1;
-  }
+  int64_t t = t_begin + wave < t_end ? t_begin + wave : -1;
+  if (dyn && t < 0) t = steal();
   // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
   // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
   auto row_ptr = [&](int64_t tile) -> const u32x4* {
@@ -655,11 +655,11 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
           if (dyn) {
             if (pend) {
               const int v = __builtin_amdgcn_readfirstlane(vpend);
-              const int64_t tt = pb(ycur) + nstat(ycur) + v;
-              if (tt < pb(ycur + 1)) {
+              const int64_t tt = decode(ycur, v);
+              if (tt >= 0) {
                 tn = tt;
               } else {
-                gone |= 1u << ycur;
+                if (tt == -1) gone |= 1u << ycur;
                 tn = steal();
               }
             } else {
@@ -3334,12 +3334,14 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
 // tiled); with the LDS-DMA tiled scan G=2 377 vs 459 us, G=4 357 vs 281 us
 // (profiles/r01f_scan_form_ab.txt), so the switch stays above two blocks.
 // ARMI_DENSE_SCAN=grouped|tiled forces one of them (A/B measurements).
-// Dynamic tile schedule of the one-block int8 scan (dense_scan_i8_kernel); ARMI_I8_SCHED=static
-// keeps the static split (A/B measurements).
+// Tile schedule of the one-block int8 scan (dense_scan_i8_kernel): static split (default) or,
+// with ARMI_I8_SCHED=dynamic, static first tiles + per-XCD dequeue. Round-3 A/B at 1M rows
+// (profiles/r03d_*): the first dynamic form (contiguous per-XCD parts) scanned in 0.248 ms vs
+// 0.231 ms static: its loop ran slower and its final steal round trips kept a tail.
 bool i8_dynamic_schedule() {
   static const bool dyn = [] {
     const char* e = getenv("ARMI_I8_SCHED");
-    return !(e && e[0] == 's');
+    return e && e[0] == 'd';
   }();
   return dyn;
 }

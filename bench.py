@@ -238,7 +238,7 @@ def main() -> None:
                     help="dense headline at N=1 only: skip the secondary configs1 / configs2 "
                          "objects (each measured by a child bench.py run)")
     ap.add_argument("--latency-iters", type=int, default=30)
-    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
+    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=1,
                     help="dense, 1 GPU: batches in flight on their own HIP streams (2: batch i+1's "
                          "scan starts when batch i's scan ends, batch i's merge runs beside it)")
     ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
