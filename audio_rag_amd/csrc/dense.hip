@@ -498,12 +498,18 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   };
   const u32x4* cur = row_ptr(t >= 0 ? t : 0);
   u32x4 buf[DEPTH][4];
-  if (t >= 0) {
+  // the first tile's first DEPTH groups. The fp16 query image issues its own (L2-resident) loads
+  // first: vmcnt counts in issue order, so an image behind this 16-load HBM burst would wait for
+  // all of it before writing LDS (round 3: the image phase took ~11 us of every launch).
+  auto prefetch_first = [&]() {
+    if (t >= 0) {
 #pragma unroll
-    for (int g = 0; g < DEPTH; ++g)
+      for (int g = 0; g < DEPTH; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) buf[g][i] = i8_load(cur + 32 * (8 * g + i));
-  }
+        for (int i = 0; i < 4; ++i) buf[g][i] = i8_load(cur + 32 * (8 * g + i));
+    }
+  };
+  if constexpr (QI8) prefetch_first();
 
   // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13) and, QI8,
   //    t_q and e_q (rounded up, plus 2^-20 |q| for the rounding of t_q * q8_i). Then the
@@ -524,6 +530,9 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
       v[i] = q < nq ? *reinterpret_cast<const u32x4*>(qrow(q) + off) : u32x4{0u, 0u, 0u, 0u};
     }
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch_first();
+    __builtin_amdgcn_sched_barrier(0);
     float ss = 0.0f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
