@@ -23,3 +23,11 @@ for rep in 1 2; do
 done
 ARMI_I8_SCHED=static bash tools/probes/i8_stamps.sh ${TAG}stps || exit $?
 ARMI_I8_SCHED=dynamic bash tools/probes/i8_stamps.sh ${TAG}stpd || exit $?
+ARMI_LINEAR_STAGE=vgpr timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gemm_gpu.py > gpurun_out/${TAG}_pytest_gemm_vgpr.log 2>&1; rc=$?
+echo "pytest gemm vgpr rc=$rc $(tail -1 gpurun_out/${TAG}_pytest_gemm_vgpr.log)"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/probes/gemm_bench.py > gpurun_out/${TAG}_gemm_dma.log 2>&1 || exit $?
+ARMI_LINEAR_STAGE=vgpr timeout -k 10 300 python tools/probes/gemm_bench.py > gpurun_out/${TAG}_gemm_vgpr.log 2>&1 || exit $?
+echo "gemm dma:"; grep shape gpurun_out/${TAG}_gemm_dma.log | cut -c1-200
+echo "gemm vgpr:"; grep shape gpurun_out/${TAG}_gemm_vgpr.log | cut -c1-200
