@@ -2767,6 +2767,19 @@ __device__ __forceinline__ float f32_round_down(double x) {
 // sel_col (J) / sel_rank (r): t0 = the r-th largest of the workgroup lists' J-th entries. r lists
 // hold >= J entries >= t0 each, so the pool holds >= r J >= kc entries >= t0 and its kc-th best is
 // >= t0 (host: the smallest J with r = ceil(kc / J) <= n_wg; with r > n_wg, t0 = -inf).
+// Probe builds only (-DARMI_PROBE_BUILD -DARMI_I8_STAMPS): s_memrealtime per merge workgroup
+// (thread 0) at entry and after each phase, read back with the scan's stamps.
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_STAMPS)
+__device__ uint64_t g_merge_stamps[64 * 8];
+#define MERGE_STAMP(slot)                                                            \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 64)                                         \
+      g_merge_stamps[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define MERGE_STAMP(slot) do {} while (0)
+#endif
+
 template <int DIM>
 __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
@@ -2790,6 +2803,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   const int lane = tid & 63;
   const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
+  MERGE_STAMP(0);
 
   // One memory round trip for everything the selection needs: the pool (8 entries per thread;
   // pool <= kMaxPool = 8 * 512, so one round), the workgroup lists' bounds and the query are all
@@ -2836,7 +2850,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
   if (lane == 0) bpart[wave] = b;
-  __syncthreads();
+  __syncthreads(); MERGE_STAMP(1);
 
   // wave 0: t0 = kc-th largest workgroup maximum, and the workgroup lists' own bounds
   if (wave == 0) {
@@ -2866,7 +2880,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
       red[9] = t0;
     }
   }
-  __syncthreads();
+  __syncthreads(); MERGE_STAMP(2);
   const float t0 = red[9];
 
   // filter the pool held in registers
@@ -2887,7 +2901,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
   if (lane == 0) red[wave] = dmax;
-  __syncthreads();
+  __syncthreads(); MERGE_STAMP(3);
   const int n_sel = ctr[0];
   const bool overflow = n_sel > kSelCap;
   const int n_keep = overflow ? kSelCap : n_sel;
@@ -2954,6 +2968,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (tid == 0) out_flags[qg] = 0;
   return;  // probe: up to the sorted selection
 #endif
+  MERGE_STAMP(4);
   float bound = red[8];
 #pragma unroll
   for (int w = 0; w < kDenseMergeThreads / 64; ++w) bound = fmaxf(bound, red[w]);
@@ -2983,6 +2998,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     }
   }
   __syncthreads();
+  MERGE_STAMP(5);
   if (kc <= 64) {
     if (wave == 0) {
       double key = lane < kc ? rkey[lane] : kNegInfD;
@@ -2996,6 +3012,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     armi::lds_sort_rank_desc(rkey, rord, kc);
   }
 
+  MERGE_STAMP(6);
   if (wave != 0) return;
   // valid entries form a prefix of the sorted list
   int n_valid = 0;
@@ -3039,6 +3056,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     thr_out[qg] = certified ? __builtin_inff() : thr;
     col_cnt[qg] = 0;
   }
+  MERGE_STAMP(7);
 }
 
 constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16;
@@ -3889,6 +3907,10 @@ int armi_dense_exact_topk(const armi_index* idx, const uint16_t* queries, int n_
 #if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_STAMPS)
 int armi_probe_i8_stamps(uint64_t* out) {
   ARMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_i8_stamps), sizeof(g_i8_stamps)));
+  return ARMI_OK;
+}
+int armi_probe_merge_stamps(uint64_t* out) {
+  ARMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_merge_stamps), sizeof(g_merge_stamps)));
   return ARMI_OK;
 }
 #endif

@@ -34,6 +34,11 @@ def main() -> None:
     fn.argtypes = [ctypes.c_void_p]
     fn.restype = ctypes.c_int
     buf = np.zeros(256 * 8 * 4, dtype=np.uint64)
+    mfn = lib.armi_probe_merge_stamps
+    mfn.argtypes = [ctypes.c_void_p]
+    mfn.restype = ctypes.c_int
+    mbuf = np.zeros(64 * 8, dtype=np.uint64)
+    mspans = []
     spans = []
     for r in range(a.reps):
         idx.topk(qs, 5, workspace=ws)
@@ -42,6 +47,7 @@ def main() -> None:
         st = buf.reshape(256, 8, 4).astype(np.int64)
         live = st[:, :, 0] > 0
         t0 = st[:, :, 0][live].min()
+        t0_abs = st[:, :, 3][live].max()  # the scan's last workgroup-merge end (absolute ticks)
         rel = (st - t0) / 100.0  # us
         e = rel[..., 0][live]
         img = (rel[..., 1] - rel[..., 0])[live]
@@ -59,9 +65,26 @@ def main() -> None:
                           loop_end_max=float(loop_end.max()), merge_mean=float(merge.mean()),
                           merge_max=float(merge.max()), total=float(end.max())))
         buf[:] = 0
+        assert mfn(mbuf.ctypes.data) == 0
+        ms = mbuf.reshape(64, 8).astype(np.int64)
+        ok = (ms > 0).all(axis=1)
+        if ok.any():
+            m0 = ms[ok][:, 0].min()
+            mrel = (ms[ok] - m0) / 100.0
+            # per phase: mean duration over the workgroups; start skew; end of the last workgroup
+            mspans.append({"start_skew": float(mrel[:, 0].max()),
+                           **{f"phase{i}": float(np.mean(mrel[:, i] - mrel[:, i - 1]))
+                              for i in range(1, 8)},
+                           "total": float(mrel[:, 7].max()),
+                           "scan_end_to_merge_start": float((ms[ok][:, 0].min() - t0_abs) / 100.0)})
+        mbuf[:] = 0
     keys = spans[0].keys()
     med = {k: float(np.median([s[k] for s in spans[2:]])) for k in keys}
-    print(json.dumps({"chunks": a.chunks, "median_us": med}))
+    out = {"chunks": a.chunks, "median_us": med}
+    if mspans:
+        out["merge_median_us"] = {k: float(np.median([s[k] for s in mspans[2:]]))
+                                  for k in mspans[0].keys()}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
