@@ -649,9 +649,22 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       const int ycur = ypref;
       const bool pend = dyn && !((gone >> ycur) & 1u);
       int vpend = 0;
-      if (pend && lane == 0) vpend = atomicAdd(heads + 32 * ycur, 1);
+      if (pend) {
+        // one lane's returning atomic in asm: the compiler's own form (atomic optimizer) waits
+        // vmcnt(0) right after it, draining the prefetched groups; this one is waited for by
+        // hand at group GROUPS - DEPTH (16 loads issued after it)
+        const uint64_t addr = reinterpret_cast<uint64_t>(heads + 32 * ycur);
+        uint64_t saved;
+        asm volatile(
+            "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\t"
+            "global_atomic_add %0, %2, %3, off sc0\n\ts_mov_b64 exec, %1"
+            : "=&v"(vpend), "=&s"(saved)
+            : "v"(addr), "v"(1)
+            : "memory");
+      }
       const u32x4* nxt = cur;
       bool has_next = false;
+      float4 sv[4], ev[4];  // a32 / e32 of the lane's 16 rows (loaded mid-tile)
       const int32_t tord = tile_ord[t];  // ordinal of the tile's image row 0 (wave-uniform)
       int qoff = h * kQB + r;
       asm volatile("" : "+v"(qoff));
@@ -663,6 +676,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         if (g == GROUPS - DEPTH) {  // the next tile, whose loads start now
           if (dyn) {
             if (pend) {
+              asm volatile("s_waitcnt vmcnt(16)" : "+v"(vpend)::"memory");
               const int v = __builtin_amdgcn_readfirstlane(vpend);
               const int64_t tt = decode(ycur, v);
               if (tt >= 0) {
@@ -679,6 +693,15 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
           }
           has_next = tn >= 0;
           nxt = row_ptr(has_next ? tn : t);
+          // the epilogue's row scales, issued before the next tile's loads: waiting for them
+          // then leaves those in flight (issued after the prefetch, their wait was a vmcnt(0)
+          // that drained it at every tile)
+          const int64_t r0s = t * TILE_ROWS;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            sv[q] = *reinterpret_cast<const float4*>(a32 + r0s + 8 * q + 4 * h);
+            ev[q] = *reinterpret_cast<const float4*>(e32 + r0s + 8 * q + 4 * h);
+          }
         }
         u32x4 a[4];
 #pragma unroll
@@ -687,7 +710,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(cur + 32 * (8 * (g + DEPTH) + i));
-        } else if (has_next) {
+        } else {  // (no next tile: the current one again, so every path issues the same loads)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
@@ -738,9 +761,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       float sc[16], ec[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(a32 + row0 + 8 * q + 4 * h);
+        const float4 v = sv[q], w = ev[q];
         sc[4 * q + 0] = v.x; sc[4 * q + 1] = v.y; sc[4 * q + 2] = v.z; sc[4 * q + 3] = v.w;
-        const float4 w = *reinterpret_cast<const float4*>(e32 + row0 + 8 * q + 4 * h);
         ec[4 * q + 0] = w.x; ec[4 * q + 1] = w.y; ec[4 * q + 2] = w.z; ec[4 * q + 3] = w.w;
       }
       // invalid and filtered rows: NaN scale (never a lane-list entry, ignored by the bound)
