@@ -180,11 +180,19 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
       asm volatile("" : "+v"(qoff));
       const u32x4* qv = qimg + qoff;
       f32x16 acc0 = {}, acc1 = {};
+      float4 iv4[4];  // inverse norms of the lane's 16 rows, loaded before the next tile's loads
 #pragma unroll
       for (int g = 0; g < GROUPS; ++g) {
         u32x4 a[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i] = buf[g % kDepth][i];
+        if (g == GROUPS - kDepth) {
+          // (an epilogue load issued after the prefetch would be waited for with a vmcnt(0)
+          // that drains the prefetch at every tile)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            iv4[q] = *reinterpret_cast<const float4*>(inv_norm32 + t * TILE_ROWS + 8 * q + 4 * h);
+        }
         if (g + kDepth < GROUPS) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) buf[g % kDepth][i] = stream_load(cur + 8 * (g + kDepth) + i);
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
       float inv[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(inv_norm32 + row0 + 8 * q + 4 * h);
+        const float4 v = iv4[q];
         inv[4 * q + 0] = v.x; inv[4 * q + 1] = v.y; inv[4 * q + 2] = v.z; inv[4 * q + 3] = v.w;
       }
       // Invalid rows carry a NaN inverse norm, filtered rows get one here: a NaN score never

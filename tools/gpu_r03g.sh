@@ -21,6 +21,8 @@ for rep in 1 2; do
     done
   done
 done
+ARMI_DENSE_FILTER=fp16 timeout -k 10 200 python bench.py $B > gpurun_out/${TAG}_fp16pass.log 2>&1 || exit $?
+echo "fp16 pass: $(j gpurun_out/${TAG}_fp16pass.log 'round(d["value"]), round(d["ms_per_step"],4), round(d["roofline"]["avg_launch_ms"],4), d["roofline"]["kernel"]')"
 ARMI_I8_SCHED=static bash tools/probes/i8_stamps.sh ${TAG}stps || exit $?
 ARMI_I8_SCHED=dynamic bash tools/probes/i8_stamps.sh ${TAG}stpd || exit $?
 
