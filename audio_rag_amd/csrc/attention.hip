@@ -696,12 +696,11 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_lds_bytes(kMaxL));
   ARMI_HIP(raised);
   const float scale_log2 = scale * 1.4426950408889634f;
-  // persistent double-buffered form for L <= 256 when there are pairs enough to keep every CU
-  // busy (ARMI_ATTENTION=oneshot forces the one-shot kernel: A/B)
-  static const bool oneshot = [] {
-    const char* e = getenv("ARMI_ATTENTION");
-    return e && e[0] == 'o';
-  }();
+  // one-shot kernel by default; ARMI_ATTENTION=persist selects the persistent double-buffered
+  // form (L <= 256, pairs enough to keep every CU busy): measured 0.9 ms per 1,280-pair forward
+  // slower on configs[2] (67.5 vs 68.4 ms, profiles/r03f_bench_rerank.json / _rerank_oneshot)
+  const char* form = getenv("ARMI_ATTENTION");  // read per call (tests switch forms in-process)
+  const bool oneshot = !(form && form[0] == 'p');
   static int cus = 0;
   if (!cus) {
     int dev = 0;

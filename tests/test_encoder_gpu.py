@@ -195,12 +195,13 @@ def test_attention_f16_matches_fp32_reference(gpu, L):
 
 
 @pytest.mark.parametrize("L", [7, 100, 256])
-def test_attention_f16_persistent_matches_fp32_reference(gpu, L):
+def test_attention_f16_persistent_matches_fp32_reference(gpu, L, monkeypatch):
     """The persistent double-buffered attention (>= 2 (sequence, head) pairs per CU, L <= 256:
     next pair's K / V / Q loads in flight during the current pair's compute) on ragged masks,
     against fp32 eager attention; every sequence is checked."""
     g = torch.Generator().manual_seed(500 + L)
     n, H, dh = 45, 12, 64  # 540 pairs > 2 x 256 CUs
+    monkeypatch.setenv("ARMI_ATTENTION", "persist")  # (the one-shot kernel is the default)
     qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
     mask = torch.ones(n, L, dtype=torch.int32)
     for i in range(0, n, 3):

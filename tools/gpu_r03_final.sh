@@ -23,8 +23,8 @@ echo "hybrid: $(j gpurun_out/${TAG}_bench_hybrid.log 'round(d["value"]), round(d
 timeout -k 10 700 python bench.py --workload hybrid_rerank --steps 5 --warmup 2 --latency-iters 3 > gpurun_out/${TAG}_bench_rerank.log 2>&1 || exit $?
 echo "rerank: $(j gpurun_out/${TAG}_bench_rerank.log 'round(d["value"],1), round(d["ms_per_step"],2), round(d["roofline"]["avg_forward_ms"],2), round(d["roofline"]["frac"],3), round(d["roofline_scan"]["avg_launch_ms"],4), round(d["cpu_baseline"]["value"],3)')"
 RR="--workload hybrid_rerank --steps 4 --warmup 2 --latency-iters 1 --no-cpu-baseline"
-ARMI_ATTENTION=oneshot timeout -k 10 400 python bench.py $RR > gpurun_out/${TAG}_rerank_oneshot.log 2>&1 || exit $?
-echo "rerank oneshot attention: $(j gpurun_out/${TAG}_rerank_oneshot.log 'round(d["value"],1), round(d["roofline"]["avg_forward_ms"],2)')"
+ARMI_ATTENTION=persist timeout -k 10 400 python bench.py $RR > gpurun_out/${TAG}_rerank_persist.log 2>&1 || exit $?
+echo "rerank persistent attention: $(j gpurun_out/${TAG}_rerank_persist.log 'round(d["value"],1), round(d["roofline"]["avg_forward_ms"],2)')"
 ARMI_RERANK_GEMM=torch timeout -k 10 400 python bench.py $RR > gpurun_out/${TAG}_rerank_torchgemm.log 2>&1 || exit $?
 echo "rerank hipBLASLt + GELU pass: $(j gpurun_out/${TAG}_rerank_torchgemm.log 'round(d["value"],1), round(d["roofline"]["avg_forward_ms"],2)')"
 exit 0
