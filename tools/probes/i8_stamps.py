@@ -58,7 +58,16 @@ def main() -> None:
         le = rel[..., 2]
         xcd_end = [float(np.max(le[x::8][live[x::8]])) if live[x::8].any() else 0.0
                    for x in range(8)]
-        spans.append(dict(xcd_loop_end_max_spread=float(max(xcd_end) - min(xcd_end)),
+        # per workgroup (all 8 waves live): the spread of its waves' loop ends and the pure merge
+        # (its end minus its last wave's loop end)
+        wl = live.all(axis=1)
+        wg_spread = (st[wl][:, :, 2].max(axis=1) - st[wl][:, :, 2].min(axis=1)) / 100.0
+        wg_merge = (st[wl][:, :, 3].max(axis=1) - st[wl][:, :, 2].max(axis=1)) / 100.0
+        spans.append(dict(wg_wave_end_spread_mean=float(wg_spread.mean()),
+                          wg_wave_end_spread_max=float(wg_spread.max()),
+                          wg_pure_merge_mean=float(wg_merge.mean()),
+                          wg_pure_merge_max=float(wg_merge.max()),
+                          xcd_loop_end_max_spread=float(max(xcd_end) - min(xcd_end)),
                           entry_spread=float(e.max()), image_mean=float(img.mean()),
                           image_max=float(img.max()), loop_mean=float(loop.mean()),
                           loop_max=float(loop.max()), loop_end_min=float(loop_end.min()),
