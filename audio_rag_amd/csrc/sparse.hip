@@ -480,7 +480,8 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
 
 #ifdef ARMI_SPARSE_PROFILE
 // Profiling build only (ARMI_BUILD_FLAGS=-DARMI_SPARSE_PROFILE): per-wave phase timers and the
-// ARMI_SPARSE_DBG knobs (1 = skip compute, 2 = stage nothing, 4 = no step barrier, 8 = report).
+// ARMI_SPARSE_DBG knobs (1 = skip compute, 2 = stage nothing, 4 = no step barrier, 8 = report,
+// 16 = clear every staged row each step).
 __device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 8];
 #define ARMI_PROF_T(x) x = wall_clock64()
 #define ARMI_PROF_ADD(i, a, b) tp[i] += (b) - (a)
@@ -645,15 +646,22 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   // The in-tile postings are a prefix of the 128 loaded (rows ascend to the list's sentinel):
   // with ne / no the even / odd positions' in-tile prefixes (lane 63 holds positions 0 and 1),
   // the prefix length is min(2 ne, 2 no + 1).
+  // rows of this wave's held terms per staging buffer that hold postings from their last use
+  // (round 3: only those are cleared; a row whose term had no posting in its tile is still
+  // all-zero, and with Zipf query terms about half the (tile, term) pairs are empty, so this
+  // halves the clearing stores, the scan's largest LDS-store item). LDS starts undefined: all dirty.
+  uint32_t dirty[2] = {(1u << kHold) - 1u, (1u << kHold) - 1u};
   auto finish = [&](int tile, int seg, int par) {
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
     const int32_t thi = tile_hi(tile);
     const int base = seg < kRegSegs ? seg * kHold : 0;
     uint32_t* buf = sbuf + (size_t)par * kU * kTile;
+    const uint32_t dm = (dbg & 16) ? (1u << kHold) - 1u : dirty[par];
+    dirty[par] = amask;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       uint32_t* row = buf + (k * kWaves + wave) * kTile;
-      reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
+      if ((dm >> k) & 1u) reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
       if ((amask >> k) & 1u) {
         const uint64_t be = __ballot(sp[k].x < thi), bo = __ballot(sp[k].z < thi);
         const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
@@ -1321,7 +1329,11 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
 #ifdef ARMI_SPARSE_PROFILE
   static const int dbg = getenv("ARMI_SPARSE_DBG") ? atoi(getenv("ARMI_SPARSE_DBG")) : 0;
 #else
-  constexpr int dbg = 0;
+  // ARMI_SPARSE_CLEAR=all: clear every staged row each step (the round-2 form; A/B)
+  static const int dbg = [] {
+    const char* e = getenv("ARMI_SPARSE_CLEAR");
+    return (e && e[0] == 'a') ? 16 : 0;
+  }();
 #endif
   const size_t lds_collect = (size_t)kCollectCap * 8;
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
