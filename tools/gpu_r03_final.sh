@@ -51,6 +51,6 @@ timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$P/write"
 # keep the summaries only (gpurun copies back at most 64 MiB)
 python3 "$R/tools/rocpd_stats.py" "$P/dense/run_results.db" > "$R/gpurun_out/${TAG}_dense_kernel_stats.csv" || exit $?
 python3 "$R/tools/rocpd_stats.py" "$P/rerank/run_results.db" > "$R/gpurun_out/${TAG}_rerank_kernel_stats.csv" || exit $?
-python3 "$R/tools/pmc_traffic.py" "$P/fetch/run_counter_collection.csv" "$P/write/run_counter_collection.csv" dense_scan_i8_kernelILi1024ELb0ELb0 1032131072 "bench.py default: 1M x 1024 rows, int8 filter image (tile-blocked, scattered row order) + a32/e32, 64 fp16 queries per launch" > "$R/gpurun_out/${TAG}_dense_scan_i8_traffic.json" || exit $?
+python3 "$R/tools/pmc_traffic.py" "$P/fetch/run_counter_collection.csv" "$P/write/run_counter_collection.csv" "dense_scan_i8_kernel<1024, false, false>" 1032131072 "bench.py default: 1M x 1024 rows, int8 filter image (tile-blocked, scattered row order) + a32/e32, 64 fp16 queries per launch" > "$R/gpurun_out/${TAG}_dense_scan_i8_traffic.json" || exit $?
 rm -rf "$P"
 echo "profiles done"
