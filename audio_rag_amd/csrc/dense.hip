@@ -417,6 +417,16 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   const int r = lane & 31;
   const int h = lane >> 5;
   I8_STAMP(0);
+  // first pass, static split: the workgroup's waves take its tiles from an LDS counter (each
+  // wave's first tile is t_begin + wave; the counter hands out the rest in order). Round-3 stamps
+  // (profiles/r03i_i8_stamps_*): with a fixed tile-per-wave split the 8 waves of a workgroup
+  // ended their loops ~32 us apart on average at 1M rows (wave speed differs by ~15 % inside a
+  // CU), and the workgroup merge waits for the last of them. An LDS atomic returns in ~100 cycles
+  // through lgkmcnt, so unlike a device-scope dequeue it never drains the vmcnt prefetch queue.
+  int32_t* const wtile = wcnt;  // wcnt[0]: next tile offset of the workgroup (non-COLLECT)
+  if constexpr (!COLLECT) {
+    if (threadIdx.x == 0) wtile[0] = kWaves;  // published by the image phase's barriers
+  }
   if constexpr (COLLECT) {
     // this block's slice [q0, q0 + 64) of the ordered list of uncertified queries
     for (int e = threadIdx.x; e < kQB; e += kThreads) {
@@ -653,6 +663,15 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   if (t >= 0) {
     int64_t tn = -1;
     for (; t >= 0; t = tn) {
+      // static split, first pass: the next tile of the workgroup's range (LDS counter)
+      int wnext = 0;
+      if constexpr (!COLLECT) {
+        if (!dyn) {
+          int got = 0;
+          if (lane == 0) got = atomicAdd(wtile, 1);  // one lane: one tile per wave
+          wnext = __builtin_amdgcn_readfirstlane(got);
+        }
+      }
       // dynamic: this tile's dequeue, in flight during the first GROUPS - DEPTH groups
       const int ycur = ypref;
       const bool pend = dyn && !((gone >> ycur) & 1u);
@@ -697,7 +716,11 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
               tn = steal();
             }
           } else {
-            tn = t + kWaves < t_end ? t + kWaves : -1;
+            if constexpr (COLLECT) {
+              tn = t + kWaves < t_end ? t + kWaves : -1;
+            } else {
+              tn = t_begin + wnext < t_end ? t_begin + wnext : -1;
+            }
           }
           has_next = tn >= 0;
           nxt = row_ptr(has_next ? tn : t);
