@@ -318,6 +318,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 
 // 4 int8 components (one dword) -> 4 fp16 fragments components (two dwords), exactly: the
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     int guard, const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr,
     int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap,
-    int32_t* __restrict__ heads) {
+    int32_t* __restrict__ heads, int wg_counter) {
   static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
   constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
@@ -664,12 +665,19 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     int64_t tn = -1;
     for (; t >= 0; t = tn) {
       // static split, first pass: the next tile of the workgroup's range (LDS counter)
-      int wnext = 0;
+      // (one lane's ds_add_rtn in asm, waited for at group GROUPS - DEPTH: the compiler's form
+      // waits lgkmcnt(0) at once, i.e. also for the tile's scalar loads)
+      int wgot = 0;
       if constexpr (!COLLECT) {
-        if (!dyn) {
-          int got = 0;
-          if (lane == 0) got = atomicAdd(wtile, 1);  // one lane: one tile per wave
-          wnext = __builtin_amdgcn_readfirstlane(got);
+        if (!dyn && wg_counter) {
+          const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)wtile;
+          uint64_t saved;
+          asm volatile(
+              "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\t"
+              "ds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
+              : "=&v"(wgot), "=&s"(saved)
+              : "v"(a), "v"(1)
+              : "memory");
         }
       }
       // dynamic: this tile's dequeue, in flight during the first GROUPS - DEPTH groups
@@ -716,9 +724,11 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
               tn = steal();
             }
           } else {
-            if constexpr (COLLECT) {
+            if (COLLECT || !wg_counter) {
               tn = t + kWaves < t_end ? t + kWaves : -1;
             } else {
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wgot)::"memory");
+              const int wnext = __builtin_amdgcn_readfirstlane(wgot);
               tn = t_begin + wnext < t_end ? t_begin + wnext : -1;
             }
           }
@@ -1217,7 +1227,6 @@ constexpr size_t gemm_glds_lds_bytes() {
   return stages > lists ? stages : lists;
 }
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // ABL: the diagnostic instantiation that honours `ablate`; the production one (ABL = false)
 // compiles the switches out, so no branch sits between the MFMAs.
@@ -3426,6 +3435,16 @@ bool i8_dynamic_schedule() {
   return dyn;
 }
 
+// Intra-workgroup tile counter of the int8 first pass (default on); ARMI_I8_WGSPLIT=fixed keeps
+// the fixed tile-per-wave split (A/B).
+bool i8_wg_counter() {
+  static const bool on = [] {
+    const char* e = getenv("ARMI_I8_WGSPLIT");
+    return !(e && e[0] == 'f');
+  }();
+  return on;
+}
+
 bool use_gemm_scan(int nq) {
   static const int force = [] {
     const char* e = getenv("ARMI_DENSE_SCAN");
@@ -3798,7 +3817,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads, i8_wg_counter() ? 1 : 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -3834,7 +3853,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
-        w.col_cnt, w.col_list, kCollectCap, nullptr);
+        w.col_cnt, w.col_list, kCollectCap, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
