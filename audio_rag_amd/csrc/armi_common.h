@@ -72,11 +72,13 @@ __device__ __forceinline__ int32_t fp16_to_fixed24(uint32_t h) {
 __device__ __forceinline__ bool fp16_in_domain(uint32_t h) { return ((h >> 10) & 31) <= 15; }
 
 // Total order used by every dense ranking: key descending, then ordinal ascending.
+// (bitwise, not short-circuit: the || / && form compiled to exec-mask branches inside the wave
+// sorts, one waited shuffle at a time; round-3 ISA of dense_scan_i8_kernel's workgroup merge)
 __device__ __forceinline__ bool rank_better(double ka, int64_t ia, double kb, int64_t ib) {
-  return ka > kb || (ka == kb && ia < ib);
+  return (ka > kb) | ((ka == kb) & (ia < ib));
 }
 __device__ __forceinline__ bool approx_better(float ka, int32_t ia, float kb, int32_t ib) {
-  return ka > kb || (ka == kb && ia < ib);
+  return (ka > kb) | ((ka == kb) & (ia < ib));
 }
 
 // In-LDS bitonic sort of n (power of two) entries into descending rank order, executed by the
@@ -136,9 +138,10 @@ __device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) 
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;
       const bool other_better = approx_better(ok, orow, key, row);
-      // lower lane of a descending pair keeps the better entry
-      const bool take_other = (lower == desc) ? other_better : !other_better;
-      if (take_other) { key = ok; row = orow; }
+      // lower lane of a descending pair keeps the better entry (selects, no branch)
+      const bool take_other = other_better ^ (lower != desc);
+      key = take_other ? ok : key;
+      row = take_other ? orow : row;
     }
   }
 }
@@ -156,8 +159,9 @@ __device__ __forceinline__ void wave_sort_rank_desc(double& key, int64_t& ord) {
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;
       const bool other_better = rank_better(ok, oo, key, ord);
-      const bool take_other = (lower == desc) ? other_better : !other_better;
-      if (take_other) { key = ok; ord = oo; }
+      const bool take_other = other_better ^ (lower != desc);
+      key = take_other ? ok : key;
+      ord = take_other ? oo : ord;
     }
   }
 }
@@ -183,8 +187,9 @@ __device__ __forceinline__ void wave_sort_approx_desc_n(float (&key)[N], int32_t
 #pragma unroll
       for (int n = 0; n < N; ++n) {
         const bool other_better = approx_better(ok[n], orow[n], key[n], row[n]);
-        const bool take_other = (lower == desc) ? other_better : !other_better;
-        if (take_other) { key[n] = ok[n]; row[n] = orow[n]; }
+        const bool take_other = other_better ^ (lower != desc);
+        key[n] = take_other ? ok[n] : key[n];
+        row[n] = take_other ? orow[n] : row[n];
       }
     }
   }

@@ -271,19 +271,19 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 
   // 2. Workgroup merge (the query image is dead: overlay it).
   __syncthreads();
-  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][64]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * 64 * 4);        // [kQB][64]
-  float* ldisc = reinterpret_cast<float*>(smem + kQB * 64 * 8);           // [kQB][16]
+  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][65]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * 65 * 4);        // [kQB][65]
+  float* ldisc = reinterpret_cast<float*>(smem + kQB * 65 * 8);           // [kQB][17]
   const int slot = wave * 2 + h;
 #pragma unroll
   for (int j = 0; j < kLaneList; ++j) {
-    lkey[r * 64 + slot * kLaneList + j] = s0[j];
-    lrow[r * 64 + slot * kLaneList + j] = i0[j];
-    lkey[(32 + r) * 64 + slot * kLaneList + j] = s1[j];
-    lrow[(32 + r) * 64 + slot * kLaneList + j] = i1[j];
+    lkey[r * 65 + slot * kLaneList + j] = s0[j];
+    lrow[r * 65 + slot * kLaneList + j] = i0[j];
+    lkey[(32 + r) * 65 + slot * kLaneList + j] = s1[j];
+    lrow[(32 + r) * 65 + slot * kLaneList + j] = i1[j];
   }
-  ldisc[r * 16 + slot] = d0;
-  ldisc[(32 + r) * 16 + slot] = d1;
+  ldisc[r * 17 + slot] = d0;
+  ldisc[(32 + r) * 17 + slot] = d1;
   __syncthreads();
   // each wave merges its kQB / kWaves queries together (interleaved shuffle chains)
   constexpr int QW = kQB / kWaves;
@@ -292,9 +292,9 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
-    key[qq] = lkey[q * 64 + lane];
-    row[qq] = lrow[q * 64 + lane];
-    b[qq] = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
+    key[qq] = lkey[q * 65 + lane];
+    row[qq] = lrow[q * 65 + lane];
+    b[qq] = (lane < 16) ? ldisc[q * 17 + lane] : kNegInf;
   }
   armi::wave_sort_approx_desc_n<QW>(key, row);
 #pragma unroll
@@ -881,21 +881,24 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
   I8_STAMP(2);
   if constexpr (COLLECT) return;
-  // 2. Workgroup merge (as dense_scan_kernel; the query image is dead: overlay it).
+  // 2. Workgroup merge (as dense_scan_kernel; the query image is dead: overlay it). Rows of 65
+  // dwords: lanes r = 0..31 write query r's row at the same column, so a 64-dword stride put all
+  // 32 stores of an instruction in one bank
+  constexpr int kLS = 65;
   __syncthreads();
-  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][64]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * 64 * 4);        // [kQB][64]
-  float* ldisc = reinterpret_cast<float*>(smem + kQB * 64 * 8);           // [kQB][16]
+  float* lkey = reinterpret_cast<float*>(smem);                           // [kQB][kLS]
+  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kQB * kLS * 4);       // [kQB][kLS]
+  float* ldisc = reinterpret_cast<float*>(smem + kQB * kLS * 8);          // [kQB][17]
   const int slot = wave * 2 + h;
 #pragma unroll
   for (int j = 0; j < kLaneList; ++j) {
-    lkey[r * 64 + slot * kLaneList + j] = s0[j];
-    lrow[r * 64 + slot * kLaneList + j] = i0[j];
-    lkey[(32 + r) * 64 + slot * kLaneList + j] = s1[j];
-    lrow[(32 + r) * 64 + slot * kLaneList + j] = i1[j];
+    lkey[r * kLS + slot * kLaneList + j] = s0[j];
+    lrow[r * kLS + slot * kLaneList + j] = i0[j];
+    lkey[(32 + r) * kLS + slot * kLaneList + j] = s1[j];
+    lrow[(32 + r) * kLS + slot * kLaneList + j] = i1[j];
   }
-  ldisc[r * 16 + slot] = d0;
-  ldisc[(32 + r) * 16 + slot] = d1;
+  ldisc[r * 17 + slot] = d0;
+  ldisc[(32 + r) * 17 + slot] = d1;
   __syncthreads();
   constexpr int QW = kQB / kWaves;
   float key[QW], b[QW];
@@ -903,9 +906,9 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
-    key[qq] = lkey[q * 64 + lane];
-    row[qq] = lrow[q * 64 + lane];
-    b[qq] = (lane < 16) ? ldisc[q * 16 + lane] : kNegInf;
+    key[qq] = lkey[q * kLS + lane];
+    row[qq] = lrow[q * kLS + lane];
+    b[qq] = (lane < 16) ? ldisc[q * 17 + lane] : kNegInf;
   }
   armi::wave_sort_approx_desc_n<QW>(key, row);
 #pragma unroll
