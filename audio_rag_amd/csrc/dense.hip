@@ -389,7 +389,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     int guard, const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr,
     int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap,
-    int32_t* __restrict__ heads, int wg_counter) {
+    int32_t* __restrict__ heads, int wg_counter, const u32x4* __restrict__ qimg_g,
+    const float* __restrict__ qnorm_g) {
   static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
   constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
@@ -534,7 +535,32 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   //    t_q and e_q (rounded up, plus 2^-20 |q| for the rounding of t_q * q8_i). Then the
   //    fragment image: fp16 (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) or
   //    QI8 int8 (components 128(s>>2) + 64h + 16(s&3) .. +15), the corpus chunks' order.
-  if constexpr (!QI8) {
+  bool img_dma = false;
+  if constexpr (!QI8 && !COLLECT) img_dma = qimg_g != nullptr;
+  if (img_dma) {
+    // the fragment image and |q| prepared by query_image_kernel: LDS-DMA pieces of 1 KB (no
+    // registers, no arithmetic), issued before the first tile's prefetch and waited for by count
+    // (vmcnt(16): the 16 prefetch loads stay in flight; a __syncthreads would drain them)
+    constexpr int NP = KSTEPS * 2 * kQB * 16 / 1024;
+    static_assert(NP % kWaves == 0, "image pieces per wave");
+    const unsigned char* src =
+        reinterpret_cast<const unsigned char*>(qimg_g + (size_t)qb * KSTEPS * 2 * kQB);
+#pragma unroll
+    for (int i = 0; i < NP / kWaves; ++i) {
+      const int p = wave + kWaves * i;
+      __builtin_amdgcn_global_load_lds(src + p * 1024 + lane * 16,
+                                       (lds_ptr_t)(reinterpret_cast<unsigned char*>(qimg) + p * 1024),
+                                       16, 0, 0);
+    }
+    if (wave == 0)
+      __builtin_amdgcn_global_load_lds(qnorm_g + (size_t)qb * kQB + lane, (lds_ptr_t)qnorm, 4, 0, 0);
+    prefetch_first();
+    if (t >= 0) {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else if constexpr (!QI8) {
     // fp16 image: thread (q = tid % 64, sh0 = tid / 64) copies entries sh = sh0 + 8 i of query q,
     // all 2*KSTEPS/8 loads in flight at once (a dependent load per entry would cost one L2 round
     // trip each), and sums its components' squares for the query norm on the way.
@@ -636,7 +662,12 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     qimg[e] = v;
   }
   }
-  __syncthreads();
+  if (img_dma) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
   I8_STAMP(1);
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
   float th0 = __builtin_inff(), th1 = __builtin_inff();
@@ -930,6 +961,52 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if (lane == 0) cand_bound[base] = b[qq];
   }
   I8_STAMP(3);
+}
+
+// The 64-query fragment image of dense_scan_i8_kernel (fp16 queries) and |q| rounded up, built
+// once per call into the workspace (one workgroup per 64-query block, the same thread partition
+// and summation order as the scan's in-kernel build, so the same bits): every scan workgroup then
+// copies it by LDS-DMA instead of each building its own from the query rows (round 3: ~10 us of
+// every launch at the kernel start).
+template <int DIM>
+__global__ __launch_bounds__(kThreads) void query_image_kernel(const uint16_t* __restrict__ queries,
+                                                               int nq_total, u32x4* __restrict__ img,
+                                                               float* __restrict__ qnorm_out) {
+  constexpr int KSTEPS = DIM / 16;
+  constexpr int PER = KSTEPS * 2 / (kThreads / kQB);
+  __shared__ float part[kThreads];
+  const int qb = blockIdx.x;
+  const int q0 = qb * kQB;
+  const int nq = min(kQB, nq_total - q0);
+  const int q = threadIdx.x & (kQB - 1);
+  const int sh0 = threadIdx.x >> 6;
+  u32x4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int sh = sh0 + (kThreads / kQB) * i;
+    const int s = sh >> 1, hh = sh & 1;
+    const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
+    v[i] = q < nq ? *reinterpret_cast<const u32x4*>(queries + (size_t)(q0 + q) * DIM + off)
+                  : u32x4{0u, 0u, 0u, 0u};
+  }
+  u32x4* dst = img + (size_t)qb * KSTEPS * 2 * kQB;
+  float ss = 0.0f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int sh = sh0 + (kThreads / kQB) * i;
+    dst[sh * kQB + q] = v[i];
+    const half8 hv = __builtin_bit_cast(half8, v[i]);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
+  }
+  part[sh0 * kQB + q] = ss;
+  __syncthreads();
+  if (threadIdx.x < kQB) {
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kThreads / kQB; ++j) t += part[j * kQB + threadIdx.x];
+    qnorm_out[(size_t)q0 + threadIdx.x] = sqrtf(t) * (1.0f + 1.0f / 4096.0f);
+  }
 }
 
 template <int DIM>
@@ -3626,6 +3703,8 @@ struct Workspace {
   int32_t* col_list;   // [nq][kCollectCap] image positions
   uint64_t* mask_img;  // row filter in int8 image order
   int32_t* heads;      // [8][32] dynamic tile schedule of the int8 scan (one counter per line)
+  u32x4* qimg;         // [n_qb][2 dim / 16][64] fragment image of each 64-query block
+  float* qnorm_img;    // [n_qb][64] |q| rounded up (the int8 key's bound term)
   size_t bytes;
 };
 
@@ -3642,6 +3721,9 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
     w.heads = cv.take<int32_t>(8 * 32);
+    const size_t n_qb = (size_t)(nq + kQB - 1) / kQB;
+    w.qimg = cv.take<u32x4>(n_qb * (size_t)(idx->dim / 16) * 2 * kQB);
+    w.qnorm_img = cv.take<float>(n_qb * kQB);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -3812,6 +3894,17 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kc = kc_i8(k);
     i8_first = true;
     const bool qi8 = use_q8(k);
+    // ARMI_I8_IMAGE=inkernel: every scan workgroup builds the query image itself (A/B)
+    static const bool img_pre = [] {
+      const char* e = getenv("ARMI_I8_IMAGE");
+      return !(e && e[0] == 'i');
+    }();
+    const bool pre = !qi8 && img_pre;
+    if (pre) {
+      query_image_kernel<DIM><<<dim3(sp.n_qb), dim3(kThreads), 0, stream>>>(queries, nq, w.qimg,
+                                                                          w.qnorm_img);
+      ARMI_LAUNCHED("query_image_kernel");
+    }
     auto kern = qi8 ? dense_scan_i8_kernel<DIM, true, false> : dense_scan_i8_kernel<DIM, false, false>;
     if (int rc = allow_lds(dense_scan_i8_kernel<DIM, true, false>, scan_i8_lds_bytes<DIM>())) return rc;
     if (int rc = allow_lds(dense_scan_i8_kernel<DIM, false, false>, scan_i8_lds_bytes<DIM>())) return rc;
@@ -3820,7 +3913,8 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads, i8_wg_counter() ? 1 : 0);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads, i8_wg_counter() ? 1 : 0,
+        pre ? w.qimg : nullptr, pre ? w.qnorm_img : nullptr);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -3856,7 +3950,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
-        w.col_cnt, w.col_list, kCollectCap, nullptr, 0);
+        w.col_cnt, w.col_list, kCollectCap, nullptr, 0, nullptr, nullptr);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
