@@ -65,7 +65,135 @@ __device__ __forceinline__ f32x16 score_block(const uint16_t* __restrict__ ks, i
   return acc;
 }
 
-__global__ __launch_bounds__(kThreads) void attention_f16_kernel(
+// maximumNumber: lowers to v_max3_f32 without the canonicalising v_max_f32 copies that fmaxf
+// gets on MFMA results (no NaN reaches these maxima)
+__device__ __forceinline__ float fmax2(float a, float b) {
+  return __builtin_elementwise_maximumnum(a, b);
+}
+
+// max over the two lanes r and r + 32 (the two key halves of query r): one permlane32 swap
+__device__ __forceinline__ float halves_max(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmax2(fmax2(x, __builtin_bit_cast(float, (uint32_t)sw[0])),
+               __builtin_bit_cast(float, (uint32_t)sw[1]));
+}
+
+__device__ __forceinline__ float halves_sum(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  // lanes < 32: sw[1] is the partner; lanes >= 32: sw[0]
+  return x + __builtin_bit_cast(float, (uint32_t)((threadIdx.x & 32) ? sw[0] : sw[1]));
+}
+
+// Online softmax of one wave's 32 queries over key blocks [0, kb_end) of the staged K / V^T
+// images (the kernels' comment). Lane kb of live_v holds block kb's live-key bits (bit j = key
+// 32 kb + j is unmasked; read with v_readlane, no LDS round trip per block); a block
+// with no live key is skipped, a full block needs no masking.
+// Per block the VALU work is kept to what the math needs: the block maximum on the raw scores
+// (8 v_max3 + one permlane32 swap), p = exp2(s * c - m * c) as one FMA + one v_exp, the row-sum
+// adds and 8 packs. The running maximum m is only raised when a score exceeds it by more than
+// 2^kRescaleLog2 in P (deferred rescale, cdna_hip_programming.md T13; the decision is taken
+// before this block's P is formed and after the previous block's P.V, so O, l and P always share
+// one m): P stays <= 2^8, well inside fp16, and the O / l rescale runs on the rare blocks that
+// raise m instead of every block. Returns O^T (unnormalised) and this lane half's row sum.
+constexpr float kRescaleLog2 = 8.f;
+
+__device__ __forceinline__ float addf(float a, float b) {
+  float d;  // (asm: keeps the row sums single adds; -O3 SLP-packs them into v_pk_add_f32, which
+            // costs more than two v_add_f32 beside MFMAs, MI355X_MICROARCH.md constants table)
+  asm("v_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
+// one key block of attend_keys: mask, deferred-rescale online softmax, P.V
+__device__ __forceinline__ void attend_block(f32x16 acc, uint32_t lv, int kb, int h, float c,
+                                             float thr, const uint16_t* __restrict__ v0,
+                                             const uint16_t* __restrict__ v1, float& m, float& mc,
+                                             float& l, f32x16& o0, f32x16& o1) {
+  if (lv == 0u) return;  // workgroup-uniform: every key of the block is padding
+  if (lv != ~0u) {
+    const uint32_t lh = lv >> (4 * h);  // this lane half's keys at bits (i & 3) + 8 (i >> 2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!(lh & (1u << ((i & 3) + 8 * (i >> 2))))) acc[i] = -INFINITY;
+  }
+  float m5[5];
+#pragma unroll
+  for (int g = 0; g < 5; ++g) m5[g] = fmax2(fmax2(acc[3 * g], acc[3 * g + 1]), acc[3 * g + 2]);
+  const float t0 = fmax2(fmax2(m5[0], m5[1]), m5[2]);
+  const float t1 = fmax2(fmax2(m5[3], m5[4]), acc[15]);
+  const float bm = halves_max(fmax2(t0, t1));
+  if (__builtin_amdgcn_ballot_w64(bm > m + thr)) {  // wave-uniform
+    const float mn = fmax2(m, bm);
+    const float alpha = __builtin_amdgcn_exp2f((m - mn) * c);  // 0 on the first live block
+    o0 *= alpha;
+    o1 *= alpha;
+    l *= alpha;
+    m = mn;
+    mc = mn * c;
+  }
+  float p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i], c, -mc));
+  float s4[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) s4[g] = addf(addf(p[4 * g], p[4 * g + 1]), addf(p[4 * g + 2], p[4 * g + 3]));
+  l = addf(l, addf(addf(s4[0], s4[1]), addf(s4[2], s4[3])));
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    // B fragment of k-step st: registers 8st..8st+7 = keys 16st + 8(j>>2) + 4h + (j&3)
+    u32x4 pb;
+    pb[0] = pack_h2(p[8 * st + 0], p[8 * st + 1]);
+    pb[1] = pack_h2(p[8 * st + 2], p[8 * st + 3]);
+    pb[2] = pack_h2(p[8 * st + 4], p[8 * st + 5]);
+    pb[3] = pack_h2(p[8 * st + 6], p[8 * st + 7]);
+    const int key0 = kb * 32 + 16 * st;
+    const u32x2 a0 = *reinterpret_cast<const u32x2*>(v0 + key0);
+    const u32x2 a1 = *reinterpret_cast<const u32x2*>(v0 + key0 + 8);
+    const u32x2 b0 = *reinterpret_cast<const u32x2*>(v1 + key0);
+    const u32x2 b1 = *reinterpret_cast<const u32x2*>(v1 + key0 + 8);
+    o0 = mfma16(u32x4{a0[0], a0[1], a1[0], a1[1]}, pb, o0);
+    o1 = mfma16(u32x4{b0[0], b0[1], b1[0], b1[1]}, pb, o1);
+  }
+}
+
+__device__ __forceinline__ void attend_keys(const uint16_t* __restrict__ ks,
+                                            const uint16_t* __restrict__ vt, int vts,
+                                            uint32_t live_v, int kb_end, int r,
+                                            int h, const u32x4 (&qf)[kDh / 16], float c,
+                                            f32x16& o0, f32x16& o1, float& l) {
+  const float thr = kRescaleLog2 / c;  // the threshold in raw score units
+  float m = -INFINITY, mc = 0.f;       // running max (raw units) and m * c
+  l = 0.f;
+  o0 = f32x16{};
+  o1 = f32x16{};
+  const uint16_t* v0 = vt + r * vts + 4 * h;
+  const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
+  // two named score buffers, blocks taken in pairs: S^T of the next block is issued before this
+  // block's softmax (its MFMAs run under that VALU work) with no register rotation
+  f32x16 sa = score_block(ks, 0, r, h, qf), sb;
+  for (int kb = 0; kb < kb_end; kb += 2) {
+    if (kb + 1 < kb_end) sb = score_block(ks, kb + 1, r, h, qf);
+    attend_block(sa, __builtin_amdgcn_readlane(live_v, kb), kb, h, c, thr, v0, v1, m, mc, l, o0, o1);
+    if (kb + 1 >= kb_end) break;
+    if (kb + 2 < kb_end) sa = score_block(ks, kb + 2, r, h, qf);
+    attend_block(sb, __builtin_amdgcn_readlane(live_v, kb + 1), kb + 1, h, c, thr, v0, v1, m, mc, l,
+                 o0, o1);
+  }
+}
+
+// Lane i < nkb of the result holds block i's live-key bits; *kb_end = one past the last block
+// holding a live key (workgroup-uniform; 0 when every key is padding).
+__device__ __forceinline__ uint32_t live_lanes(const uint32_t* live, int nkb, int& kb_end) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t v = lane < nkb ? live[lane] : 0u;
+  const uint64_t nz = __builtin_amdgcn_ballot_w64(v != 0u);
+  kb_end = nz ? 64 - __builtin_clzll(nz) : 0;
+  return v;
+}
+
+__global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
     const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
     int L, int heads, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -73,7 +201,7 @@ __global__ __launch_bounds__(kThreads) void attention_f16_kernel(
   const int vts = vt_stride(lp);
   uint16_t* ks = reinterpret_cast<uint16_t*>(smem);               // [lp][kKStride]
   uint16_t* vt = ks + lp * kKStride;                               // [kDh][vts]
-  float* kbias = reinterpret_cast<float*>(vt + kDh * vts);         // [lp] 0 or -inf
+  uint32_t* live = reinterpret_cast<uint32_t*>(vt + kDh * vts);   // [lp / 32] live-key bits
 
   const int qblk = blockIdx.x;
   const int head = blockIdx.y;
@@ -142,66 +270,26 @@ __global__ __launch_bounds__(kThreads) void attention_f16_kernel(
       }
     }
   }
-  for (int j = tid; j < lp; j += kThreads)
-    kbias[j] = (j < L && mask[(size_t)seq * L + j] != 0) ? 0.f : -INFINITY;
+  {  // key j = tid (L <= 512 = kThreads): one ballot per wave gives two blocks' live bits
+    const bool lk = tid < L && mask[(size_t)seq * L + tid] != 0;
+    const uint64_t bits = __builtin_amdgcn_ballot_w64(lk);
+    if (lane == 0 && 64 * wave < lp) {
+      live[2 * wave] = (uint32_t)bits;
+      if (64 * wave + 32 < lp) live[2 * wave + 1] = (uint32_t)(bits >> 32);
+    }
+  }
   __syncthreads();
   if (qw0 >= L) return;  // wave-uniform: no query of this wave exists (after the only barrier)
-  const int nkb = lp / 32;
+  int kb_end;
+  const uint32_t live_v = live_lanes(live, lp / 32, kb_end);
 
   // One pass, online softmax in the exp2 domain (s' = s * scale * log2 e). O is accumulated
   // transposed, O^T = V^T . P^T: the P^T accumulator of S^T is the B operand as it stands and
   // O^T's column (the query) is the lane, so the running max, sum and rescale are all in-lane.
-  float m = -INFINITY, l = 0.f;
-  f32x16 o0 = {}, o1 = {};  // O^T rows (dims) (i&3)+8(i>>2)+4h and 32 + that, column q
-  const uint16_t* v0 = vt + r * vts + 4 * h;
-  const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
-  // S^T of block kb + 1 is issued before the softmax of block kb, so its MFMAs run under that
-  // VALU work. exp2 is the bare v_exp_f32 (arguments are <= 0; a result below 2^-126 flushes to
-  // 0, which no fp16 P or fp32 running sum can represent next to the block maximum's 1 anyway).
-  f32x16 nxt = score_block(ks, 0, r, h, qf);
-  for (int kb = 0; kb < nkb; ++kb) {
-    const f32x16 acc = nxt;
-    if (kb + 1 < nkb) nxt = score_block(ks, kb + 1, r, h, qf);
-    float s[16];
-    float bm = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s[i] = acc[i] * scale_log2 + kbias[kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
-      bm = fmaxf(bm, s[i]);
-    }
-    bm = fmaxf(bm, __shfl_xor(bm, 32));
-    const float mn = fmaxf(m, bm);
-    if (mn == -INFINITY) continue;  // every key so far is padding (same for all lanes)
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);  // 0 on the first live block (m == -inf)
-    float p[16];
-    float add = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      p[i] = __builtin_amdgcn_exp2f(s[i] - mn);
-      add += p[i];
-    }
-    l = l * alpha + add;
-    m = mn;
-    o0 *= alpha;
-    o1 *= alpha;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      // B fragment of k-step st: registers 8st..8st+7 = keys 16st + 8(j>>2) + 4h + (j&3)
-      u32x4 pb;
-      pb[0] = pack_h2(p[8 * st + 0], p[8 * st + 1]);
-      pb[1] = pack_h2(p[8 * st + 2], p[8 * st + 3]);
-      pb[2] = pack_h2(p[8 * st + 4], p[8 * st + 5]);
-      pb[3] = pack_h2(p[8 * st + 6], p[8 * st + 7]);
-      const int key0 = kb * 32 + 16 * st;
-      const u32x2 a0 = *reinterpret_cast<const u32x2*>(v0 + key0);
-      const u32x2 a1 = *reinterpret_cast<const u32x2*>(v0 + key0 + 8);
-      const u32x2 b0 = *reinterpret_cast<const u32x2*>(v1 + key0);
-      const u32x2 b1 = *reinterpret_cast<const u32x2*>(v1 + key0 + 8);
-      o0 = mfma16(u32x4{a0[0], a0[1], a1[0], a1[1]}, pb, o0);
-      o1 = mfma16(u32x4{b0[0], b0[1], b1[0], b1[1]}, pb, o1);
-    }
-  }
-  l += __shfl_xor(l, 32);  // both lane halves saw the same running max
+  f32x16 o0, o1;
+  float l;
+  attend_keys(ks, vt, vts, live_v, kb_end, r, h, qf, scale_log2, o0, o1, l);
+  l = halves_sum(l);  // both lane halves share the running max
   const float inv_l = l > 0.f ? 1.0f / l : 0.f;
 
   // lane (r, h) holds query r, dims 8g + 4h + (0..3) (o0) and 32 + those (o1): 8-byte stores
@@ -247,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void attention_f16_persist_kernel(
   // prefetch registers (next pair): K chunks e = tid + 512 u (u < 4), V key pairs e = tid + 512 u
   // (u < 2), as the one-shot kernel's round; the wave's Q fragments; this thread's key bias
   u32x4 kv[4], va[2], vb[2], qn[kDh / 16];
-  float kbias_pre = 0.f;
+  bool key_live = false;
   auto load_pair = [&](int pair) {
     const int seq = pair / heads, head = pair - (pair / heads) * heads;
     const uint16_t* base = qkv + (size_t)seq * L * row_stride + head * kDh;
@@ -275,13 +363,12 @@ __global__ __launch_bounds__(kThreads) void attention_f16_persist_kernel(
       if (j < L) va[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)j * row_stride);
       if (j + 1 < L) vb[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)(j + 1) * row_stride);
     }
-    kbias_pre = -INFINITY;
-    if (tid < L && mask[(size_t)seq * L + tid] != 0) kbias_pre = 0.f;
+    key_live = tid < L && mask[(size_t)seq * L + tid] != 0;
   };
   auto store_pair = [&](int buf) {
     uint16_t* ks = reinterpret_cast<uint16_t*>(smem + (size_t)buf * buf_bytes);
     uint16_t* vt = ks + lp * kKStride;
-    float* kbias = reinterpret_cast<float*>(vt + kDh * vts);
+    uint32_t* live = reinterpret_cast<uint32_t*>(vt + kDh * vts);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = tid + kThreads * u;
@@ -303,7 +390,11 @@ __global__ __launch_bounds__(kThreads) void attention_f16_persist_kernel(
         }
       }
     }
-    if (tid < lp) kbias[tid] = kbias_pre;
+    const uint64_t bits = __builtin_amdgcn_ballot_w64(key_live);
+    if (lane == 0 && 64 * wave < lp) {
+      live[2 * wave] = (uint32_t)bits;
+      if (64 * wave + 32 < lp) live[2 * wave + 1] = (uint32_t)(bits >> 32);
+    }
   };
 
   int pair = blockIdx.x;
@@ -321,54 +412,13 @@ __global__ __launch_bounds__(kThreads) void attention_f16_persist_kernel(
     if (qw0 < L) {  // wave-uniform: this wave has queries
       const uint16_t* ks = reinterpret_cast<const uint16_t*>(smem + (size_t)buf * buf_bytes);
       const uint16_t* vt = ks + lp * kKStride;
-      const float* kbias = reinterpret_cast<const float*>(vt + kDh * vts);
-      float m = -INFINITY, l = 0.f;
-      f32x16 o0 = {}, o1 = {};
-      const uint16_t* v0 = vt + r * vts + 4 * h;
-      const uint16_t* v1 = vt + (32 + r) * vts + 4 * h;
-      f32x16 nxt = score_block(ks, 0, r, h, qf);
-      for (int kb = 0; kb < nkb; ++kb) {
-        const f32x16 acc = nxt;
-        if (kb + 1 < nkb) nxt = score_block(ks, kb + 1, r, h, qf);
-        float sc[16];
-        float bm = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          sc[i] = acc[i] * scale_log2 + kbias[kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
-          bm = fmaxf(bm, sc[i]);
-        }
-        bm = fmaxf(bm, __shfl_xor(bm, 32));
-        const float mn = fmaxf(m, bm);
-        if (mn == -INFINITY) continue;
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        float pr[16];
-        float add = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          pr[i] = __builtin_amdgcn_exp2f(sc[i] - mn);
-          add += pr[i];
-        }
-        l = l * alpha + add;
-        m = mn;
-        o0 *= alpha;
-        o1 *= alpha;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          u32x4 pb;
-          pb[0] = pack_h2(pr[8 * st + 0], pr[8 * st + 1]);
-          pb[1] = pack_h2(pr[8 * st + 2], pr[8 * st + 3]);
-          pb[2] = pack_h2(pr[8 * st + 4], pr[8 * st + 5]);
-          pb[3] = pack_h2(pr[8 * st + 6], pr[8 * st + 7]);
-          const int key0 = kb * 32 + 16 * st;
-          const u32x2 a0 = *reinterpret_cast<const u32x2*>(v0 + key0);
-          const u32x2 a1 = *reinterpret_cast<const u32x2*>(v0 + key0 + 8);
-          const u32x2 b0 = *reinterpret_cast<const u32x2*>(v1 + key0);
-          const u32x2 b1 = *reinterpret_cast<const u32x2*>(v1 + key0 + 8);
-          o0 = mfma16(u32x4{a0[0], a0[1], a1[0], a1[1]}, pb, o0);
-          o1 = mfma16(u32x4{b0[0], b0[1], b1[0], b1[1]}, pb, o1);
-        }
-      }
-      l += __shfl_xor(l, 32);
+      const uint32_t* live = reinterpret_cast<const uint32_t*>(vt + kDh * vts);
+      f32x16 o0, o1;
+      float l;
+      int kb_end;
+      const uint32_t live_v = live_lanes(live, nkb, kb_end);
+      attend_keys(ks, vt, vts, live_v, kb_end, r, h, qf, scale_log2, o0, o1, l);
+      l = halves_sum(l);
       const float inv_l = l > 0.f ? 1.0f / l : 0.f;
       if (q < L) {
         const int seq = pair / heads, head = pair - (pair / heads) * heads;

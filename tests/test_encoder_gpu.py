@@ -179,7 +179,8 @@ def _attention_ref(qkv, mask, H, dh):
 @pytest.mark.parametrize("L", [1, 7, 33, 128, 200, 256, 512])
 def test_attention_f16_matches_fp32_reference(gpu, L):
     """armi_enc_attention_f16 against fp32 eager attention of the same fp16 Q/K/V; tolerance
-    3e-3 absolute on O(1) outputs (P is rounded to fp16 before P.V)."""
+    3e-3 absolute + 1e-3 relative on O(1) outputs (P is rounded to fp16 before P.V, and the
+    output itself is fp16: half an ulp is 4.9e-4 relative, 2e-3 at |o| = 4)."""
     g = torch.Generator().manual_seed(100 + L)
     n, H, dh = 3, 12, 64
     qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
@@ -191,7 +192,7 @@ def test_attention_f16_matches_fp32_reference(gpu, L):
     out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
     _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
           1 / math.sqrt(dh))
-    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
 
 
 @pytest.mark.parametrize("L", [7, 100, 256])
@@ -212,7 +213,7 @@ def test_attention_f16_persistent_matches_fp32_reference(gpu, L, monkeypatch):
     out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
     _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
           1 / math.sqrt(dh))
-    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
 
 
 def test_attention_f16_peaked_scores(gpu):
@@ -230,7 +231,33 @@ def test_attention_f16_peaked_scores(gpu):
     out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
     _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
           1 / math.sqrt(dh))
-    torch.testing.assert_close(out.float().cpu(), ref, rtol=0, atol=3e-3)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
+
+
+@pytest.mark.parametrize("growth", [0.5, 9.0, 40.0])
+def test_attention_f16_rising_scores(gpu, growth):
+    """Scores that rise block after block (key j's K = (1 + growth * j / 32) * k0, queries
+    aligned with k0), so the running maximum grows by less than, about and far more than the
+    deferred-rescale threshold (2^8 in P) from one 32-key block to the next: every rescale
+    decision (taken, skipped, first block) is exercised, ragged masks included."""
+    n, L, H, dh = 3, 320, 12, 64
+    g = torch.Generator().manual_seed(11)
+    qkv = torch.randn(n, L, 3, H, dh, generator=g) * 0.3
+    k0 = torch.randn(H, dh, generator=g)
+    k0 = k0 / k0.norm(dim=-1, keepdim=True)
+    ramp = 1 + growth * torch.arange(L, dtype=torch.float32) / 32
+    qkv[:, :, 1] += (ramp[:, None, None] * k0[None]) * 2.0
+    qkv[:, :, 0] += k0[None, None] * 2.5
+    qkv = qkv.reshape(n, L, 3 * H * dh).half()
+    mask = torch.ones(n, L, dtype=torch.int32)
+    mask[1, 200:] = 0
+    mask[2, 37:301] = 0
+    ref = _attention_ref(qkv, mask, H, dh)
+    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
+    out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
+    _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
+          1 / math.sqrt(dh))
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
 
 
 @pytest.mark.parametrize("L", [1, 7, 256, 300, 512])
