@@ -134,7 +134,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
             return _lib
         import torch  # noqa: F401  (binds the process to torch's HIP runtime first)
 
-        p = Path(path) if path else LIB_PATH
+        # ARMI_LIB_PATH: another build of the library (A/B measurements of two builds)
+        p = Path(path or os.environ.get("ARMI_LIB_PATH") or LIB_PATH)
         if not p.exists():
             raise ArmiUnavailable(
                 f"{p} not found: build it with `python -m audio_rag_amd.build` (hipcc, gfx950)")
