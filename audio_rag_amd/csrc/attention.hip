@@ -38,6 +38,12 @@ constexpr int kThreads = kWaves * 64;
 constexpr int kQPerWg = kQPerWave * kWaves;
 constexpr int kKStride = kDh + 8;  // K row stride in halves (144 B: conflict-free b128 reads)
 constexpr int kMaxL = 512;
+// Probe builds only (ARMI_BUILD_FLAGS=-DARMI_ATT_ABL=n): 1 = stage K / V / Q but skip the
+// softmax / P.V loop, 2 = skip the HBM loads (stage zeros) but compute, 0 = the product kernel
+// (tools/probes/att_pmc.sh: at 1280 x 256 the product kernel takes the SUM of the two)
+#ifndef ARMI_ATT_ABL
+#define ARMI_ATT_ABL 0
+#endif
 
 __device__ __forceinline__ int vt_stride(int lp) { return lp + 4; }  // V^T row stride (halves)
 
@@ -222,7 +228,8 @@ __global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
 #pragma unroll
   for (int t = 0; t < kDh / 16; ++t) {
     qf[t] = u32x4{0u, 0u, 0u, 0u};
-    if (q < L) qf[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
+    if (ARMI_ATT_ABL != 2 && q < L)
+      qf[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
   }
   // Stage K (row-major) and V^T (two keys per 32-bit LDS word) of this (seq, head). Per round of
   // 256 keys thread tid loads K chunks e = tid + 512u (u < 4) and V key pairs e = tid + 512u
@@ -236,7 +243,8 @@ __global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
       const int e = tid + kThreads * u;
       const int j = j0 + (e >> 3);
       kv[u] = u32x4{0u, 0u, 0u, 0u};
-      if (j < L) kv[u] = *reinterpret_cast<const u32x4*>(kbase + (size_t)j * row_stride + 8 * (e & 7));
+      if (ARMI_ATT_ABL != 2 && j < L)
+        kv[u] = *reinterpret_cast<const u32x4*>(kbase + (size_t)j * row_stride + 8 * (e & 7));
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -245,8 +253,9 @@ __global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
       const uint16_t* vp = vbase + 8 * (e & 7);
       va[u] = u32x4{0u, 0u, 0u, 0u};
       vb[u] = u32x4{0u, 0u, 0u, 0u};
-      if (j < L) va[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)j * row_stride);
-      if (j + 1 < L) vb[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)(j + 1) * row_stride);
+      if (ARMI_ATT_ABL != 2 && j < L) va[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)j * row_stride);
+      if (ARMI_ATT_ABL != 2 && j + 1 < L)
+        vb[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)(j + 1) * row_stride);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -288,7 +297,13 @@ __global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
   // O^T's column (the query) is the lane, so the running max, sum and rescale are all in-lane.
   f32x16 o0, o1;
   float l;
-  attend_keys(ks, vt, vts, live_v, kb_end, r, h, qf, scale_log2, o0, o1, l);
+  if (ARMI_ATT_ABL == 1) {
+    o0 = f32x16{};
+    o1 = f32x16{};
+    l = 1.f;
+  } else {
+    attend_keys(ks, vt, vts, live_v, kb_end, r, h, qf, scale_log2, o0, o1, l);
+  }
   l = halves_sum(l);  // both lane halves share the running max
   const float inv_l = l > 0.f ? 1.0f / l : 0.f;
 
