@@ -46,6 +46,14 @@ SIGNATURES: dict[str, tuple] = {
     "armi_dense_topk_ex": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                                    c_void_p]),
+    "armi_dense_topk_first": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                      c_void_p, c_void_p, c_void_p]),
+    "armi_dense_second_pass": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
+    "armi_index_set_scan_cus": (c_int, [c_void_p, c_int]),
+    "armi_cu_split_streams": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "armi_dense_exact_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
     "armi_dense_exact_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -3769,16 +3769,31 @@ int launch_exact(const armi_index* idx, const uint16_t* queries, int nq, int k,
 }
 
 template <int DIM>
+int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, int k,
+                      const uint64_t* row_mask, const uint64_t* mask_i8, float* out_scores,
+                      int64_t* out_ids, double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                      const Workspace& w, hipStream_t stream, hipStream_t merge_stream,
+                      hipEvent_t merge_done, hipEvent_t pass_done);
+
+template <int DIM>
 int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int k,
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                    const Workspace& w, hipStream_t stream, hipEvent_t scan_done) {
+                    const Workspace& w, hipStream_t stream, hipEvent_t scan_done,
+                    hipStream_t merge_stream, int phases = 3, hipEvent_t merge_done = nullptr,
+                    hipEvent_t pass_done = nullptr) {
   const ScanPlan sp = plan_scan(idx, k, nq);
   int n_wg = sp.n_wg;
   int kc = sp.kc;
   const int64_t T = std::max<int64_t>(idx->n_tiles, 1);
   // the int8 passes (first pass and collect pass) read the filter in image order
   const uint64_t* mask_i8 = nullptr;
+  if (!(phases & 1)) {  // armi_dense_second_pass: the first call built the filter image
+    mask_i8 = row_mask ? w.mask_img : nullptr;
+    return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,
+                                  out_rank, out_count, out_flags, w, stream, merge_stream,
+                                  merge_done, pass_done);
+  }
   const bool i8_path = !use_gemm_scan(nq) && use_i8_filter(idx, k);
   int32_t* heads = i8_path && sp.n_qb == 1 && i8_dynamic_schedule() ? w.heads : nullptr;
   if (row_mask || heads) {
@@ -3931,6 +3946,10 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (int rc = tl.end()) return rc;
   }
   if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
+  if (merge_stream != stream) {  // armi_dense_topk_split: the rest of the call on merge_stream
+    ARMI_HIP(hipStreamWaitEvent(merge_stream, scan_done, 0));
+    stream = merge_stream;
+  }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
   ARMI_REQUIRE(n_wg >= 1 && n_wg * kKW <= kMaxPool,
@@ -3942,8 +3961,22 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
       w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
       idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt);
   ARMI_LAUNCHED("dense_merge_kernel");
-  // second pass for the uncertified queries (both kernels exit at once when every query of the
-  // call is certified): int8 collect over the whole shard, then exact rescore of the lists
+  if (!(phases & 2)) return ARMI_OK;  // armi_dense_topk_first
+  return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,
+                                out_rank, out_count, out_flags, w, stream, stream, nullptr, nullptr);
+}
+
+// Second pass for the uncertified queries (both kernels exit at once when every query of the
+// call is certified): int8 collect over the whole shard on `stream`, then exact rescore of the
+// lists on merge_stream. merge_done (nullable): `stream` waits on it first; pass_done (needed when
+// the streams differ): recorded after the collect pass, merge_stream waits on it.
+template <int DIM>
+int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, int k,
+                      const uint64_t* row_mask, const uint64_t* mask_i8, float* out_scores,
+                      int64_t* out_ids, double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                      const Workspace& w, hipStream_t stream, hipStream_t merge_stream,
+                      hipEvent_t merge_done, hipEvent_t pass_done) {
+  if (merge_done) ARMI_HIP(hipStreamWaitEvent(stream, merge_done, 0));
   {
     const ScanPlan cp = plan_scan(idx, k, 1);  // one block's ranges; blocks of one range share an XCD
     const int n_qb = (nq + kQB - 1) / kQB;
@@ -3955,6 +3988,11 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
         w.col_cnt, w.col_list, kCollectCap, nullptr, 0, nullptr, nullptr);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
+  }
+  if (merge_stream != stream) {
+    ARMI_HIP(hipEventRecord(pass_done, stream));
+    ARMI_HIP(hipStreamWaitEvent(merge_stream, pass_done, 0));
+    stream = merge_stream;
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
   dense_collect_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kColMergeLds, stream>>>(
@@ -3974,6 +4012,49 @@ int dispatch_dim(int dim, F&& f) {
     case 1024: return f(std::integral_constant<int, 1024>{});
     default: return armi::fail(ARMI_ERR_INVALID, "unsupported dim");
   }
+}
+
+int dense_topk_entry(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                     double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
+                     size_t workspace_bytes, hipStream_t stream, hipStream_t merge_stream,
+                     hipEvent_t scan_done, int phases, hipEvent_t merge_done,
+                     hipEvent_t pass_done) {
+  ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
+  ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
+  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
+  if (n_queries == 0) return ARMI_OK;
+  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && out_flags && workspace,
+               "armi_dense_topk: null pointer argument");
+  ARMI_REQUIRE(workspace_bytes >= armi_dense_workspace_bytes(idx, n_queries, k),
+               "armi_dense_topk: workspace too small");
+  ARMI_HIP(hipSetDevice(idx->device));
+  if (idx->n_rows == 0) {
+    if (phases & 1) {
+      ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
+      ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
+      ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
+      if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
+      if (merge_stream != stream) ARMI_HIP(hipStreamWaitEvent(merge_stream, scan_done, 0));
+    } else {
+      if (merge_done) ARMI_HIP(hipStreamWaitEvent(stream, merge_done, 0));
+      if (merge_stream != stream) {
+        ARMI_HIP(hipEventRecord(pass_done, stream));
+        ARMI_HIP(hipStreamWaitEvent(merge_stream, pass_done, 0));
+      }
+    }
+    return ARMI_OK;
+  }
+  const Workspace w = carve(workspace, idx, n_queries, k, true);
+  double* rank = out_rank;
+  if (!rank)
+    rank = reinterpret_cast<double*>(static_cast<char*>(workspace) + armi::align_up(w.bytes, 256));
+  return dispatch_dim(idx->dim, [&](auto D) {
+    constexpr int DIM = decltype(D)::value;
+    return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
+                                out_count, out_flags, w, stream, scan_done, merge_stream, phases,
+                                merge_done, pass_done);
+  });
 }
 
 }  // namespace
@@ -4008,31 +4089,33 @@ int armi_dense_topk_ex(const armi_index* idx, const uint16_t* queries, int n_que
                        const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                        double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
                        size_t workspace_bytes, hipStream_t stream, hipEvent_t scan_done) {
-  ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
-  ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
-  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
-  if (n_queries == 0) return ARMI_OK;
-  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && out_flags && workspace,
-               "armi_dense_topk: null pointer argument");
-  ARMI_REQUIRE(workspace_bytes >= armi_dense_workspace_bytes(idx, n_queries, k),
-               "armi_dense_topk: workspace too small");
-  ARMI_HIP(hipSetDevice(idx->device));
-  if (idx->n_rows == 0) {
-    ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
-    ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
-    ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
-    if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
-    return ARMI_OK;
-  }
-  const Workspace w = carve(workspace, idx, n_queries, k, true);
-  double* rank = out_rank;
-  if (!rank)
-    rank = reinterpret_cast<double*>(static_cast<char*>(workspace) + armi::align_up(w.bytes, 256));
-  return dispatch_dim(idx->dim, [&](auto D) {
-    constexpr int DIM = decltype(D)::value;
-    return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
-                                out_count, out_flags, w, stream, scan_done);
-  });
+  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
+                          out_count, out_flags, workspace, workspace_bytes, stream, stream,
+                          scan_done, 3, nullptr, nullptr);
+}
+
+int armi_dense_topk_first(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                          double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                          void* workspace, size_t workspace_bytes, hipStream_t stream,
+                          hipStream_t merge_stream, hipEvent_t scan_done) {
+  ARMI_REQUIRE(merge_stream == stream || scan_done != nullptr,
+               "armi_dense_topk_first: a separate merge stream needs the scan_done event");
+  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
+                          out_count, out_flags, workspace, workspace_bytes, stream, merge_stream,
+                          scan_done, 1, nullptr, nullptr);
+}
+
+int armi_dense_second_pass(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
+                           const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                           double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                           void* workspace, size_t workspace_bytes, hipStream_t stream,
+                           hipStream_t merge_stream, hipEvent_t merge_done, hipEvent_t pass_done) {
+  ARMI_REQUIRE(merge_stream == stream || pass_done != nullptr,
+               "armi_dense_second_pass: a separate merge stream needs the pass_done event");
+  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
+                          out_count, out_flags, workspace, workspace_bytes, stream, merge_stream,
+                          nullptr, 2, merge_done, pass_done);
 }
 
 size_t armi_dense_exact_workspace_bytes(const armi_index* idx, int n_queries, int k) {

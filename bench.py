@@ -241,6 +241,10 @@ def main() -> None:
     ap.add_argument("--pipeline", type=int, choices=[1, 2], default=1,
                     help="dense, 1 GPU: batches in flight on their own HIP streams (2: batch i+1's "
                          "scan starts when batch i's scan ends, batch i's merge runs beside it)")
+    ap.add_argument("--merge-cus", type=int, default=0,
+                    help="dense, 1 GPU, --pipeline 2: reserve this many CUs for the merge / second "
+                         "pass (a CU-masked stream pair, armi_cu_split_streams): every scan runs on "
+                         "the other CUs, batch i's merge on the reserved ones beside batch i+1's scan")
     ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
                                            "ingest"],
                     default="dense",
@@ -384,7 +388,49 @@ def main() -> None:
     # merge / second-pass launches run beside batch i+1's scan. Every batch still runs its whole
     # call (scan, merge, exact rescore, second pass); only the overlap is new.
     pipe = wl == "dense" and sharded is None and args.pipeline == 2
-    if pipe:
+    split = pipe and args.merge_cus > 0
+    if split:
+        # CU split: every scan (and every collect pass) on the scan stream's CUs, back to back;
+        # batch i's merge on the reserved CUs (merge stream) beside batch i+1's scan; batch i's
+        # second pass (collect pass + collect merge, both exit at once when every query is
+        # certified) issued after batch i+1's scan. Three workspaces / output sets rotate: batch
+        # i+3's scan waits until batch i's last kernel is done. Every batch still runs its whole
+        # call; finish() completes the last one inside the timed region.
+        from audio_rag_amd.retrieval.device import (cu_split_streams, dense_second_pass,
+                                                    dense_topk_first)
+        s_scan, s_merge = cu_split_streams(dev, args.merge_cus)
+        n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        index.set_scan_cus(n_cus - args.merge_cus)
+        ws = torch.empty(index.workspace_bytes(batch, pre_k), dtype=torch.uint8, device=dev)
+        p_ws = [ws, torch.empty_like(ws), torch.empty_like(ws)]
+        p_out = [TopK(scores=torch.empty((batch, k), dtype=torch.float32, device=dev),
+                      ids=torch.empty((batch, k), dtype=torch.int64, device=dev),
+                      rank=torch.empty((batch, k), dtype=torch.float64, device=dev),
+                      count=torch.empty(batch, dtype=torch.int32, device=dev),
+                      flags=torch.empty(batch, dtype=torch.int32, device=dev)) for _ in range(3)]
+        p_scan_ev = [torch.cuda.Event() for _ in range(3)]
+        p_pass_ev = [torch.cuda.Event() for _ in range(3)]
+        p_merge_ev = [None] * 3
+        p_done_ev = [None] * 3
+        p_pending = [None]  # (slot, queries) of the batch whose second pass is not issued yet
+        s_scan.wait_stream(torch.cuda.current_stream())
+        s_merge.wait_stream(torch.cuda.current_stream())
+
+        def finish():
+            """Issue the pending batch's second pass (collect on the scan CUs, collect merge on
+            the reserved ones)."""
+            if p_pending[0] is None:
+                return
+            slot, qp = p_pending[0]
+            with torch.cuda.stream(s_scan):
+                dense_second_pass(index, qp, k, p_ws[slot], p_out[slot], s_merge,
+                                  p_merge_ev[slot], p_pass_ev[slot])
+            ev = torch.cuda.Event()
+            ev.record(s_merge)
+            p_done_ev[slot] = ev
+            torch.cuda.current_stream().wait_event(ev)  # consumers on the default stream
+            p_pending[0] = None
+    elif pipe:
         p_streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
         p_ws = [ws, torch.empty_like(ws)]
         p_ev = [torch.cuda.Event() for _ in range(2)]
@@ -395,7 +441,20 @@ def main() -> None:
         j = i % n_q_batches
         ql = q_local if q_local is not None else queries[j]
         if wl == "dense":
-            if sharded is None and pipe:
+            if split and ql.shape[0] == batch:
+                slot = i % 3
+                if p_done_ev[slot] is not None:  # batch i-3's workspace / outputs released
+                    s_scan.wait_event(p_done_ev[slot])
+                with torch.cuda.stream(s_scan):
+                    out = dense_topk_first(index, ql, k, p_ws[slot], p_out[slot], s_merge,
+                                           p_scan_ev[slot])
+                ev = torch.cuda.Event()
+                ev.record(s_merge)
+                p_merge_ev[slot] = ev
+                finish()  # the previous batch's second pass, behind this batch's scan
+                p_pending[0] = (slot, ql)
+                return out
+            if sharded is None and pipe and not split:
                 st, ev = p_streams[i % 2], p_ev[i % 2]
                 if not p_synced[i % 2]:  # the inputs were made on the default stream
                     st.wait_stream(torch.cuda.current_stream())
@@ -428,6 +487,8 @@ def main() -> None:
 
     for i in range(args.warmup):
         step(i)
+    if split:
+        finish()
     barrier()
     _armi.call("armi_scan_timing_enable", 1)
     for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN):
@@ -439,6 +500,8 @@ def main() -> None:
     last = None
     for i in range(args.steps):
         last = step(i)
+    if split:
+        finish()
     barrier()
     elapsed = time.perf_counter() - t0
     rr_timing["on"] = False
@@ -453,7 +516,17 @@ def main() -> None:
     certified = None
     if wl == "dense" and last is not None and last.flags is not None:
         # over every query batch of the run (first-pass certificate; the rest took the second pass)
-        fl = torch.cat([step(i).flags for i in range(n_q_batches)]) if sharded is None else last.flags
+        if sharded is None:
+            fls = []
+            for i in range(n_q_batches):  # (pipelined modes: outputs land on other streams)
+                o = step(i)
+                if split:
+                    finish()
+                torch.cuda.synchronize()
+                fls.append(o.flags.clone())
+            fl = torch.cat(fls)
+        else:
+            fl = last.flags
         certified = float((fl == 1).float().mean().item())
 
     # p50 latency of one step (batch of 64 per GPU) and of a single query
@@ -462,6 +535,8 @@ def main() -> None:
         barrier()
         t1 = time.perf_counter()
         step(i)
+        if split:
+            finish()
         barrier()
         lat.append(time.perf_counter() - t1)
     for i in range(args.latency_iters):
@@ -528,6 +603,7 @@ def main() -> None:
             }[wl],
             "n_chunks": n, "dim": dim, "batch_per_gpu": batch, "top_k": k, "corpus": args.corpus,
             "batches_in_flight": 2 if pipe else 1,
+            "merge_cus": args.merge_cus if split else 0,
             "parallelism": f"corpus-shard{world}" + ("" if backend == "nccl" or world == 1
                                                       else f" ({backend} rehearsal, shared GPUs)"),
         },

@@ -130,6 +130,40 @@ int armi_dense_topk_ex(const armi_index* index, const uint16_t* queries, int n_q
                        void* workspace, size_t workspace_bytes, hipStream_t stream,
                        hipEvent_t scan_done);
 
+/* armi_dense_topk_ex in two calls over two streams, for a caller that keeps one batch's merge off
+ * the next batch's scan CUs (CU-split stream pair of armi_cu_split_streams, scan CUs set with
+ * armi_index_set_scan_cus):
+ *   armi_dense_topk_first: the first-pass scan on `stream`, scan_done recorded there, then the
+ *     merge on merge_stream after waiting on scan_done (required when the streams differ). The
+ *     outputs hold the certified answers; uncertified queries need the second pass.
+ *   armi_dense_second_pass: `stream` waits on merge_done (nullable: recorded by the caller on
+ *     merge_stream after the first call), runs the collect pass (exits at once when every query
+ *     is certified), records pass_done; merge_stream waits on it and rescores the collect lists.
+ * Both calls take the same workspace, which stays in use until the second call's work on
+ * merge_stream is done (bench.py rotates three). The answers equal armi_dense_topk's. */
+int armi_dense_topk_first(const armi_index* index, const uint16_t* queries, int n_queries, int k,
+                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                          double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                          void* workspace, size_t workspace_bytes, hipStream_t stream,
+                          hipStream_t merge_stream, hipEvent_t scan_done);
+int armi_dense_second_pass(const armi_index* index, const uint16_t* queries, int n_queries, int k,
+                           const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
+                           double* out_rank, int32_t* out_count, uint32_t* out_flags,
+                           void* workspace, size_t workspace_bytes, hipStream_t stream,
+                           hipStream_t merge_stream, hipEvent_t merge_done, hipEvent_t pass_done);
+
+/* Scan workgroups of the index's dense first pass: one per CU it may use; cus = 0 restores every
+ * CU of the device, cus > device CUs clamps. Changes armi_dense_workspace_bytes (size workspaces
+ * after calling it). */
+int armi_index_set_scan_cus(armi_index* index, int cus);
+
+/* Two streams over disjoint CU sets of `device` (hipExtStreamCreateWithCUMask): merge_stream on
+ * `reserve` CUs (the mask's top bits, which the runtime spreads over the XCDs), scan_stream on
+ * all the others. The caller
+ * destroys both with hipStreamDestroy. */
+int armi_cu_split_streams(int device, int reserve, hipStream_t* scan_stream,
+                          hipStream_t* merge_stream);
+
 size_t armi_dense_exact_workspace_bytes(const armi_index* index, int n_queries, int k);
 /* Exhaustive exact scan with the same outputs and ranking as armi_dense_topk. */
 int armi_dense_exact_topk(const armi_index* index, const uint16_t* queries, int n_queries, int k,
