@@ -710,9 +710,10 @@ def main() -> None:
 
 
 def secondary_configs(args) -> dict:
-    """BASELINE configs[1] and configs[2] measured beside the headline (the driver runs only the
-    default bench line): each is a child bench.py run on the same GPU, its JSON line attached
-    under "configs1" / "configs2" (value, ms_per_step, p50, rooflines)."""
+    """BASELINE configs[1] and configs[2], and north_star's 10k / 10M ends of the size sweep,
+    measured beside the headline (the driver runs only the default bench line): each is a child
+    bench.py run on the same GPU, its JSON line attached under "configs1" / "configs2" /
+    "chunks_10k" / "chunks_10M" (value, ms_per_step, p50, rooflines)."""
     import subprocess
 
     runs = {
@@ -720,6 +721,12 @@ def secondary_configs(args) -> dict:
                      "--latency-iters", "20"],
         "configs2": ["--workload", "hybrid_rerank", "--chunks", str(args.chunks), "--steps", "10",
                      "--warmup", "2", "--latency-iters", "3"],
+        # north_star's size sweep (10k / 100k / 1M / 10M chunks): the two ends besides configs1
+        # and the headline
+        "chunks_10k": ["--chunks", "10000", "--steps", "200", "--warmup", "10",
+                       "--latency-iters", "10"],
+        "chunks_10M": ["--chunks", "10000000", "--steps", "20", "--warmup", "3",
+                       "--latency-iters", "3"],
     }
     out = {}
     for key, extra in runs.items():
@@ -737,7 +744,8 @@ def secondary_configs(args) -> dict:
                 "certified_frac", "config", "roofline", "roofline_scan", "roofline_sparse",
                 "rerank_share_of_step", "dtype")
         out[key] = {kk: d[kk] for kk in keep if kk in d}
-        out[key]["baseline_config"] = {"configs1": 1, "configs2": 2}[key]
+        if key in ("configs1", "configs2"):
+            out[key]["baseline_config"] = {"configs1": 1, "configs2": 2}[key]
     return out
 
 
