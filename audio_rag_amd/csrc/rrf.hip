@@ -6,7 +6,8 @@
 //   score[id] = sum over prefetch lists of 1 / (2 + pos), pos 0-based, summed in fp64 in list
 //   order (dense list first); results sorted by score descending with a stable sort, so equal
 //   scores keep first-seen order (dense-list ids in dense order, then sparse-only ids).
-// One wave per query; both lists hold ids unique within the list (they come from top-k).
+// One wave per query; both lists hold ids unique within the list (they come from top-k). The
+// fused order is found by counting (each slot's rank = slots ahead of it), not by a sort.
 #include <limits>
 
 #include "armi_common.h"
@@ -26,7 +27,7 @@ __global__ __launch_bounds__(64) void rrf_kernel(const int64_t* __restrict__ a_i
                                                  int32_t* __restrict__ out_count) {
   __shared__ double score[kPool];
   __shared__ int64_t id[kPool];
-  __shared__ int32_t seen[kPool];
+  __shared__ int64_t a_lds[kMaxList];
   __shared__ int32_t b_match[kMaxList];
   const int q = blockIdx.x;
   const int lane = threadIdx.x;
@@ -35,26 +36,20 @@ __global__ __launch_bounds__(64) void rrf_kernel(const int64_t* __restrict__ a_i
   const int64_t* a = a_ids + (size_t)q * ka;
   const int64_t* b = b_ids + (size_t)q * kb;
 
-  // sort only the power of two covering both lists
-  const int n2 = armi::pow2_at_least(max(ca + cb, 2));
-  for (int i = lane; i < n2; i += 64) {
-    score[i] = -std::numeric_limits<double>::infinity();
-    id[i] = -1;
-    seen[i] = 0x7fffffff;
-  }
-  __syncthreads();
+  // slot s of the pool = first-seen position: dense ids in dense order, then the sparse-only ids
+  // in sparse order (the reference's dict insertion order); its ranking key is (score desc, s asc)
   for (int i = lane; i < ca; i += 64) {
-    id[i] = a[i];
+    const int64_t x = a[i];
+    a_lds[i] = x;
+    id[i] = x;
     score[i] = 1.0 / (double)(rrf_k + i);
-    seen[i] = i;
   }
   __syncthreads();
-  // each sparse id: its slot in the dense list, or -1
+  // each sparse id: its slot in the dense list, or -1 (the dense ids are read as LDS broadcasts)
   for (int j = lane; j < cb; j += 64) {
     const int64_t x = b[j];
     int hit = -1;
-    for (int i = 0; i < ca; ++i)
-      if (id[i] == x) { hit = i; break; }
+    for (int i = ca - 1; i >= 0; --i) hit = a_lds[i] == x ? i : hit;
     b_match[j] = hit;
   }
   __syncthreads();
@@ -72,35 +67,32 @@ __global__ __launch_bounds__(64) void rrf_kernel(const int64_t* __restrict__ a_i
       const int slot = ca + appended + before;
       id[slot] = b[j];
       score[slot] = 1.0 / (double)(rrf_k + j);
-      seen[slot] = slot;
     }
     appended += __popcll(m);
   }
   const int n = ca + appended;
   __syncthreads();
-  // stable descending sort: key (score desc, seen asc)
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = lane; t < n2 / 2; t += 64) {
-        const int lo = 2 * t - (t & (stride - 1));
-        const int hi = lo + stride;
-        const bool desc = (lo & size) == 0;
-        const bool hi_better =
-            score[hi] > score[lo] || (score[hi] == score[lo] && seen[hi] < seen[lo]);
-        if (hi_better == desc) {
-          const double ts = score[lo]; score[lo] = score[hi]; score[hi] = ts;
-          const int64_t ti = id[lo]; id[lo] = id[hi]; id[hi] = ti;
-          const int32_t tn = seen[lo]; seen[lo] = seen[hi]; seen[hi] = tn;
-        }
-      }
-      __syncthreads();
+  // rank by counting: the final position of slot p is the number of slots ranked ahead of it
+  // (higher score, or equal score and earlier slot: the stable descending sort); every lane
+  // reads the pool as LDS broadcasts, no sorting network and no barrier per stage
+  const int n_out = min(n, limit);
+  for (int p = lane; p < n; p += 64) {
+    const double sp = score[p];
+    int r = 0;
+    for (int o = 0; o < n; ++o) {
+      const double so = score[o];
+      r += (so > sp || (so == sp && o < p)) ? 1 : 0;
+    }
+    if (r < n_out) {
+      const size_t dst = (size_t)q * limit + r;
+      out_ids[dst] = id[p];
+      out_scores[dst] = sp;
     }
   }
-  const int n_out = min(n, limit);
-  for (int c = lane; c < limit; c += 64) {
-    const size_t o = (size_t)q * limit + c;
-    out_ids[o] = c < n_out ? id[c] : -1;
-    out_scores[o] = c < n_out ? score[c] : 0.0;
+  for (int c = n_out + lane; c < limit; c += 64) {
+    const size_t dst = (size_t)q * limit + c;
+    out_ids[dst] = -1;
+    out_scores[dst] = 0.0;
   }
   if (lane == 0) out_count[q] = n_out;
 }
