@@ -363,9 +363,15 @@ class ConcurrentHybrid:
         for t in sparse_inputs:
             if isinstance(t, torch.Tensor) and t.is_cuda:
                 t.record_stream(self.side)
-        with torch.cuda.stream(self.side):
-            s = sparse_fn()
-        d = dense_fn()
+        # issue order (A/B, ARMI_HYBRID_ORDER=dense): the sparse chain first by default
+        if os.environ.get("ARMI_HYBRID_ORDER", "sparse").startswith("d"):
+            d = dense_fn()
+            with torch.cuda.stream(self.side):
+                s = sparse_fn()
+        else:
+            with torch.cuda.stream(self.side):
+                s = sparse_fn()
+            d = dense_fn()
         main.wait_stream(self.side)
         for t in s.tensors():
             t.record_stream(main)

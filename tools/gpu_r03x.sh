@@ -11,6 +11,10 @@ echo "pytest rc=$rc $(tail -1 gpurun_out/${TAG}_pytest.log)"
 j() { tail -1 "$1" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($2)"; }
 timeout -k 10 300 python bench.py --workload hybrid --no-cpu-baseline > gpurun_out/${TAG}_bench_hybrid.log 2>&1 || exit $?
 echo "hybrid: $(j gpurun_out/${TAG}_bench_hybrid.log 'round(d["value"]), round(d["ms_per_step"],4)')"
+ARMI_HYBRID_ORDER=dense timeout -k 10 300 python bench.py --workload hybrid --no-cpu-baseline > gpurun_out/${TAG}_bench_hybrid_dfirst.log 2>&1 || exit $?
+echo "hybrid dense-first: $(j gpurun_out/${TAG}_bench_hybrid_dfirst.log 'round(d["value"]), round(d["ms_per_step"],4)')"
+ARMI_HYBRID_SERIAL=1 timeout -k 10 300 python bench.py --workload hybrid --no-cpu-baseline > gpurun_out/${TAG}_bench_hybrid_serial.log 2>&1 || exit $?
+echo "hybrid serial: $(j gpurun_out/${TAG}_bench_hybrid_serial.log 'round(d["value"]), round(d["ms_per_step"],4)')"
 bash tools/probes/hyb_stats.sh ${TAG} > gpurun_out/${TAG}_hybst.txt 2>&1 || exit $?
 grep -i "rrf" gpurun_out/${TAG}_hybrid_kernel_stats.csv | cut -c1-30,60-140
 bash tools/gpu_bench_default.sh ${TAG}
