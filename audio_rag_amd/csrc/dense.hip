@@ -2896,6 +2896,75 @@ __device__ __forceinline__ void exact_keys8(const int32_t (&qf)[DIM / 64],
   key = row >= 0 ? (double)dot * myinv : kNegInfD;
 }
 
+// fp32 keys of 8 rows at once, in exact_keys8's layout and key units (2^24 |q| cos). Each lane's
+// DIM/64 products q_i x_i are exact in fp32 (fp16 significands: 11 x 11 bits, |q_i x_i| < 4 and
+// >= 2^-48, no under- or overflow), summed by FMA in element order, then the 8 rows' 64 lane
+// partials by the same halving butterfly; key_f = dot_f * 2^48 * inv_norm[row] in double, stored
+// as float. |key_f - key| <= (DIM + 66) 2^-24 |q| |x| * 2^24 / |x| + |key| 2^-24
+// <= (DIM + 67) |q| (standard FMA-sum error bound over <= DIM + 6 roundings, Cauchy-Schwarz;
+// the last term the float store).
+template <int DIM>
+__device__ __forceinline__ void approx_keys8(const float (&qh)[DIM / 64],
+                                             const uint16_t* __restrict__ rows,
+                                             const double* __restrict__ inv_norm,
+                                             const int32_t (&rr)[8], int lane, float& key,
+                                             int32_t& row) {
+  u32x2 raw[8][DIM / 256];
+  double inv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int32_t src = rr[j] >= 0 ? rr[j] : 0;
+    load_raw<DIM>(rows + (size_t)src * DIM, lane, raw[j]);
+    inv[j] = inv_norm[src];
+  }
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < DIM / 256; ++i) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const uint32_t word = raw[j][i][w];
+        const float x0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(word & 0xffffu));
+        const float x1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(word >> 16));
+        acc = __builtin_fmaf(qh[4 * i + 2 * w], x0, acc);
+        acc = __builtin_fmaf(qh[4 * i + 2 * w + 1], x1, acc);
+      }
+    }
+    v[j] = acc;
+  }
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const float mine = b5 ? v[4 + m] : v[m];
+    const float give = b5 ? v[m] : v[4 + m];
+    v[m] = mine + __shfl_xor(give, 32);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float mine = b4 ? v[2 + m] : v[m];
+    const float give = b4 ? v[m] : v[2 + m];
+    v[m] = mine + __shfl_xor(give, 16);
+  }
+  float dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
+  dot += __shfl_xor(dot, 4);
+  dot += __shfl_xor(dot, 2);
+  dot += __shfl_xor(dot, 1);
+  const int r = (lane >> 3) & 7;
+  row = -1;
+  double myinv = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j == r) {
+      row = rr[j];
+      myinv = inv[j];
+    }
+  }
+  key = row >= 0 ? (float)((double)dot * 281474976710656.0 * myinv) : kNegInf;
+  if (key != key) key = __builtin_inff();  // NaN: always rescored exactly
+}
+
 // Largest float <= x (x finite or infinite).
 __device__ __forceinline__ float f32_round_down(double x) {
   float f = (float)x;
@@ -2931,7 +3000,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     int sel_rank, int64_t ordinal_base,
     float* __restrict__ out_scores, int64_t* __restrict__ out_ids, double* __restrict__ out_rank,
     int32_t* __restrict__ out_count, uint32_t* __restrict__ out_flags, float* __restrict__ thr_out,
-    int32_t* __restrict__ col_cnt) {
+    int32_t* __restrict__ col_cnt, int two_stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* skey = reinterpret_cast<float*>(smem);                              // [kSelCap]
   int32_t* srow = reinterpret_cast<int32_t*>(smem + kSelCap * 4);            // [kSelCap]
@@ -3117,48 +3186,142 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   if (n_keep > 64 && n_keep <= 4 * 64 && kc <= 64) bound = fmaxf(bound, red[10]);
   if (kc < n2) bound = fmaxf(bound, skey[kc]);
 
-  // exact rescore of the kc best, kRescoreBatch rows in flight per wave (exact_keys8)
   static_assert(kRescoreBatch == 8, "exact_keys8 reduces 8 rows");
   constexpr int kMW = kDenseMergeThreads / 64;
   const int per_wave = (kc + kMW - 1) / kMW;
-  for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
+  // Two-stage rescore (default; two_stage = 0: every one of the kc exactly, the round-3 form).
+  // Stage 1: fp32 keys key_f of the kc best (approx_keys8), |key_f - key| <= e_f. Every row with
+  // key_f >= cut = (k-th largest key_f) - 2 e_f is rescored exactly; a row below cut has
+  // key < k-th key_f - e_f <= the exact key of each of the k rows with key_f >= k-th key_f, so
+  // the exactly rescored rows hold the top-k of the kc (ties at the k-th included), and only
+  // ~k + a few of the kc pay the int64 arithmetic.
+  int32_t* xlist = reinterpret_cast<int32_t*>(smem + kSelCap * 8 + 256 * 16 + 64 + 16);  // [256]
+  int n_x = kc;  // rows rescored exactly (entries of xlist when two_stage)
+  if (two_stage) {
+    float qh[DIM / 64];
+    {
+      u32x2 qraw[DIM / 256];
+      load_raw<DIM>(queries + (size_t)qg * DIM, lane, qraw);
+#pragma unroll
+      for (int i = 0; i < DIM / 256; ++i)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          qh[4 * i + 2 * w] = (float)__builtin_bit_cast(_Float16, (uint16_t)(qraw[i][w] & 0xffffu));
+          qh[4 * i + 2 * w + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(qraw[i][w] >> 16));
+        }
+    }
+    for (int i0 = 0; i0 < per_wave; i0 += kRescoreBatch) {
+      int32_t rr[kRescoreBatch];
+#pragma unroll
+      for (int j = 0; j < kRescoreBatch; ++j) {
+        const int c = wave + kMW * (i0 + j);
+        const bool live = (i0 + j < per_wave) && c < kc && skey[c] != kNegInf;
+        rr[j] = live ? srow[c] : -1;
+      }
+      float key;
+      int32_t myrow;
+      approx_keys8<DIM>(qh, rows, inv_norm, rr, lane, key, myrow);
+      const int r = (lane >> 3) & 7;
+      if ((lane & 7) == 0 && i0 + r < per_wave) {
+        const int c = wave + kMW * (i0 + r);
+        if (c < kc) skey[c] = key;  // (this wave's own entries: read above, then replaced)
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      // k-th largest key_f (radix select over <= 256 entries), the cut, the list of rows >= cut
+      uint32_t u[4];
+      int live = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        u[i] = c < kc ? ord_key(skey[c]) : ord_key(kNegInf);
+        live += c < kc && skey[c] != kNegInf;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+      double cut = kNegInfD;
+      if (live >= k) {
+        uint32_t prefix = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t cand = prefix | (1u << bit);
+          int cnt = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(u[i] >= cand));
+          if (cnt >= k) prefix = cand;
+        }
+        const double e_f = (double)(DIM + 67) * qnorm_real * 1.0625;  // key units, 6 % margin
+        cut = (double)from_ord_key(prefix) - 2.0 * e_f;
+      }
+      int m = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = lane + 64 * i;
+        const float kf = c < kc ? skey[c] : kNegInf;
+        const bool take = kf != kNegInf && (double)kf >= cut;
+        const unsigned long long bm = __ballot(take);
+        if (take) xlist[m + __popcll(bm & ((1ull << lane) - 1ull))] = c;
+        m += __popcll(bm);
+      }
+      if (lane == 0) ctr[1] = m;
+    }
+    __syncthreads();
+    n_x = ctr[1];
+  }
+  // exact rescore, kRescoreBatch rows in flight per wave (exact_keys8): entry i of the exact set
+  // is xlist[i] (two_stage) or i
+  const int per_wave_x = (n_x + kMW - 1) / kMW;
+  for (int i0 = 0; i0 < per_wave_x; i0 += kRescoreBatch) {
     int32_t rr[kRescoreBatch];
 #pragma unroll
     for (int j = 0; j < kRescoreBatch; ++j) {
-      const int c = wave + kMW * (i0 + j);
-      const bool live = (i0 + j < per_wave) && skey[c] != kNegInf;
+      const int i = wave + kMW * (i0 + j);
+      bool live = i0 + j < per_wave_x && i < n_x;
+      int c = 0;
+      if (live) {
+        c = two_stage ? xlist[i] : i;
+        live = skey[c] != kNegInf;
+      }
       rr[j] = live ? srow[c] : -1;
     }
     double key;
     int32_t myrow;
     exact_keys8<DIM>(qf, rows, inv_norm, rr, lane, key, myrow);
     const int r = (lane >> 3) & 7;
-    if ((lane & 7) == 0 && i0 + r < per_wave) {
-      const int c = wave + kMW * (i0 + r);
-      rkey[c] = key;
-      rord[c] = myrow >= 0 ? ordinal_base + myrow : kNoOrd;
+    if ((lane & 7) == 0 && i0 + r < per_wave_x) {
+      const int i = wave + kMW * (i0 + r);
+      if (i < n_x) {
+        rkey[i] = key;
+        rord[i] = myrow >= 0 ? ordinal_base + myrow : kNoOrd;
+      }
     }
+  }
+  // sort the exact set: n_s = its size padded to a power of two (<= kc)
+  const int n_s = n_x <= 64 ? 64 : armi::pow2_at_least(n_x);
+  for (int i = n_x + tid; i < n_s; i += kDenseMergeThreads) {
+    rkey[i] = kNegInfD;
+    rord[i] = kNoOrd;
   }
   __syncthreads();
   MERGE_STAMP(5);
-  if (kc <= 64) {
+  if (n_s <= 64) {
     if (wave == 0) {
-      double key = lane < kc ? rkey[lane] : kNegInfD;
-      int64_t ord = lane < kc ? rord[lane] : kNoOrd;
+      double key = rkey[lane];
+      int64_t ord = rord[lane];
       armi::wave_sort_rank_desc(key, ord);
       rkey[lane] = key;
       rord[lane] = ord;
     }
     __syncthreads();
   } else {
-    armi::lds_sort_rank_desc(rkey, rord, kc);
+    armi::lds_sort_rank_desc(rkey, rord, n_s);
   }
 
   MERGE_STAMP(6);
   if (wave != 0) return;
   // valid entries form a prefix of the sorted list
   int n_valid = 0;
-  for (int c = lane; c < kc; c += 64) n_valid += rord[c] != kNoOrd;
+  for (int c = lane; c < n_s; c += 64) n_valid += rord[c] != kNoOrd;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
   bool certified;
@@ -3201,7 +3364,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   MERGE_STAMP(7);
 }
 
-constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16;
+constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16 + 256 * 4;
 
 // Second-pass merge, one workgroup per query (certified queries exit at once): exact keys of the
 // rows dense_scan_i8_kernel<COLLECT> appended (image positions -> ordinals), top-k by (key desc,
@@ -3638,6 +3801,19 @@ int kc_i8(int k) {
   return use_q8(k) ? 128 : (k <= 10 ? 64 : (k <= 20 ? 128 : 256));
 }
 
+// dense_merge_kernel's rescore: fp32 keys of the kc best, exact keys only for the rows within the
+// fp32 error of the k-th, when kc > 64 (k > 10: hybrid's prefetch of 40 rescores 256); else every
+// one of the kc exactly. Measured (profiles/r03y_*): kc 256 two-stage 0.274 vs 0.280 ms per 1M
+// step at k = 40 and hybrid 0.568 vs 0.575-0.589 ms; kc 64 two-stage 0.2585 vs 0.2557 ms (k = 5)
+// and 0.0775 vs 0.0724 ms at 100k rows, where the fp32 pass's extra round trip and barrier cost
+// more than the int64 work it saves. ARMI_MERGE_RESCORE=exact|two forces either (A/B, tests).
+bool merge_two_stage(int kc) {
+  const char* e = getenv("ARMI_MERGE_RESCORE");  // (read per call: tests switch in-process)
+  if (e && e[0] == 'e') return false;
+  if (e && e[0] == 't') return true;
+  return kc > 64;
+}
+
 // Threshold column of the merge's pool selection (dense_merge_kernel): the smallest J (power of
 // two, <= kKW) with r = ceil(kc / J) <= n_wg.
 void merge_select(int kc, int n_wg, int& col, int& rank) {
@@ -3959,7 +4135,8 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
-      idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt);
+      idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt,
+      merge_two_stage(kc) ? 1 : 0);
   ARMI_LAUNCHED("dense_merge_kernel");
   if (!(phases & 2)) return ARMI_OK;  // armi_dense_topk_first
   return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,

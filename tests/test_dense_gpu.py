@@ -317,3 +317,27 @@ def test_cu_split_scan_and_merge_streams(gpu, oracle_mod):
     idx.set_scan_cus(0)
     got = _run(idx, qs[2], 10, gpu)
     _assert_same(got, oracle_mod.dense_topk(rows, qs[2], 10), 10)
+
+
+@pytest.mark.parametrize("mode", ["two_stage", "exact"])
+@pytest.mark.parametrize("k", [5, 40])
+def test_merge_rescore_modes_near_ties(gpu, oracle_mod, monkeypatch, mode, k):
+    """dense_merge_kernel's rescore: fp32 keys first, int64 exact keys only within the fp32 error
+    of the k-th (ARMI_MERGE_RESCORE=two; the default for kc > 64), or all kc exactly (=exact; the
+    default for kc <= 64). Rows that differ from
+    each other by one fp16 ulp in one component, exact duplicates around the k-th position and
+    a query equal to a row: both modes return the oracle's answer bit for bit."""
+    monkeypatch.setenv("ARMI_MERGE_RESCORE", "exact" if mode == "exact" else "two")
+    rows = oracle_mod.unit_fp16(30000, 1024, seed=91)
+    base = rows[500].copy()
+    for j in range(1, 60):  # one-ulp neighbours of row 500 in component j
+        r = base.copy()
+        r[j] = np.uint16(int(r[j]) + (1 if j % 2 else -1))
+        rows[500 + j] = r
+    rows[700:712] = rows[500]  # exact duplicates
+    idx = _index(rows, gpu)
+    qs = oracle_mod.unit_fp16(64, 1024, seed=92)
+    qs[:4] = rows[500]
+    qs[4:8] = rows[530]
+    got = _run(idx, qs, k, gpu)
+    _assert_same(got, oracle_mod.dense_topk(rows, qs, k), k)
