@@ -62,11 +62,13 @@ struct Carver {
 
 // Exact integer image of an IEEE binary16 value: x * 2^24 (every finite fp16 is an integer
 // multiple of 2^-24). Callers guarantee exponent field <= 15 (|x| < 2), so |result| < 2^25.
+// Through fp32: the fp16 -> fp32 conversion is exact (subnormals included), x * 2^24 is an
+// integer of at most 11 significant bits (exact in fp32) and the conversion to int32 exact:
+// 3 instructions instead of the bit-field form's ~9 (every in-domain fp16 bit pattern checked
+// against the bit-field form, the same integers).
 __device__ __forceinline__ int32_t fp16_to_fixed24(uint32_t h) {
-  const int32_t e = (h >> 10) & 31;
-  const int32_t m = h & 1023;
-  const int32_t v = (e == 0) ? m : ((1024 | m) << (e - 1));
-  return (h & 0x8000u) ? -v : v;
+  const float x = (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  return (int32_t)(x * 16777216.0f);
 }
 
 __device__ __forceinline__ bool fp16_in_domain(uint32_t h) { return ((h >> 10) & 31) <= 15; }
