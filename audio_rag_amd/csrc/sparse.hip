@@ -914,8 +914,22 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   }
 }
 
+// Order-preserving map of a float to uint32 (larger float -> larger key; -inf lowest).
+__device__ __forceinline__ uint32_t ord_key_f(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float from_ord_key_f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 // One workgroup per query: keep the pooled entries >= t0 (the k-th largest workgroup maximum, a
 // lower bound of the pooled k-th best), sort them, keep k, certify, emit.
+// Round 3: the whole pool (16 entries per thread), the lists' bounds and maxima are loaded in one
+// round trip before anything waits (was one dependent load per loop trip), t0 comes from a
+// one-wave radix select over the maxima (was a 256-entry LDS bitonic sort), and up to 64 kept
+// entries are sorted inside one wave.
+constexpr int kSmPer = kMaxRanges * kKW / 256;  // pool entries per thread (one round)
 __global__ __launch_bounds__(256) void sparse_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
     const float* __restrict__ cand_bound, int n_wg, int q_first, int k, int64_t ordinal_base,
@@ -924,9 +938,9 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   // flags / kth_out are indexed by the query's position within the pass (ql); outputs by qg
   __shared__ float skey[kSelCap];
   __shared__ int32_t srow[kSelCap];
-  __shared__ float mx[256];
-  __shared__ int32_t mxr[256];
+  __shared__ uint32_t umax[256];
   __shared__ float red[8];
+  __shared__ float t0s;
   __shared__ int ctr[2];
   const int ql = blockIdx.x;
   const int qg = q_first + ql;
@@ -934,35 +948,63 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   const int lane = tid & 63;
   const int wave = armi::wave_id();
   const int pool = n_wg * kKW;
-  float b = kNegInf;
-  for (int g = tid; g < 256; g += 256) {
-    float m = kNegInf;
-    if (g < n_wg) {
-      m = cand_key[((size_t)g * kQB + ql) * kKW];
-      b = fmaxf(b, cand_bound[(size_t)g * kQB + ql]);
-    }
-    mx[g] = m;
-    mxr[g] = g;
+  float kk[kSmPer];
+  int32_t rw[kSmPer];
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    const int e = tid + 256 * j;
+    const size_t src = ((size_t)(e / kKW) * kQB + ql) * kKW + (e % kKW);
+    kk[j] = e < pool ? cand_key[src] : kNegInf;
+    rw[j] = e < pool ? cand_row[src] : 0;
+  }
+  float b = tid < n_wg ? cand_bound[(size_t)tid * kQB + ql] : kNegInf;
+  // entry g * kKW is list g's maximum (sorted lists): entry j = 0 of thread tid for g = tid / 16
+  // when kKW divides 256; write every list's maximum from the thread that holds it
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    const int e = tid + 256 * j;
+    if (e < pool && e % kKW == 0) umax[e / kKW] = ord_key_f(kk[j]);
   }
   if (tid == 0) ctr[0] = 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
   if (lane == 0) red[wave] = b;
-  armi::lds_sort_approx_desc(mx, mxr, 256);
-  const float t0 = (n_wg >= k) ? mx[k - 1] : kNegInf;
+  __syncthreads();
+  if (wave == 0) {  // t0 = k-th largest list maximum (radix select over <= 256 keys)
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int g = lane + 64 * i;
+      u[i] = g < n_wg ? umax[g] : ord_key_f(kNegInf);
+    }
+    float t0 = kNegInf;
+    if (n_wg >= k) {
+      uint32_t prefix = 0;
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = prefix | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(u[i] >= cand));
+        if (cnt >= k) prefix = cand;
+      }
+      t0 = from_ord_key_f(prefix);
+    }
+    if (lane == 0) t0s = t0;
+  }
+  __syncthreads();
+  const float t0 = t0s;
   float dmax = kNegInf;
-  for (int e = tid; e < pool; e += 256) {
-    const size_t src = ((size_t)(e / kKW) * kQB + ql) * kKW + (e % kKW);
-    const float kk = cand_key[src];
-    if (kk == kNegInf) continue;
-    if (kk >= t0) {
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    if (kk[j] == kNegInf) continue;
+    if (kk[j] >= t0) {
       const int slot = atomicAdd(&ctr[0], 1);
       if (slot < kSelCap) {
-        skey[slot] = kk;
-        srow[slot] = cand_row[src];
+        skey[slot] = kk[j];
+        srow[slot] = rw[j];
       }
     } else {
-      dmax = fmaxf(dmax, kk);
+      dmax = fmaxf(dmax, kk[j]);
     }
   }
 #pragma unroll
@@ -972,23 +1014,34 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   const int n_sel = ctr[0];
   const bool overflow = n_sel > kSelCap;
   const int n_keep = overflow ? kSelCap : n_sel;
-  const int n2 = armi::pow2_at_least(max(n_keep, max(k, 2)));
-  for (int e = n_keep + tid; e < n2; e += 256) {
-    skey[e] = kNegInf;
-    srow[e] = 0x7fffffff;
+  int n2 = armi::pow2_at_least(max(n_keep, max(k, 2)));
+  if (n2 <= 64) {
+    n2 = 64;
+    if (wave == 0) {
+      float key = lane < n_keep ? skey[lane] : kNegInf;
+      int32_t row = lane < n_keep ? srow[lane] : 0x7fffffff;
+      armi::wave_sort_approx_desc(key, row);
+      skey[lane] = key;
+      srow[lane] = row;
+    }
+    __syncthreads();
+  } else {
+    for (int e = n_keep + tid; e < n2; e += 256) {
+      skey[e] = kNegInf;
+      srow[e] = 0x7fffffff;
+    }
+    armi::lds_sort_approx_desc(skey, srow, n2);
   }
-  armi::lds_sort_approx_desc(skey, srow, n2);
   float bound = red[0];
 #pragma unroll
   for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
   if (n2 > k) bound = fmaxf(bound, skey[k]);
-  if (tid == 0) {
-    int nv = 0;
-    while (nv < n2 && nv < k && skey[nv] != kNegInf) ++nv;
-    ctr[1] = nv;
-  }
-  __syncthreads();
-  const int nv = ctr[1];
+  if (wave != 0) return;
+  // valid entries form a prefix of the sorted list
+  int nv = 0;
+  for (int c = lane; c < min(n2, k); c += 64) nv += skey[c] != kNegInf;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
   bool certified;
   if (nv >= k)
     certified = skey[k - 1] > bound;
@@ -996,13 +1049,13 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
     certified = (bound == kNegInf);
   certified = certified && !overflow;
   if (certified) {
-    for (int c = tid; c < k; c += 256) {
+    for (int c = lane; c < k; c += 64) {
       const size_t o = (size_t)qg * k + c;
       out_scores[o] = c < nv ? skey[c] : kNegInf;
       out_ids[o] = c < nv ? ordinal_base + srow[c] : -1;
     }
   }
-  if (tid == 0) {
+  if (lane == 0) {
     out_count[qg] = certified ? nv : 0;
     flags[ql] |= certified ? ARMI_FLAG_CERTIFIED : 0u;
     // collection threshold of the fallback: the k-th candidate (a lower bound of the true k-th);
