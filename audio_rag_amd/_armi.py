@@ -9,11 +9,14 @@ retrieval kernels. If the library is missing or fails to load, every caller gets
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libarmi.so"
+CSRC = Path(__file__).resolve().parent / "csrc"
+HEADER = Path(__file__).resolve().parents[1] / "include" / "armi.h"
 
 ARMI_OK = 0
 ARMI_FLAG_CERTIFIED = 1
@@ -33,6 +36,7 @@ c_float = ctypes.c_float
 SIGNATURES: dict[str, tuple] = {
     "armi_last_error": (ctypes.c_char_p, []),
     "armi_abi_version": (c_int, []),
+    "armi_source_digest": (ctypes.c_char_p, []),
     "armi_index_create": (c_int, [c_int, c_void_p, c_int64, c_int, c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_dense_scan_form": (c_int, [c_void_p, c_int, c_int]),
     "armi_index_destroy": (c_int, [c_void_p]),
@@ -43,17 +47,6 @@ SIGNATURES: dict[str, tuple] = {
     "armi_dense_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
     "armi_dense_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
-    "armi_dense_topk_ex": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
-                                   c_void_p]),
-    "armi_dense_topk_first": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
-                                      c_void_p, c_void_p, c_void_p]),
-    "armi_dense_second_pass": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
-                                       c_void_p, c_void_p, c_void_p, c_void_p]),
-    "armi_index_set_scan_cus": (c_int, [c_void_p, c_int]),
-    "armi_cu_split_streams": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "armi_dense_exact_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
     "armi_dense_exact_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -116,6 +109,20 @@ SIGNATURES: dict[str, tuple] = {
 }
 
 
+def source_digest() -> str | None:
+    """sha256 (16 hex digits) over the library's sources: every csrc/*.hip, *.cpp, *.h and
+    include/armi.h, by name and content. build.py compiles it into libarmi.so
+    (armi_source_digest), and load() refuses a library built from other sources. None when the
+    sources are not present next to the package."""
+    if not CSRC.is_dir() or not HEADER.exists():
+        return None
+    h = hashlib.sha256()
+    files = sorted(p for p in CSRC.iterdir() if p.suffix in (".hip", ".cpp", ".h"))
+    for f in [*files, HEADER]:
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
 class ArmiUnavailable(RuntimeError):
     """libarmi.so is missing or unloadable: the MI355X path cannot run."""
 
@@ -157,6 +164,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
             fn.argtypes = argtypes
         if lib.armi_abi_version() != ABI_VERSION:
             raise ArmiUnavailable(f"{p}: ABI version {lib.armi_abi_version()} != {ABI_VERSION}")
+        want = source_digest()
+        got = lib.armi_source_digest().decode()
+        if want is not None and got != want:
+            raise ArmiUnavailable(f"{p} was built from other sources (digest {got}, csrc/ is "
+                                  f"{want}): rebuild it with `python -m audio_rag_amd.build`")
         _lib = lib
         return lib
 

@@ -40,12 +40,17 @@ def _digest(path: Path, headers: list[Path]) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: str, headers: list[Path]) -> Path:
+def _compile(src: str, headers: list[Path], source_digest: str) -> Path:
     path = CSRC / src
-    obj = OBJ_DIR / f"{path.stem}-{_digest(path, headers)}.o"
+    extra = []
+    tag = _digest(path, headers)
+    if src == "armi_common.cpp":  # carries armi_source_digest(): rebuilt whenever any source changes
+        extra = [f'-DARMI_SOURCE_DIGEST="{source_digest}"']
+        tag = hashlib.sha256((tag + source_digest).encode()).hexdigest()[:16]
+    obj = OBJ_DIR / f"{path.stem}-{tag}.o"
     if obj.exists():
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", str(path), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", str(path), "-o", str(obj)]
     if src.endswith(".hip"):
         cmd.insert(1, f"--offload-arch={ARCH}")
     else:
@@ -60,8 +65,11 @@ def build(verbose: bool = False) -> Path:
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h")) + [ROOT / "include" / "armi.h"]
+    from audio_rag_amd._armi import source_digest
+
+    sd = source_digest()
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, headers), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, headers, sd), SOURCES))
     tmp = LIB.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
            "-Wl,-rpath,/opt/rocm/lib", "-Wl,-z,defs", "-lamdhip64", "-lpthread"]

@@ -72,6 +72,11 @@ const char* armi_last_error(void) { return armi::g_last_error.c_str(); }
 
 int armi_abi_version(void) { return ARMI_ABI_VERSION; }
 
+#ifndef ARMI_SOURCE_DIGEST
+#define ARMI_SOURCE_DIGEST "unknown"
+#endif
+const char* armi_source_digest(void) { return ARMI_SOURCE_DIGEST; }
+
 int armi_scan_timing_enable(int enable) {
   armi::Timing& t = armi::timing();
   std::lock_guard<std::mutex> g(t.mu);

@@ -12,7 +12,7 @@ struct armi_index {
   int64_t n_tiles = 0;       // ceil(n_rows / 32)
   int dim = 0;
   int64_t ordinal_base = 0;
-  int num_cus = 0;           // CUs the dense scans launch one workgroup each for (armi_index_set_scan_cus)
+  int num_cus = 0;           // CUs of the device: the dense scans launch one workgroup each
   int device_cus = 0;        // CUs of the device
   int64_t* norm2 = nullptr;  // [n_tiles*32] exact sum of squares of the 2^24-scaled row (-1 = invalid)
   double* inv_norm = nullptr;    // [n_tiles*32] 1/sqrt(norm2)

@@ -322,139 +322,6 @@ __global__ __launch_bounds__(kThreads, 4) void attention_f16_kernel(
   }
 }
 
-// Persistent form of attention_f16_kernel for L <= 256 (one query block per (sequence, head)):
-// grid = one workgroup per CU, each walking pairs (seq, head) = blockIdx.x, +gridDim.x, ... with
-// two LDS buffers. The K / V^T / key-bias images and the Q fragments of the NEXT pair are loaded
-// into registers before the current pair's compute starts and written to the other buffer after
-// it, so every pair's HBM reads run under the previous pair's MFMAs and softmax instead of in a
-// load phase of their own (the one-shot kernel loaded, then computed, with at most two workgroups
-// per CU to overlap the two). Same arithmetic per (query, key) as attention_f16_kernel.
-constexpr int kPersistMaxL = 256;
-
-__global__ __launch_bounds__(kThreads) void attention_f16_persist_kernel(
-    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ mask, uint16_t* __restrict__ ctx,
-    int L, int heads, int n_pairs, float scale_log2, int buf_bytes) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lp = (L + 31) & ~31;
-  const int vts = vt_stride(lp);
-  const int tid = threadIdx.x;
-  const int row_stride = 3 * heads * kDh;
-  const int wave = armi::wave_id();
-  const int lane = tid & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int qw0 = wave * kQPerWave;
-  const int q = qw0 + r;
-  const int nkb = lp / 32;
-
-  // prefetch registers (next pair): K chunks e = tid + 512 u (u < 4), V key pairs e = tid + 512 u
-  // (u < 2), as the one-shot kernel's round; the wave's Q fragments; this thread's key bias
-  u32x4 kv[4], va[2], vb[2], qn[kDh / 16];
-  bool key_live = false;
-  auto load_pair = [&](int pair) {
-    const int seq = pair / heads, head = pair - (pair / heads) * heads;
-    const uint16_t* base = qkv + (size_t)seq * L * row_stride + head * kDh;
-    const uint16_t* kbase = base + heads * kDh;
-    const uint16_t* vbase = base + 2 * heads * kDh;
-#pragma unroll
-    for (int t = 0; t < kDh / 16; ++t) {
-      qn[t] = u32x4{0u, 0u, 0u, 0u};
-      if (q < L) qn[t] = *reinterpret_cast<const u32x4*>(base + (size_t)q * row_stride + 16 * t + 8 * h);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + kThreads * u;
-      const int j = e >> 3;
-      kv[u] = u32x4{0u, 0u, 0u, 0u};
-      if (j < L) kv[u] = *reinterpret_cast<const u32x4*>(kbase + (size_t)j * row_stride + 8 * (e & 7));
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + kThreads * u;
-      const int j = 2 * (e >> 3);
-      const uint16_t* vp = vbase + 8 * (e & 7);
-      va[u] = u32x4{0u, 0u, 0u, 0u};
-      vb[u] = u32x4{0u, 0u, 0u, 0u};
-      if (j < L) va[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)j * row_stride);
-      if (j + 1 < L) vb[u] = *reinterpret_cast<const u32x4*>(vp + (size_t)(j + 1) * row_stride);
-    }
-    key_live = tid < L && mask[(size_t)seq * L + tid] != 0;
-  };
-  auto store_pair = [&](int buf) {
-    uint16_t* ks = reinterpret_cast<uint16_t*>(smem + (size_t)buf * buf_bytes);
-    uint16_t* vt = ks + lp * kKStride;
-    uint32_t* live = reinterpret_cast<uint32_t*>(vt + kDh * vts);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + kThreads * u;
-      const int j = e >> 3;
-      if (j < lp) *reinterpret_cast<u32x4*>(ks + j * kKStride + 8 * (e & 7)) = kv[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + kThreads * u;
-      const int j = 2 * (e >> 3);
-      const int c = e & 7;
-      if (j < lp) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t lo = (va[u][i] & 0xffffu) | (vb[u][i] << 16);
-          const uint32_t hi = (va[u][i] >> 16) | (vb[u][i] & 0xffff0000u);
-          *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i) * vts + j) = lo;
-          *reinterpret_cast<uint32_t*>(vt + (8 * c + 2 * i + 1) * vts + j) = hi;
-        }
-      }
-    }
-    const uint64_t bits = __builtin_amdgcn_ballot_w64(key_live);
-    if (lane == 0 && 64 * wave < lp) {
-      live[2 * wave] = (uint32_t)bits;
-      if (64 * wave + 32 < lp) live[2 * wave + 1] = (uint32_t)(bits >> 32);
-    }
-  };
-
-  int pair = blockIdx.x;
-  if (pair >= n_pairs) return;  // workgroup-uniform
-  load_pair(pair);
-  store_pair(0);
-  __syncthreads();
-  for (int it = 0;; ++it) {
-    const int buf = it & 1;
-    u32x4 qf[kDh / 16];
-#pragma unroll
-    for (int t = 0; t < kDh / 16; ++t) qf[t] = qn[t];
-    const int next = pair + (int)gridDim.x;
-    if (next < n_pairs) load_pair(next);  // in flight during this pair's compute
-    if (qw0 < L) {  // wave-uniform: this wave has queries
-      const uint16_t* ks = reinterpret_cast<const uint16_t*>(smem + (size_t)buf * buf_bytes);
-      const uint16_t* vt = ks + lp * kKStride;
-      const uint32_t* live = reinterpret_cast<const uint32_t*>(vt + kDh * vts);
-      f32x16 o0, o1;
-      float l;
-      int kb_end;
-      const uint32_t live_v = live_lanes(live, nkb, kb_end);
-      attend_keys(ks, vt, vts, live_v, kb_end, r, h, qf, scale_log2, o0, o1, l);
-      l = halves_sum(l);
-      const float inv_l = l > 0.f ? 1.0f / l : 0.f;
-      if (q < L) {
-        const int seq = pair / heads, head = pair - (pair / heads) * heads;
-        uint16_t* dst = ctx + ((size_t)seq * L + q) * (heads * kDh) + head * kDh + 4 * h;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u32x2 w0 = {pack_h2(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l),
-                            pack_h2(o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l)};
-          const u32x2 w1 = {pack_h2(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l),
-                            pack_h2(o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l)};
-          *reinterpret_cast<u32x2*>(dst + 8 * g) = w0;
-          *reinterpret_cast<u32x2*>(dst + 32 + 8 * g) = w1;
-        }
-      }
-    }
-    if (next >= n_pairs) break;  // workgroup-uniform
-    store_pair(buf ^ 1);  // that buffer's last reader (the previous pair) passed the barrier below
-    __syncthreads();
-    pair = next;
-  }
-}
 
 // out = LayerNorm(x + res) (x fp16, res fp32 nullable) -> fp32 out and fp16 out16 (nullable).
 constexpr int kMaxPerLane = 16;
@@ -761,29 +628,6 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_lds_bytes(kMaxL));
   ARMI_HIP(raised);
   const float scale_log2 = scale * 1.4426950408889634f;
-  // one-shot kernel by default; ARMI_ATTENTION=persist selects the persistent double-buffered
-  // form (L <= 256, pairs enough to keep every CU busy): measured 0.9 ms per 1,280-pair forward
-  // slower on configs[2] (67.5 vs 68.4 ms, profiles/r03f_bench_rerank.json / _rerank_oneshot)
-  const char* form = getenv("ARMI_ATTENTION");  // read per call (tests switch forms in-process)
-  const bool oneshot = !(form && form[0] == 'p');
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    ARMI_HIP(hipGetDevice(&dev));
-    ARMI_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int64_t pairs = (int64_t)n_seq * heads;
-  if (!oneshot && L <= kPersistMaxL && pairs >= 2 * cus && pairs < (int64_t(1) << 31)) {
-    static const hipError_t raised_p = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(attention_f16_persist_kernel),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * attention_lds_bytes(kPersistMaxL)));
-    ARMI_HIP(raised_p);
-    const int bb = (int)((attention_lds_bytes(L) + 15) & ~size_t(15));
-    attention_f16_persist_kernel<<<dim3(cus), dim3(kThreads), 2 * (size_t)bb, stream>>>(
-        qkv, mask, ctx, L, heads, (int)pairs, scale_log2, bb);
-    ARMI_LAUNCHED("attention_f16_persist_kernel");
-    return ARMI_OK;
-  }
   attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(kThreads), lds,
                          stream>>>(qkv, mask, ctx, L, heads, scale_log2);
   ARMI_LAUNCHED("attention_f16_kernel");

@@ -103,8 +103,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
-    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
-    int guard) {
+    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
   constexpr int KSTEPS = DIM / 16;
   // workgroup -> (64-query block qb, tile range rp). With several blocks, the blocks of one range
   // get workgroup ids congruent mod 8, i.e. the same XCD: they stream the same rows at about the
@@ -245,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
       if (__any(mx0 > s0[kLaneList - 1])) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(x0[j] > s0[kLaneList - 1])) {
+          if (!__any(x0[j] > s0[kLaneList - 1])) {
             d0 = fmaxf(d0, x0[j]);  // = topm_insert of a value no lane list takes
             continue;
           }
@@ -257,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
       if (__any(mx1 > s1[kLaneList - 1])) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(x1[j] > s1[kLaneList - 1])) {
+          if (!__any(x1[j] > s1[kLaneList - 1])) {
             d1 = fmaxf(d1, x1[j]);  // = topm_insert of a value no lane list takes
             continue;
           }
@@ -332,14 +331,7 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& 
   hi = __builtin_bit_cast(uint32_t, h - bias);
 }
 
-// Loads of the int8 image (probe builds may try the non-temporal policy: -DARMI_I8_NT).
-__device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
-#if defined(ARMI_PROBE_BUILD) && defined(ARMI_I8_NT)
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+__device__ __forceinline__ u32x4 i8_load(const u32x4* p) { return *p; }
 
 // Int8-filter form of dense_scan_kernel: the default 64-query scan (round 2). Each row's first
 // pass reads its 1-byte int8 image (rows8, one 1 KB row at dim 1024) instead of its 2-byte fp16
@@ -352,12 +344,6 @@ __device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
 // dense_merge_kernel discards still satisfy exact <= bound + delta (delta: the fp32 accumulation
 // term, unchanged) and its certificate holds as for the fp16 scan; it rescoring more of the pool
 // (kc_i8) absorbs the looser keys.
-// QI8 (k <= 6): the queries are int8 too (t_q = max |q_i| / 127) and the MFMA is
-// v_mfma_i32_32x32x32_i8: exact int32 dots, no conversion VALU, half the MFMA cycles of the fp16
-// form; the key adds the query's own quantisation term: acc * t a32 + e32 |q| + e_q (1 + e32)
-// with e_q >= ||q - t_q q8||_2 (|q.x - (t q8).(s x8)| / |x| <= |q| e32 + ||q - t q8|| |s x8| / |x|).
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 // Probe builds only (-DARMI_PROBE_BUILD -DARMI_I8_STAMPS): per (workgroup, wave) s_memrealtime
 // (100 MHz, chip-wide) at kernel entry, after the query image, after the tile loop and at the
@@ -380,19 +366,16 @@ __device__ uint64_t g_i8_stamps[256 * kWaves * 4];
 // reaches it is appended to the query's list: a row of the true top-k has exact >= k-th found,
 // hence key >= thr, so the list holds the whole top-k whatever the corpus looks like (runs of
 // near-duplicates, one-ulp neighbours, exact duplicates). dense_collect_merge_kernel rescores it.
-template <int DIM, bool QI8, bool COLLECT>
+template <int DIM, bool COLLECT>
 __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
     int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
-    int guard, const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
-    const float* __restrict__ thr,
-    int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap,
-    int32_t* __restrict__ heads, int wg_counter, const u32x4* __restrict__ qimg_g,
-    const float* __restrict__ qnorm_g) {
-  static_assert(!(QI8 && COLLECT), "the collect pass uses fp16 queries");
-  constexpr int KSTEPS = QI8 ? DIM / 32 : DIM / 16;  // MFMA k-steps
+    const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
+    const float* __restrict__ thr, int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list,
+    int col_cap) {
+  constexpr int KSTEPS = DIM / 16;  // MFMA k-steps
   constexpr int GROUPS = DIM / 128;  // 128-B groups of a row: 4 chunks per lane half
   constexpr int DEPTH = GROUPS % 4 == 0 ? 4 : 2;  // groups in flight per lane
   int qb = 0, rp = blockIdx.x;
@@ -408,8 +391,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
   float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
-  float* qscale = qnorm + kQB;  // [kQB] t_q (QI8)
-  float* qerr = qscale + kQB;   // [kQB] e_q (QI8); [8][kQB] norm partials (fp16 queries)
+  float* qscale = qnorm + kQB;  // (unused slot, keeps the layout of scan_i8_lds_bytes)
+  float* qerr = qscale + kQB;   // [8][kQB] norm partials
   int32_t* qsel = reinterpret_cast<int32_t*>(qerr + kQB * (kThreads / kQB));  // [kQB] COLLECT
   float* qthr = reinterpret_cast<float*>(qsel + kQB);                        // [kQB] COLLECT
   int32_t* wcnt = reinterpret_cast<int32_t*>(qthr + kQB);                    // [kWaves]
@@ -464,53 +447,13 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
     return queries + (size_t)q * DIM;
   };
-  // Tile schedule. Static (heads == nullptr, the default): workgroup rp owns tiles
-  // [rp * tiles_per_wg, ...), wave w every kWaves-th from w. Dynamic (heads; ARMI_I8_SCHED=
-  // dynamic, one 64-query block): each wave starts on the same static tile, then dequeues the
-  // remaining tiles of its XCD's workgroups (workgroup rp runs on XCD rp % 8) from that XCD's head
-  // counter, one returning device-scope atomic per tile (issued at the top of a tile and consumed
-  // GROUPS - DEPTH groups later, when the next tile's loads start), in an order that keeps every
-  // range advancing together (dequeue v -> range i = v % nx, position kWaves + v / nx: the same
-  // spatial spread over the image as the static split), and steals from the other XCDs' heads
-  // once its own is exhausted. Every tile is scanned by exactly one wave; a workgroup's
-  // candidate lists and bound cover whatever tiles its waves scanned.
-  const bool dyn = heads != nullptr;
+  // Tile schedule: workgroup rp owns tiles [rp * tiles_per_wg, ...); wave w starts on tile
+  // t_begin + w, then takes the next tile of the range from the workgroup's LDS counter (first
+  // pass) or every kWaves-th (collect pass). A dynamic cross-workgroup dequeue (round 3) was
+  // slower (profiles/r03d_*, r03e_*) and was removed in round 4.
   const int64_t t_begin = (int64_t)rp * tiles_per_wg;
   const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
-  const int xcd = rp & 7;
-  const int64_t dyn_per_range = tiles_per_wg > kWaves ? tiles_per_wg - kWaves : 0;
-  auto nx = [&](int y) -> int64_t {  // workgroups (ranges) on XCD y
-    return y < n_ranges ? (int64_t)((n_ranges - 1 - y) / 8 + 1) : 0;
-  };
-  uint32_t gone = 0;  // XCD heads this wave found exhausted
-  int ypref = xcd;    // head dequeued from
-  // tile of dequeue v on XCD y's head: >= 0 a tile, -1 exhausted, -2 a hole (short last range)
-  auto decode = [&](int y, int64_t v) -> int64_t {
-    const int64_t n = nx(y);
-    if (v >= n * dyn_per_range) return -1;
-    const int64_t g = y + 8 * (v % n);
-    const int64_t tt = g * tiles_per_wg + kWaves + v / n;
-    return tt < min((g + 1) * (int64_t)tiles_per_wg, n_tiles) ? tt : -2;
-  };
-  auto steal = [&]() -> int64_t {  // synchronous dequeue over the heads not yet exhausted
-    for (int d = 0; d < 8; ++d) {
-      const int y = (ypref + d) & 7;
-      while (!((gone >> y) & 1u)) {
-        int v = 0;
-        if (lane == 0) v = atomicAdd(heads + 32 * y, 1);
-        v = __builtin_amdgcn_readfirstlane(v);
-        const int64_t tt = decode(y, v);
-        if (tt >= 0) {
-          ypref = y;
-          return tt;
-        }
-        if (tt == -1) gone |= 1u << y;
-      }
-    }
-    return -1;
-  };
   int64_t t = t_begin + wave < t_end ? t_begin + wave : -1;
-  if (dyn && t < 0) t = steal();
   // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
   // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
   auto row_ptr = [&](int64_t tile) -> const u32x4* {
@@ -529,41 +472,13 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         for (int i = 0; i < 4; ++i) buf[g][i] = i8_load(cur + 32 * (8 * g + i));
     }
   };
-  if constexpr (QI8) prefetch_first();
 
-  // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13) and, QI8,
-  //    t_q and e_q (rounded up, plus 2^-20 |q| for the rounding of t_q * q8_i). Then the
-  //    fragment image: fp16 (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7) or
-  //    QI8 int8 (components 128(s>>2) + 64h + 16(s&3) .. +15), the corpus chunks' order.
-  bool img_dma = false;
-  if constexpr (!QI8 && !COLLECT) img_dma = qimg_g != nullptr;
-  if (img_dma) {
-    // the fragment image and |q| prepared by query_image_kernel: LDS-DMA pieces of 1 KB (no
-    // registers, no arithmetic), issued before the first tile's prefetch and waited for by count
-    // (vmcnt(16): the 16 prefetch loads stay in flight; a __syncthreads would drain them)
-    constexpr int NP = KSTEPS * 2 * kQB * 16 / 1024;
-    static_assert(NP % kWaves == 0, "image pieces per wave");
-    const unsigned char* src =
-        reinterpret_cast<const unsigned char*>(qimg_g + (size_t)qb * KSTEPS * 2 * kQB);
-#pragma unroll
-    for (int i = 0; i < NP / kWaves; ++i) {
-      const int p = wave + kWaves * i;
-      __builtin_amdgcn_global_load_lds(src + p * 1024 + lane * 16,
-                                       (lds_ptr_t)(reinterpret_cast<unsigned char*>(qimg) + p * 1024),
-                                       16, 0, 0);
-    }
-    if (wave == 0)
-      __builtin_amdgcn_global_load_lds(qnorm_g + (size_t)qb * kQB + lane, (lds_ptr_t)qnorm, 4, 0, 0);
-    prefetch_first();
-    if (t >= 0) {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  } else if constexpr (!QI8) {
-    // fp16 image: thread (q = tid % 64, sh0 = tid / 64) copies entries sh = sh0 + 8 i of query q,
-    // all 2*KSTEPS/8 loads in flight at once (a dependent load per entry would cost one L2 round
-    // trip each), and sums its components' squares for the query norm on the way.
+  // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13), and the
+  //    fp16 fragment image (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7, the
+  //    corpus chunks' order). Thread (q = tid % 64, sh0 = tid / 64) copies entries sh = sh0 + 8 i
+  //    of query q, all 2*KSTEPS/8 loads in flight at once (a dependent load per entry would cost
+  //    one L2 round trip each), and sums its components' squares on the way.
+  {
     constexpr int PER = KSTEPS * 2 / (kThreads / kQB);  // entries per thread (16 at dim 1024)
     const int q = threadIdx.x & (kQB - 1);
     const int sh0 = threadIdx.x >> 6;
@@ -587,87 +502,16 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
       for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
     }
-    qerr[sh0 * kQB + q] = ss;  // partial sums, [8][kQB] (qerr is free in this form)
+    qerr[sh0 * kQB + q] = ss;  // partial sums, [8][kQB]
     __syncthreads();
     if (threadIdx.x < kQB) {
-      float t = 0.0f;
+      float tq = 0.0f;
 #pragma unroll
-      for (int j = 0; j < kThreads / kQB; ++j) t += qerr[j * kQB + threadIdx.x];
-      qnorm[threadIdx.x] = sqrtf(t) * (1.0f + 1.0f / 4096.0f);
+      for (int j = 0; j < kThreads / kQB; ++j) tq += qerr[j * kQB + threadIdx.x];
+      qnorm[threadIdx.x] = sqrtf(tq) * (1.0f + 1.0f / 4096.0f);
     }
-  } else {
-  for (int q = wave; q < kQB; q += kWaves) {
-    float v[DIM / 64];
-    float ss = 0.0f, mx = 0.0f;
-#pragma unroll
-    for (int i = 0; i < DIM / 64; ++i) {
-      v[i] = q < nq ? (float)__builtin_bit_cast(_Float16, queries[(size_t)q * DIM + lane + 64 * i])
-                    : 0.0f;
-      ss += v[i] * v[i];
-      mx = fmaxf(mx, fabsf(v[i]));
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      ss += __shfl_xor(ss, off);
-      mx = fmaxf(mx, __shfl_xor(mx, off));
-    }
-    const float qn = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
-    if constexpr (QI8) {
-      const float t = mx > 0.0f ? mx / 127.0f : 1.0f;
-      float ee = 0.0f;
-#pragma unroll
-      for (int i = 0; i < DIM / 64; ++i) {
-        const float d = v[i] - t * fminf(fmaxf(rintf(v[i] / t), -127.0f), 127.0f);
-        ee += d * d;
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) ee += __shfl_xor(ee, off);
-      if (lane == 0) {
-        qscale[q] = t;
-        qerr[q] = sqrtf(ee) * (1.0f + 1.0f / 4096.0f) + qn * (1.0f / 1048576.0f);
-      }
-    }
-    if (lane == 0) qnorm[q] = qn;
   }
-  if constexpr (QI8) __syncthreads();
-  for (int e = threadIdx.x; e < KSTEPS * 2 * kQB; e += kThreads) {
-    const int q = e & (kQB - 1);
-    const int sh = e >> 6;
-    const int hh = sh & 1;
-    const int s = sh >> 1;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if constexpr (QI8) {
-      if (q < nq) {
-        const int off = 128 * (s >> 2) + 64 * hh + 16 * (s & 3);
-        const float t = qscale[q];
-        uint32_t w[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          uint32_t pk = 0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const float x = (float)__builtin_bit_cast(
-                _Float16, queries[(size_t)q * DIM + off + 4 * d + b]);
-            const int qi = (int)fminf(fmaxf(rintf(x / t), -127.0f), 127.0f);
-            pk |= ((uint32_t)qi & 0xffu) << (8 * b);
-          }
-          w[d] = pk;
-        }
-        v = u32x4{w[0], w[1], w[2], w[3]};
-      }
-    } else {
-      const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
-      if (q < nq) v = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + off);
-    }
-    qimg[e] = v;
-  }
-  }
-  if (img_dma) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  } else {
-    __syncthreads();
-  }
+  __syncthreads();
   I8_STAMP(1);
   const float qn0 = qnorm[r], qn1 = qnorm[32 + r];
   float th0 = __builtin_inff(), th1 = __builtin_inff();
@@ -677,11 +521,6 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     th1 = qthr[32 + r];
     qi0 = qsel[r];
     qi1 = qsel[32 + r];
-  }
-  float qt0 = 1.0f, qt1 = 1.0f, qe0 = 0.0f, qe1 = 0.0f;
-  if constexpr (QI8) {
-    qt0 = qscale[r]; qt1 = qscale[32 + r];
-    qe0 = qerr[r]; qe1 = qerr[32 + r];
   }
 
   float s0[kLaneList], s1[kLaneList];
@@ -695,37 +534,18 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   if (t >= 0) {
     int64_t tn = -1;
     for (; t >= 0; t = tn) {
-      // static split, first pass: the next tile of the workgroup's range (LDS counter)
-      // (one lane's ds_add_rtn in asm, waited for at group GROUPS - DEPTH: the compiler's form
-      // waits lgkmcnt(0) at once, i.e. also for the tile's scalar loads)
+      // first pass: the next tile of the workgroup's range from the LDS counter (one lane's
+      // ds_add_rtn in asm, waited for at group GROUPS - DEPTH: the compiler's form waits
+      // lgkmcnt(0) at once, i.e. also for the tile's scalar loads)
       int wgot = 0;
       if constexpr (!COLLECT) {
-        if (!dyn && wg_counter) {
-          const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)wtile;
-          uint64_t saved;
-          asm volatile(
-              "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\t"
-              "ds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
-              : "=&v"(wgot), "=&s"(saved)
-              : "v"(a), "v"(1)
-              : "memory");
-        }
-      }
-      // dynamic: this tile's dequeue, in flight during the first GROUPS - DEPTH groups
-      const int ycur = ypref;
-      const bool pend = dyn && !((gone >> ycur) & 1u);
-      int vpend = 0;
-      if (pend) {
-        // one lane's returning atomic in asm: the compiler's own form (atomic optimizer) waits
-        // vmcnt(0) right after it, draining the prefetched groups; this one is waited for by
-        // hand at group GROUPS - DEPTH (16 loads issued after it)
-        const uint64_t addr = reinterpret_cast<uint64_t>(heads + 32 * ycur);
+        const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)wtile;
         uint64_t saved;
         asm volatile(
             "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\t"
-            "global_atomic_add %0, %2, %3, off sc0\n\ts_mov_b64 exec, %1"
-            : "=&v"(vpend), "=&s"(saved)
-            : "v"(addr), "v"(1)
+            "ds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
+            : "=&v"(wgot), "=&s"(saved)
+            : "v"(a), "v"(1)
             : "memory");
       }
       const u32x4* nxt = cur;
@@ -735,33 +555,16 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       int qoff = h * kQB + r;
       asm volatile("" : "+v"(qoff));
       const u32x4* qv = qimg + qoff;
-      using Acc = std::conditional_t<QI8, i32x16, f32x16>;
-      Acc acc0 = {}, acc1 = {};
+      f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
       for (int g = 0; g < GROUPS; ++g) {
         if (g == GROUPS - DEPTH) {  // the next tile, whose loads start now
-          if (dyn) {
-            if (pend) {
-              asm volatile("s_waitcnt vmcnt(16)" : "+v"(vpend)::"memory");
-              const int v = __builtin_amdgcn_readfirstlane(vpend);
-              const int64_t tt = decode(ycur, v);
-              if (tt >= 0) {
-                tn = tt;
-              } else {
-                if (tt == -1) gone |= 1u << ycur;
-                tn = steal();
-              }
-            } else {
-              tn = steal();
-            }
+          if constexpr (COLLECT) {
+            tn = t + kWaves < t_end ? t + kWaves : -1;
           } else {
-            if (COLLECT || !wg_counter) {
-              tn = t + kWaves < t_end ? t + kWaves : -1;
-            } else {
-              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wgot)::"memory");
-              const int wnext = __builtin_amdgcn_readfirstlane(wgot);
-              tn = t_begin + wnext < t_end ? t_begin + wnext : -1;
-            }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wgot)::"memory");
+            const int wnext = __builtin_amdgcn_readfirstlane(wgot);
+            tn = t_begin + wnext < t_end ? t_begin + wnext : -1;
           }
           has_next = tn >= 0;
           nxt = row_ptr(has_next ? tn : t);
@@ -788,19 +591,6 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
             buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (QI8) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int s = 4 * g + i;
-            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                __builtin_bit_cast(i32x4, a[i]), __builtin_bit_cast(i32x4, qv[s * 2 * kQB]), acc0,
-                0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                __builtin_bit_cast(i32x4, a[i]), __builtin_bit_cast(i32x4, qv[s * 2 * kQB + 32]),
-                acc1, 0, 0, 0);
-          }
-          continue;
-        } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           uint32_t c[8];  // fp16 pairs of components 0-7 (c[0..3]) and 8-15 (c[4..7])
@@ -823,7 +613,6 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
           acc0 = mfma16(f1, qv[(s + 1) * 2 * kQB], acc0);
           acc1 = mfma16(f1, qv[(s + 1) * 2 * kQB + 32], acc1);
 #endif
-        }
         }
       }
       cur = nxt;
@@ -848,15 +637,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       float mx0 = kNegInf, mx1 = kNegInf;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        if constexpr (QI8) {  // int32 dots are exact, |acc| < 2^24 converts exactly
-          x0[j] = __builtin_fmaf((float)acc0[j], sc[j] * qt0,
-                                 __builtin_fmaf(ec[j], qn0 + qe0, qe0));
-          x1[j] = __builtin_fmaf((float)acc1[j], sc[j] * qt1,
-                                 __builtin_fmaf(ec[j], qn1 + qe1, qe1));
-        } else {
-          x0[j] = __builtin_fmaf(acc0[j], sc[j], ec[j] * qn0);
-          x1[j] = __builtin_fmaf(acc1[j], sc[j], ec[j] * qn1);
-        }
+        x0[j] = __builtin_fmaf(acc0[j], sc[j], ec[j] * qn0);
+        x1[j] = __builtin_fmaf(acc1[j], sc[j], ec[j] * qn1);
         mx0 = fmaxf(mx0, x0[j]);
         mx1 = fmaxf(mx1, x1[j]);
       }
@@ -886,7 +668,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       if (__any(mx0 > s0[kLaneList - 1])) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(x0[j] > s0[kLaneList - 1])) {
+          if (!__any(x0[j] > s0[kLaneList - 1])) {
             d0 = fmaxf(d0, x0[j]);
             continue;
           }
@@ -898,7 +680,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
       if (__any(mx1 > s1[kLaneList - 1])) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(x1[j] > s1[kLaneList - 1])) {
+          if (!__any(x1[j] > s1[kLaneList - 1])) {
             d1 = fmaxf(d1, x1[j]);
             continue;
           }
@@ -963,1056 +745,20 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   I8_STAMP(3);
 }
 
-// The 64-query fragment image of dense_scan_i8_kernel (fp16 queries) and |q| rounded up, built
-// once per call into the workspace (one workgroup per 64-query block, the same thread partition
-// and summation order as the scan's in-kernel build, so the same bits): every scan workgroup then
-// copies it by LDS-DMA instead of each building its own from the query rows (round 3: ~10 us of
-// every launch at the kernel start).
-template <int DIM>
-__global__ __launch_bounds__(kThreads) void query_image_kernel(const uint16_t* __restrict__ queries,
-                                                               int nq_total, u32x4* __restrict__ img,
-                                                               float* __restrict__ qnorm_out) {
-  constexpr int KSTEPS = DIM / 16;
-  constexpr int PER = KSTEPS * 2 / (kThreads / kQB);
-  __shared__ float part[kThreads];
-  const int qb = blockIdx.x;
-  const int q0 = qb * kQB;
-  const int nq = min(kQB, nq_total - q0);
-  const int q = threadIdx.x & (kQB - 1);
-  const int sh0 = threadIdx.x >> 6;
-  u32x4 v[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int sh = sh0 + (kThreads / kQB) * i;
-    const int s = sh >> 1, hh = sh & 1;
-    const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
-    v[i] = q < nq ? *reinterpret_cast<const u32x4*>(queries + (size_t)(q0 + q) * DIM + off)
-                  : u32x4{0u, 0u, 0u, 0u};
-  }
-  u32x4* dst = img + (size_t)qb * KSTEPS * 2 * kQB;
-  float ss = 0.0f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int sh = sh0 + (kThreads / kQB) * i;
-    dst[sh * kQB + q] = v[i];
-    const half8 hv = __builtin_bit_cast(half8, v[i]);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
-  }
-  part[sh0 * kQB + q] = ss;
-  __syncthreads();
-  if (threadIdx.x < kQB) {
-    float t = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kThreads / kQB; ++j) t += part[j * kQB + threadIdx.x];
-    qnorm_out[(size_t)q0 + threadIdx.x] = sqrtf(t) * (1.0f + 1.0f / 4096.0f);
-  }
-}
-
 template <int DIM>
 constexpr int scan_i8_lds_bytes() {
   return scan_lds_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB) + kQB * 8 + kWaves * 4;
 }
 
-// Multi-block scan for calls with more than kQB queries (the all-gathered batch of a sharded
-// step: G * 64 queries over a 1/G shard). A GEMM-tiled form of dense_scan_kernel: both operands
-// are staged through LDS in 64-wide k-steps, so each corpus row is read from HBM once per
-// 256-query block (once per call up to 256 queries) instead of once per 64 queries, and the
-// per-pass fixed cost (query image, workgroup merge, launch) is paid once.
-//   workgroup = (256-query block qb, contiguous row range rp); 8 waves as 4 (query groups of 64)
-//   x 2 (row groups of 64) over a 128-row tile; per wave 2 x 2 v_mfma_f32_32x32x16_f16 tiles
-//   (A = corpus rows, B = queries: the lane holds one query column, as in dense_scan_kernel, so
-//   the epilogue and the 4-deep lane lists are the same). LDS: double-buffered [rows][64+8] and
-//   [queries][64+8] fp16 images (144-B rows: conflict-free ds_read_b128), register-staged two
-//   k-steps ahead (two register sets), one barrier per k-step.
-//   The two query blocks of a 512-query call stream the same row range on one XCD (workgroup
-//   ids i and i+8), so the second read of each row tile can hit that XCD's L2.
-//   Output: per (rp, query) the 16 entries of the two row groups' lane lists, sorted: the
-//   candidate layout dense_merge_kernel reads (n_wg = number of row ranges).
+// Multi-block scan for calls with more than 2 * kQB queries (the all-gathered batch of a sharded
+// step: G * 64 queries over a 1/G shard): dense_gemm_scan_w4_kernel below. Corpus rows are read
+// from HBM once per 256-query block; the output is the candidate layout dense_merge_kernel reads
+// (n_wg = number of row ranges). Round 1-2 forms (register-staged, eight-wave LDS-DMA, phase
+// pipelined) and the round-3 16x16x32 form were measured slower and removed in round 4
+// (profiles/r02_w4_scan_ab.txt, r02_p8_scan_ab.txt).
 constexpr int kGQB = 256;           // queries per block
-constexpr int kGRT = 128;           // rows per tile iteration
-constexpr int kGStride = 64 + 8;    // LDS row stride (halves)
-constexpr int kGStage = (kGRT + kGQB) * kGStride;  // halves per LDS stage
-constexpr int kGThreads = kThreads;
-constexpr int kGChunks = (kGRT + kGQB) * 8 / kGThreads;  // 16-B staging chunks per thread
-
-template <int DIM>
-__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_kernel(
-    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
-    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
-    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
-  constexpr int KT = DIM / 64;  // k-steps per row tile
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][kGStage]
-
-  // workgroup -> (query block, row range); ids i and i+8 share a row range (same XCD)
-  const int id = blockIdx.x;
-  int qb, rp;
-  if (n_qb == 2) {
-    qb = (id >> 3) & 1;
-    rp = (id >> 4) * 8 + (id & 7);
-  } else {
-    qb = id % n_qb;
-    rp = id / n_qb;
-  }
-  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
-  const int64_t lo = (int64_t)rp * rows_per_range;
-  const int64_t hi = min(lo + rows_per_range, n_rows);
-  const int q_base = qb * kGQB;
-
-  const int tid = threadIdx.x;
-  const int wave = armi::wave_id();
-  const int lane = tid & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int wq = wave & 3;   // query group: queries wq*64 + qt*32 + r
-  const int wr = wave >> 2;  // row group: rows wr*64 + rt*32 + ...
-
-  float s0[kLaneList], s1[kLaneList];
-  int32_t i0[kLaneList], i1[kLaneList];
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
-  }
-  float d0 = kNegInf, d1 = kNegInf;
-
-  // Branch-free staging loads (clamped addresses, nothing consumes them before the store): the compiler can
-  // count them, so storing k-step s+1 waits only for its own loads (vmcnt(6)) and the k-step s+2
-  // loads issued after them stay in flight across the MFMAs and the barrier.
-  static_assert(kGRT * 8 == 2 * kGThreads && kGQB * 8 == 4 * kGThreads, "staging split");
-  auto load_stage = [&](int64_t st, u32x4 (&reg)[kGChunks]) {
-    const int64_t tn = st / KT;
-    const int t = (int)(st - tn * KT);
-    const int64_t row0 = lo + tn * kGRT;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {  // 128 rows x 8 chunks
-      const int e = tid + c * kGThreads;
-      const int64_t row = min(row0 + (e >> 3), n_rows - 1);
-      reg[c] = *reinterpret_cast<const u32x4*>(rows + row * DIM + 64 * t + 8 * (e & 7));
-    }
-#pragma unroll
-    for (int c = 2; c < kGChunks; ++c) {  // 256 queries x 8 chunks
-      const int e = tid + c * kGThreads;
-      // query columns past nq load a copy of the last query: their scores are never emitted
-      const int q = min(q_base + (e >> 3) - kGRT, nq - 1);
-      reg[c] = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 64 * t + 8 * (e & 7));
-    }
-  };
-  auto store_stage = [&](int buf, const u32x4 (&reg)[kGChunks]) {
-    uint16_t* st = lds + buf * kGStage;
-#pragma unroll
-    for (int c = 0; c < kGChunks; ++c) {
-      const int e = tid + c * kGThreads;
-      const int rr = e >> 3, ch = e & 7;
-      *reinterpret_cast<u32x4*>(st + rr * kGStride + 8 * ch) = reg[c];
-    }
-  };
-
-  const int64_t n_tiles = (hi - lo + kGRT - 1) / kGRT;
-  const int64_t n_steps = n_tiles * KT;
-  f32x16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};  // [row tile][query tile]
-  // one k-step from LDS buffer buf; the row tile's epilogue after its last k-step
-  auto compute = [&](int64_t st, int buf) {
-    const int64_t tile = st / KT;
-    const int t = (int)(st - tile * KT);
-    const uint16_t* xs = lds + buf * kGStage + (wr * 64 + r) * kGStride + 8 * h;
-    const uint16_t* qs = lds + buf * kGStage + (kGRT + wq * 64 + r) * kGStride + 8 * h;
-#pragma unroll
-    for (int sub = 0; sub < 4; ++sub) {
-      const u32x4 a0 = *reinterpret_cast<const u32x4*>(xs + 16 * sub);
-      const u32x4 a1 = *reinterpret_cast<const u32x4*>(xs + 32 * kGStride + 16 * sub);
-      const u32x4 b0 = *reinterpret_cast<const u32x4*>(qs + 16 * sub);
-      const u32x4 b1 = *reinterpret_cast<const u32x4*>(qs + 32 * kGStride + 16 * sub);
-      acc00 = mfma16(a0, b0, acc00);
-      acc01 = mfma16(a0, b1, acc01);
-      acc10 = mfma16(a1, b0, acc10);
-      acc11 = mfma16(a1, b1, acc11);
-    }
-    if (t != KT - 1) return;
-    // epilogue of the row tile: lane holds rows (j&3)+8(j>>2)+4h of each 32-row tile
-    const int64_t row0 = lo + tile * kGRT + wr * 64;
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int64_t rb = row0 + rt * 32;
-      float inv[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t rr = rb + 8 * g + 4 * h + e;
-          inv[4 * g + e] = rr < hi ? inv_norm32[rr] : __builtin_nanf("");
-        }
-      }
-      uint32_t mbits = 0xffffffffu;
-      if (row_mask) mbits = rb < hi ? (uint32_t)(row_mask[rb >> 6] >> (rb & 63)) : 0u;
-      const f32x16& x0 = rt == 0 ? acc00 : acc10;
-      const f32x16& x1 = rt == 0 ? acc01 : acc11;
-      const int32_t rbase = (int32_t)rb + 4 * h;
-      float y0[16], y1[16];
-      float mx0 = kNegInf, mx1 = kNegInf;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int rt_in = (j & 3) + 8 * (j >> 2) + 4 * h;
-        const float a0 = x0[j] * inv[j];
-        const float a1 = x1[j] * inv[j];
-        const bool ok = ((mbits >> rt_in) & 1u) && (a0 == a0) && (a1 == a1);
-        y0[j] = ok ? a0 : kNegInf;
-        y1[j] = ok ? a1 : kNegInf;
-        mx0 = fmaxf(mx0, y0[j]);
-        mx1 = fmaxf(mx1, y1[j]);
-      }
-      if (__any(mx0 > s0[kLaneList - 1])) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(y0[j] > s0[kLaneList - 1])) {
-            d0 = fmaxf(d0, y0[j]);  // = topm_insert of a value no lane list takes
-            continue;
-          }
-          topm_insert<kLaneList>(y0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
-        }
-      } else {
-        d0 = fmaxf(d0, mx0);
-      }
-      if (__any(mx1 > s1[kLaneList - 1])) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(y1[j] > s1[kLaneList - 1])) {
-            d1 = fmaxf(d1, y1[j]);  // = topm_insert of a value no lane list takes
-            continue;
-          }
-          topm_insert<kLaneList>(y1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
-        }
-      } else {
-        d1 = fmaxf(d1, mx1);
-      }
-    }
-    acc00 = f32x16{}; acc01 = f32x16{}; acc10 = f32x16{}; acc11 = f32x16{};
-  };
-  if (n_steps > 0) {
-    // k-step s lives in LDS buffer s & 1. Step s: store the registers of s+1 (loaded during step
-    // s-1, so their wait is a whole step old), load s+2 into the same registers, MFMAs of s,
-    // epilogue, barrier. One register set; every load has the MFMA phase of a step to land.
-    u32x4 reg[kGChunks];
-    load_stage(0, reg);
-    store_stage(0, reg);
-    if (n_steps > 1) load_stage(1, reg);
-    __syncthreads();
-    for (int64_t st = 0; st < n_steps; ++st) {
-      const int buf = (int)(st & 1);
-      if (st + 1 < n_steps) store_stage(buf ^ 1, reg);
-      if (st + 2 < n_steps) load_stage(st + 2, reg);
-      compute(st, buf);
-      __syncthreads();
-    }
-  }
-
-  // workgroup lists: per query the 16 entries of (row group, lane half, 4), sorted
-  __syncthreads();
-  float* lkey = reinterpret_cast<float*>(smem);                          // [256][16]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);      // [256][16]
-  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);         // [256][4]
-  {
-    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
-    const int slot = (wr * 2 + h) * kLaneList;
-#pragma unroll
-    for (int j = 0; j < kLaneList; ++j) {
-      lkey[qa * 16 + slot + j] = s0[j];
-      lrow[qa * 16 + slot + j] = i0[j];
-      lkey[qc * 16 + slot + j] = s1[j];
-      lrow[qc * 16 + slot + j] = i1[j];
-    }
-    ldisc[qa * 4 + wr * 2 + h] = d0;
-    ldisc[qc * 4 + wr * 2 + h] = d1;
-  }
-  __syncthreads();
-  // each wave sorts 4 queries (16 lanes each) per round, 8 rounds
-  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
-    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
-    float key = lkey[ql * 16 + (lane & 15)];
-    int32_t row = lrow[ql * 16 + (lane & 15)];
-#pragma unroll
-    for (int size = 2; size <= 16; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const float ok = __shfl_xor(key, stride);
-        const int32_t orow = __shfl_xor(row, stride);
-        const bool lower = (lane & stride) == 0;
-        const bool desc = (lane & size) == 0;
-        const bool other_better = armi::approx_better(ok, orow, key, row);
-        const bool take_other = (lower == desc) ? other_better : !other_better;
-        if (take_other) { key = ok; row = orow; }
-      }
-    }
-    // 16-lane segments with (lane & 16) == 0 end descending, the others ascending
-    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
-    const int qg = q_base + ql;
-    if (qg < nq) {
-      const size_t base = (size_t)rp * nq + qg;
-      cand_key[base * kKW + rank] = key;
-      cand_row[base * kKW + rank] = row;
-      if (rank == 0) {
-        const float* dd = ldisc + ql * 4;
-        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
-      }
-    }
-  }
-}
-
-template <int DIM>
-constexpr size_t gemm_scan_lds_bytes() {
-  constexpr size_t stages = (size_t)2 * kGStage * 2;
-  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
-  return stages > lists ? stages : lists;
-}
-
-// LDS-DMA tiled scan (the default form of the multi-block scan; the register-staged
-// dense_gemm_scan_kernel above is kept for A/B, ARMI_GEMM_STAGE=reg). Same output layout.
-//   workgroup = (256-query block, row range); tile = 256 rows x 256 queries; 8 waves as
-//   2 (row groups of 128) x 4 (query groups of 64); per wave 4 x 2 v_mfma_f32_32x32x16_f16
-//   accumulators (128 VGPRs). The bigger tile halves the staged bytes per MFMA of the 128-row
-//   form: per 32-wide k-step a stage is 32 KB for 256 MFMAs per workgroup.
-//   Staging is global_load_lds_dwordx4 straight into four LDS stages ([256 rows][32] +
-//   [256 queries][32] fp16 images with 64-B rows, plus [8 waves][64] fp32 inverse norms), so
-//   three k-steps are in flight across each barrier (~100 KB per CU) and no VGPRs or ds_write
-//   pass are spent on staging. A wave-instruction writes 1 KB = 16 image rows lane-linearly;
-//   chunk c (16 B) of image row ir sits in slot c ^ ((ir >> 2) & 3): the swizzle is applied to
-//   the lanes' global source addresses and puts every ds_read_b128 lane group of the fragment
-//   reads on 16 distinct 16-B bank slots.
-//   Per k-step s (raw s_barrier, counted vmcnt, never vmcnt(0) in steady state): issue stage
-//   s+3 into buffer (s+3)%4 (last read in step s-1, before the previous barrier) -> MFMAs of
-//   stage s (+ the tile epilogue after its last k-step) -> vmcnt(10) retires this wave's stage
-//   s+1 -> barrier.
+constexpr int kGRT = 128;           // smallest row range of the plan
 constexpr int kG2Rows = 256;  // rows per tile
-// Geometry per k-step width KS (32: four stages, three in flight; 64: two stages of full 128-B
-// row segments, one in flight).
-template <int KS>
-struct G2 {
-  static constexpr int Img = (kG2Rows + kGQB) * KS * 2;           // image bytes per stage
-  static constexpr int StageBytes = Img + kWaves * 64 * 4;         // + inverse norms
-  static constexpr int Stages = KS == 32 ? 4 : 2;
-  static constexpr int Ahead = Stages - 1;                         // stages issued ahead
-  static constexpr int RowsPerPiece = 1024 / (KS * 2);             // image rows per 1-KB piece
-  static constexpr int Pieces = (kG2Rows + kGQB) / RowsPerPiece / kWaves;  // per wave: 4 / 8
-  static constexpr int Chunks = KS / 8;                            // 16-B chunks per image row
-  static constexpr int SwzShift = KS == 32 ? 2 : 1;
-  static constexpr int Subs = KS / 16;
-};
-static_assert(G2<32>::Pieces == 4 && G2<64>::Pieces == 8, "vmcnt counts below");
-
-template <int DIM, int KS>
-constexpr size_t gemm_glds_lds_bytes() {
-  constexpr size_t stages = (size_t)G2<KS>::Stages * G2<KS>::StageBytes;
-  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
-  return stages > lists ? stages : lists;
-}
-
-
-// ABL: the diagnostic instantiation that honours `ablate`; the production one (ABL = false)
-// compiles the switches out, so no branch sits between the MFMAs.
-template <int DIM, int KS, bool ABL>
-__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_glds_kernel(
-    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
-    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
-    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard, int ablate) {
-  using GG = G2<KS>;
-  constexpr int KT = DIM / KS;  // k-steps per row tile
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int id = blockIdx.x;
-  int qb, rp;
-  if (n_qb == 2) {
-    qb = (id >> 3) & 1;
-    rp = (id >> 4) * 8 + (id & 7);
-  } else {
-    qb = id % n_qb;
-    rp = id / n_qb;
-  }
-  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
-  const int64_t lo = (int64_t)rp * rows_per_range;
-  const int64_t hi = min(lo + rows_per_range, n_rows);
-  const int q_base = qb * kGQB;
-
-  const int tid = threadIdx.x;
-  const int wave = armi::wave_id();
-  const int lane = tid & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int wq = wave & 3;   // query group: queries wq*64 + n*32 + r
-  const int wr = wave >> 2;  // row group: rows wr*128 + m*32 + ...
-  // the swizzle of every image row this lane reads (rows differ by multiples of 32)
-  const int swz = (r >> GG::SwzShift) & (GG::Chunks - 1);
-
-  float s0[kLaneList], s1[kLaneList];
-  int32_t i0[kLaneList], i1[kLaneList];
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
-  }
-  float d0 = kNegInf, d1 = kNegInf;
-
-  // Wave piece p covers image rows 16 * (p * 8 + wave) + lane / 4: pieces 0-15 are the tile's
-  // corpus rows, 16-31 the query block. Lane slot lane % 4 holds chunk (lane % 4) ^ swizzle.
-  const int pr = lane / GG::Chunks;
-  // piece p < 4 of stage st (16 image rows), p == 4: the stage's inverse norms (tile rows
-  // (wave & 3) * 64 + lane, one fp32 per lane)
-  auto issue_piece = [&](int64_t st, int p) {
-    const int64_t tn = st / KT;
-    const int t = (int)(st - tn * KT);
-    const int64_t row0 = lo + tn * kG2Rows;
-    unsigned char* base = smem + (int)(st & (GG::Stages - 1)) * GG::StageBytes;
-    if (p == GG::Pieces) {
-      const int64_t nr = min(row0 + (wave & 3) * 64 + lane, n_rows - 1);
-      __builtin_amdgcn_global_load_lds(inv_norm32 + nr, (lds_ptr_t)(base + GG::Img + wave * 256),
-                                       4, 0, 0);
-      return;
-    }
-    const int piece = p * kWaves + wave;
-    const int ir = piece * GG::RowsPerPiece + pr;
-    const int c = (lane & (GG::Chunks - 1)) ^ ((ir >> GG::SwzShift) & (GG::Chunks - 1));
-    const uint16_t* src;
-    if (ir < kG2Rows) {  // wave-uniform: pieces never straddle the row / query images
-      const int64_t row = min(((ABL && (ablate & 8)) ? lo : row0) + ir, n_rows - 1);
-      src = rows + row * DIM + KS * t + 8 * c;
-    } else {
-      const int q = min(q_base + ir - kG2Rows, nq - 1);
-      src = queries + (size_t)q * DIM + KS * t + 8 * c;
-    }
-    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(base + piece * 1024), 16, 0, 0);
-  };
-  auto issue_stage = [&](int64_t st) {
-#pragma unroll
-    for (int p = 0; p <= GG::Pieces; ++p) issue_piece(st, p);
-  };
-
-  const int64_t n_tiles = (hi - lo + kG2Rows - 1) / kG2Rows;
-  const int64_t n_steps = n_tiles * KT;
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) { acc[m][0] = f32x16{}; acc[m][1] = f32x16{}; }
-
-  auto epilogue = [&](int64_t tile, const unsigned char* base) {
-    const int64_t row0 = lo + tile * kG2Rows + wr * 128;
-    const bool full = lo + (tile + 1) * kG2Rows <= hi;  // workgroup-uniform
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      // Inverse norms by inline asm: for a plain LDS read hipcc cannot tell the in-flight
-      // LDS-DMA writes of the other stages apart and emits vmcnt(0), draining the pipeline once
-      // per tile. This stage was retired by the vmcnt + barrier before this step.
-      const uint32_t linv = (uint32_t)(uintptr_t)(lds_ptr_t)(
-          base + GG::Img + (wr * 2 + (m >> 1)) * 256 + ((m & 1) * 32 + 4 * h) * 4);
-      u32x4 invw[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      const int64_t rb = row0 + m * 32;
-      float inv[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        inv[4 * g + 0] = __uint_as_float(invw[g].x);
-        inv[4 * g + 1] = __uint_as_float(invw[g].y);
-        inv[4 * g + 2] = __uint_as_float(invw[g].z);
-        inv[4 * g + 3] = __uint_as_float(invw[g].w);
-      }
-      // Rows past the range and rows the filter drops get a NaN scale. A NaN score never enters
-      // a lane list (x > s is false), and fmaxf ignores it in the maxima and the bound: the
-      // same lists and bounds as a -inf score, without per-score tests on full tiles.
-      if (!full) {
-        const int lim = (int)max<int64_t>(0, min<int64_t>(32, hi - rb));
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if ((j & 3) + 8 * (j >> 2) + 4 * h >= lim) inv[j] = __builtin_nanf("");
-      }
-      if (row_mask) {
-        const uint32_t mbits = rb < hi ? (uint32_t)(row_mask[rb >> 6] >> (rb & 63)) : 0u;
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (!((mbits >> ((j & 3) + 8 * (j >> 2) + 4 * h)) & 1u)) inv[j] = __builtin_nanf("");
-      }
-      const int32_t rbase = (int32_t)rb + 4 * h;
-      float y0[16], y1[16];
-      float mx0 = kNegInf, mx1 = kNegInf;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        y0[j] = acc[m][0][j] * inv[j];
-        y1[j] = acc[m][1][j] * inv[j];
-        mx0 = fmaxf(mx0, y0[j]);
-        mx1 = fmaxf(mx1, y1[j]);
-      }
-      if (__any(mx0 > s0[kLaneList - 1])) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(y0[j] > s0[kLaneList - 1])) {
-            d0 = fmaxf(d0, y0[j]);  // = topm_insert of a value no lane list takes
-            continue;
-          }
-          topm_insert<kLaneList>(y0[j], rbase + (j & 3) + 8 * (j >> 2), s0, i0, d0);
-        }
-      } else {
-        d0 = fmaxf(d0, mx0);
-      }
-      if (__any(mx1 > s1[kLaneList - 1])) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(y1[j] > s1[kLaneList - 1])) {
-            d1 = fmaxf(d1, y1[j]);
-            continue;
-          }
-          topm_insert<kLaneList>(y1[j], rbase + (j & 3) + 8 * (j >> 2), s1, i1, d1);
-        }
-      } else {
-        d1 = fmaxf(d1, mx1);
-      }
-      acc[m][0] = f32x16{};
-      acc[m][1] = f32x16{};
-    }
-  };
-
-  // MFMAs of stage st with the issue of stage st+3 (when `more`) spread between them: issuing
-  // the five LDS-DMA loads as one block after the barrier kept every wave's fragment reads and
-  // MFMAs waiting behind them.
-  auto compute = [&](int64_t st, bool more) {
-    const int64_t tile = st / KT;
-    const int t = (int)(st - tile * KT);
-    const unsigned char* base = smem + (int)(st & (GG::Stages - 1)) * GG::StageBytes;
-    const unsigned char* xs = base + (wr * 128 + r) * (KS * 2);
-    const unsigned char* qs = base + (kG2Rows + wq * 64 + r) * (KS * 2);
-    u32x4 a[2][4], b[2][2];  // fragments of sub-steps sub (cur) and sub + 1 (nxt)
-    auto load_frags = [&](int sub, u32x4 (&fa)[4], u32x4 (&fb)[2]) {
-      const int off = ((2 * sub + h) ^ swz) << 4;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-        fb[n] = *reinterpret_cast<const u32x4*>(qs + n * 32 * (KS * 2) + off);
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        fa[m] = *reinterpret_cast<const u32x4*>(xs + m * 32 * (KS * 2) + off);
-    };
-    load_frags(0, a[0], b[0]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int sub = 0; sub < GG::Subs; ++sub) {
-      const int cur = sub & 1;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        if (ABL && (ablate & 32)) {
-          asm volatile("" :: "v"(a[cur][m]), "v"(b[cur][0]), "v"(b[cur][1]));
-        } else {
-#pragma unroll
-          for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(a[cur][m], b[cur][n], acc[m][n]);
-        }
-        const int p = sub * 4 + m;  // the next stage's loads, spread between the MFMAs
-        if (p <= GG::Pieces && more) issue_piece(st + GG::Ahead, p);
-        if (m == 1 && sub + 1 < GG::Subs) load_frags(sub + 1, a[cur ^ 1], b[cur ^ 1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (GG::Subs * 4 <= GG::Pieces && more) issue_piece(st + GG::Ahead, GG::Pieces);
-    if (t == KT - 1) epilogue(tile, base);
-  };
-
-  // vmcnt for "retire the oldest outstanding stage, leave `later` younger ones in flight"
-  auto wait_stage = [&](int64_t later) {
-    if constexpr (KS == 32) {
-      if (later >= 2) {
-        asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-      } else if (later == 1) {
-        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      }
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-  };
-  // Stages past the last k-step are issued too: their rows / queries are clamped in-bounds and
-  // land in the buffer of the step before (read before the previous barrier), nobody reads them,
-  // and every wait keeps the same count, so the k-step loop carries no issue branches.
-  if (n_steps > 0) {
-#pragma unroll
-    for (int j = 0; j < GG::Ahead; ++j) issue_stage(j);
-    wait_stage(GG::Ahead - 1);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    for (int64_t st = 0; st < n_steps; ++st) {
-      compute(st, true);
-      // retire stage st+1: the stages issued after it stay in flight
-      const int64_t later = GG::Ahead - 1;
-      if (ABL && (ablate & 16)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      } else {
-        wait_stage(later);
-      }
-      if (!(ABL && (ablate & 64))) __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  }
-
-  // workgroup lists: per query the 16 entries of (row group, lane half, 4), sorted (the layout
-  // of dense_gemm_scan_kernel). The tail stages' LDS-DMA writes must land before the stage
-  // buffers are reused.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
-  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);      // [256][4]
-  {
-    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
-    const int slot = (wr * 2 + h) * kLaneList;
-#pragma unroll
-    for (int j = 0; j < kLaneList; ++j) {
-      lkey[qa * 16 + slot + j] = s0[j];
-      lrow[qa * 16 + slot + j] = i0[j];
-      lkey[qc * 16 + slot + j] = s1[j];
-      lrow[qc * 16 + slot + j] = i1[j];
-    }
-    ldisc[qa * 4 + wr * 2 + h] = d0;
-    ldisc[qc * 4 + wr * 2 + h] = d1;
-  }
-  __syncthreads();
-  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
-    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
-    float key = lkey[ql * 16 + (lane & 15)];
-    int32_t row = lrow[ql * 16 + (lane & 15)];
-#pragma unroll
-    for (int size = 2; size <= 16; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const float ok = __shfl_xor(key, stride);
-        const int32_t orow = __shfl_xor(row, stride);
-        const bool lower = (lane & stride) == 0;
-        const bool desc = (lane & size) == 0;
-        const bool other_better = armi::approx_better(ok, orow, key, row);
-        const bool take_other = (lower == desc) ? other_better : !other_better;
-        if (take_other) { key = ok; row = orow; }
-      }
-    }
-    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
-    const int qg = q_base + ql;
-    if (qg < nq) {
-      const size_t base = (size_t)rp * nq + qg;
-      cand_key[base * kKW + rank] = key;
-      cand_row[base * kKW + rank] = row;
-      if (rank == 0) {
-        const float* dd = ldisc + ql * 4;
-        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
-      }
-    }
-  }
-}
-
-
-// Phase-pipelined tiled scan (ARMI_GEMM_FORM=p8; measured slower than the four-stage kernel
-// above, which stays the default: see DESIGN.md §7 and profiles/r02_p8_scan_ab.txt). Same tile (256 rows x 256 queries), same wave geometry
-// (2 row groups of 128 x 4 query groups of 64, waves w and w + 4 on one SIMD) and the same
-// candidate output as dense_gemm_scan_glds_kernel, a different schedule:
-//   * a K-tile is 64 deep; the wave's 128 x 64 output is cut into four QUADRANTS, visited in
-//     snake order q = (rows 0-63, queries 0-31), (0-63, 32-63), (64-127, 32-63), (64-127, 0-31),
-//     so consecutive quadrants share one operand (kept in registers); one PHASE = one quadrant x
-//     the K-tile = 8 v_mfma_f32_32x32x16_f16 (2 row tiles x 4 k-steps);
-//   * each phase of a wave is LOAD (LDS-DMA issue of one 16-KB piece of a later K-tile, the
-//     quadrant's new fragments: 12 / 4 / 8 / 4 ds_read_b128, lgkmcnt(0)) -> s_barrier -> MATH ->
-//     s_barrier, and waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MATH
-//     runs while its partner's LOAD runs;
-//   * the LDS holds two K-tiles of four 16-KB pieces, 128 image rows x 128 B (k 0-63: every
-//     LDS-DMA instruction moves 8 whole 128-B lines): PA0 = the rows 0-63 of both row groups,
-//     PB0 = the queries 0-31 of every query group, PA1 = rows 64-127, PB1 = queries 32-63; 16-B
-//     chunk c of image row ir sits in slot c ^ ((ir >> 1) & 7) (conflict-free ds_read_b128). A
-//     piece is last read in phase 0 (PA0), 1 (PB1), 2 (PA1) or 3 (PB0) of its K-tile, and the
-//     same piece of the K-tile two ahead is issued in the next phase (7, 7, 7 and 4 phases
-//     before its first reader); a constant vmcnt(6) per phase retires it in time;
-//   * the epilogue of each quadrant (inverse norms from an LDS copy, NaN masking, lane-list
-//     insertion) runs in the LOAD segment after the quadrant's last MFMAs, beside the partner's
-//     MATH.
-constexpr int kP8Piece = 16384;            // bytes per piece (128 image rows x 128 B)
-constexpr int kP8Buf = 4 * kP8Piece;       // one K-tile
-constexpr int kP8Lds = 2 * kP8Buf;         // two K-tiles (128 KB)
-
-template <int DIM>
-constexpr size_t gemm_p8_lds_bytes() {
-  constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
-  return kP8Lds + 2048 > lists ? (size_t)kP8Lds + 2048 : lists;
-}
-
-// ABL: diagnostic ablations, compiled only into a probe build (-DARMI_PROBE_BUILD, results
-// wrong): 1 no vmcnt wait, 2 every row piece re-reads the range's first row tile (L2 hits),
-// 4 no MFMAs, 8 no barriers in the phase loop. The shipped instantiation is ABL = 0.
-template <int DIM, int ABL>
-__global__ __launch_bounds__(kGThreads) void dense_gemm_scan_p8_kernel(
-    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
-    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
-    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
-  constexpr int KT = DIM / 64;  // K-tiles per row tile
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int id = blockIdx.x;
-  int qb, rp;
-  if (n_qb == 2) {
-    qb = (id >> 3) & 1;
-    rp = (id >> 4) * 8 + (id & 7);
-  } else {
-    qb = id % n_qb;
-    rp = id / n_qb;
-  }
-  if (rp >= n_ranges) return;  // workgroup-uniform, before any barrier
-  const int64_t lo = (int64_t)rp * rows_per_range;
-  const int64_t hi = min(lo + rows_per_range, n_rows);
-  const int q_base = qb * kGQB;
-  // 32-bit row offsets from here on: the range's rows, its pointers and its limits
-  const int n_here = (int)(hi - lo);                  // rows of this range
-  const int last_row = (int)(n_rows - 1 - lo);        // last valid row offset (clamp target)
-  const uint16_t* __restrict__ rows_r = rows + lo * DIM;
-  const float* __restrict__ inv_r = inv_norm32 + lo;
-  const int last4 = (int)(((n_rows + 31) / 32) * 32 - 4 - lo);  // last 16-B group of the norms
-
-  const int tid = threadIdx.x;
-  const int wave = armi::wave_id();
-  const int lane = tid & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int wq = wave & 3;   // query group: queries wq*64 + n*32 + r
-  const int wr = wave >> 2;  // row group: rows wr*128 + m*32 + ...
-
-  float s0[kLaneList], s1[kLaneList];
-  int32_t i0[kLaneList], i1[kLaneList];
-#pragma unroll
-  for (int j = 0; j < kLaneList; ++j) {
-    s0[j] = kNegInf; s1[j] = kNegInf; i0[j] = -1; i1[j] = -1;
-  }
-  float d0 = kNegInf, d1 = kNegInf;
-
-  const int n_tiles = (n_here + kG2Rows - 1) / kG2Rows;
-
-  // Piece x in {PA0, PB0, PA1, PB1} of K-tile (tile, kt), into buffer `buf`. This wave's two
-  // 1-KB instructions cover image rows 16 * wave + [0, 16): lane slot lane % 8 of image row
-  // ir holds chunk (lane % 8) ^ ((ir >> 1) & 7). The per-lane source offsets are fixed per piece
-  // type and instruction (8 VGPRs, bytes from a wave-uniform base), so an issue is one
-  // LDS-DMA and a scalar base; the last row tile of the range (and the clamped tiles past it,
-  // issued into the free buffer and never read) clamps its rows to the store instead.
-  uint32_t off_a[2][2], off_b[2][2];  // [x >> 1][instruction]
-  int tr_a[2][2];
-#pragma unroll
-  for (int hx = 0; hx < 2; ++hx)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int ir = 16 * wave + 8 * i + (lane >> 3);
-      const int c = (lane & 7) ^ ((ir >> 1) & 7);
-      tr_a[hx][i] = (ir >> 6) * 128 + hx * 64 + (ir & 63);  // row of the tile
-      off_a[hx][i] = (uint32_t)(tr_a[hx][i] * DIM * 2 + c * 16);
-      const int q = min(q_base + (ir >> 5) * 64 + hx * 32 + (ir & 31), nq - 1);
-      off_b[hx][i] = (uint32_t)((q - q_base) * DIM * 2 + c * 16);
-    }
-  const unsigned char* __restrict__ qsrc =
-      reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
-  const unsigned char* __restrict__ rsrc = reinterpret_cast<const unsigned char*>(rows_r);
-  const int full_tiles = n_here / kG2Rows;  // tiles whose 256 rows are all inside the store
-  auto issue_piece = [&](int tile, int kt, int buf, auto X) {
-    constexpr int x = decltype(X)::value;
-    constexpr int hx = x >> 1;
-    unsigned char* base = smem + buf * kP8Buf + x * kP8Piece + wave * 2048;
-    if constexpr ((x & 1) == 0) {
-      if (tile < full_tiles && tile * kG2Rows + kG2Rows - 1 <= last_row) {
-        const unsigned char* tb = rsrc + ((size_t)tile * kG2Rows * DIM + kt * 64) * 2;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          __builtin_amdgcn_global_load_lds(tb + off_a[hx][i], (lds_ptr_t)(base + i * 1024), 16, 0,
-                                           0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int row = min(tile * kG2Rows + tr_a[hx][i], last_row);
-          const uint32_t c16 = off_a[hx][i] & 127u;
-          __builtin_amdgcn_global_load_lds(rsrc + ((size_t)row * DIM + kt * 64) * 2 + c16,
-                                           (lds_ptr_t)(base + i * 1024), 16, 0, 0);
-        }
-      }
-    } else {
-      const unsigned char* tb = qsrc + kt * 64 * 2;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds(tb + off_b[hx][i], (lds_ptr_t)(base + i * 1024), 16, 0, 0);
-    }
-  };
-  // Inverse norms of row tile `tile` -> LDS [kP8Lds + (tile & 1) KB]: one 1-KB LDS-DMA by wave 0
-  // (its later vmcnt waits then cover one instruction more: a slightly earlier retire, never a
-  // missed one). Clamped to the padded norm array; rows past the range are masked anyway.
-  auto issue_norms = [&](int tile) {
-    if (wave == 0) {
-      const int rr = min(tile * kG2Rows + 4 * lane, last4);
-      __builtin_amdgcn_global_load_lds(inv_r + rr,
-                                       (lds_ptr_t)(smem + kP8Lds + (tile & 1) * 1024), 16, 0, 0);
-    }
-  };
-
-  if constexpr (ABL & 1024) {
-    // an AGPR operand anywhere in the kernel makes hipcc select the AGPR form of the MFMAs
-    // (accumulators in AccVGPRs) instead of the ArchVGPR form it picks for <= 256 registers
-    int zero = 0;
-    asm volatile("; agpr-form hint %0" ::"a"(zero));
-  }
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) { acc[m][0] = f32x16{}; acc[m][1] = f32x16{}; }
-
-  // Epilogue of quadrant Q (row tiles 2 mh, 2 mh + 1 x query tile nh of the wave) of `tile`.
-  auto epilogue = [&](int tile, auto Q) {
-    constexpr int q = decltype(Q)::value;
-    constexpr int mh = q >> 1;
-    constexpr int nh = (q == 1 || q == 2) ? 1 : 0;
-#pragma unroll
-    for (int mm = 0; mm < 2; ++mm) {
-      const int m = 2 * mh + mm;
-      const int ro = tile * kG2Rows + wr * 128 + m * 32;  // row offset of the 32-row block
-      const int64_t rb = lo + ro;
-      // inverse norms of rows ro + (j & 3) + 8 (j >> 2) + 4 h from the tile's LDS copy; by inline
-      // asm, else hipcc cannot tell them from the in-flight LDS-DMA and drains it (vmcnt(0))
-      const uint32_t linv = (uint32_t)(uintptr_t)(lds_ptr_t)(
-          smem + kP8Lds + (tile & 1) * 1024 + (wr * 128 + m * 32 + 4 * h) * 4);
-      u32x4 invw[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
-      // valid rows of the block (wave-uniform bits): inside the range and kept by the filter
-      uint32_t valid = ro + 32 <= n_here ? 0xffffffffu
-                                         : (ro >= n_here ? 0u : (1u << (n_here - ro)) - 1u);
-      if (row_mask) valid &= (uint32_t)(row_mask[rb >> 6] >> (rb & 63));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      float inv[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        inv[4 * g + 0] = __uint_as_float(invw[g].x);
-        inv[4 * g + 1] = __uint_as_float(invw[g].y);
-        inv[4 * g + 2] = __uint_as_float(invw[g].z);
-        inv[4 * g + 3] = __uint_as_float(invw[g].w);
-      }
-      // invalid rows get a NaN scale: a NaN score never enters a lane list and fmaxf ignores it
-      if (valid != 0xffffffffu) {
-        const uint32_t vb = valid >> (4 * h);
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (!((vb >> ((j & 3) + 8 * (j >> 2))) & 1u)) inv[j] = __builtin_nanf("");
-      }
-      // opaque: keeps hipcc from hoisting the 16 row ids of every block out of the phase loop
-      // (they would stay live across all K-tiles and spill)
-      int32_t rbase = (int32_t)rb + 4 * h;
-      asm volatile("" : "+v"(rbase));
-      f32x16& c = mm ? acc[2 * mh + 1][nh] : acc[2 * mh][nh];
-      float* sl = nh ? s1 : s0;
-      int32_t* il = nh ? i1 : i0;
-      float& dl = nh ? d1 : d0;
-      float y[16];
-      float mx = kNegInf;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        y[j] = c[j] * inv[j];
-        mx = fmaxf(mx, y[j]);
-      }
-      if (__any(mx > sl[kLaneList - 1])) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (guard && !__any(y[j] > sl[kLaneList - 1])) {
-            dl = fmaxf(dl, y[j]);  // = topm_insert of a value no lane list takes
-            continue;
-          }
-          float v = y[j];
-          int32_t id2 = rbase + (j & 3) + 8 * (j >> 2);
-#pragma unroll
-          for (int e = 0; e < kLaneList; ++e) {
-            const bool cbt = v > sl[e];
-            const float ts = cbt ? v : sl[e];
-            const int32_t ti = cbt ? id2 : il[e];
-            v = cbt ? sl[e] : v;
-            id2 = cbt ? il[e] : id2;
-            sl[e] = ts;
-            il[e] = ti;
-          }
-          dl = fmaxf(dl, v);
-        }
-      } else {
-        dl = fmaxf(dl, mx);
-      }
-      c = f32x16{};
-    }
-  };
-
-  // Per-lane LDS addresses: image row (wr*64 + r) of an A piece / (wq*32 + r) of a B piece, and
-  // the swizzled chunk of k-step ks: 2*ks + h.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  const uint32_t a_lane = lds0 + (uint32_t)(wr * 64 + r) * 128;
-  const uint32_t b_lane = lds0 + (uint32_t)(wq * 32 + r) * 128;
-  const int swz = (r >> 1) & 7;
-  uint32_t co[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) co[ks] = (uint32_t)(((2 * ks + h) ^ swz) << 4);
-
-  u32x4 fa[2][4], fb[4];  // A: [row tile of the half][k-step], B: [k-step]
-  auto read_a = [&](uint32_t piece) {
-    const uint32_t b = a_lane + piece;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[0][ks]) : "v"(b + co[ks]));
-      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fa[1][ks]) : "v"(b + co[ks]));
-    }
-  };
-  auto read_b = [&](uint32_t piece) {
-    const uint32_t b = b_lane + piece;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fb[ks]) : "v"(b + co[ks]));
-  };
-
-  auto advance = [&](int& t, int& k) {
-    if (++k == KT) { k = 0; ++t; }
-  };
-  // One phase (quadrant j of K-tile T = (tile, kt)): LOAD -> barrier -> MATH -> barrier.
-  auto phase = [&](int T, int tile, int kt, auto J) {
-    constexpr int j = decltype(J)::value;
-    constexpr int mh = j >> 1;
-    constexpr int nh = (j == 1 || j == 2) ? 1 : 0;
-    // ---- LOAD: epilogue of the quadrant whose last MFMAs ran in the previous phase
-    if constexpr (j == 0) {
-      if (kt == 0 && tile > 0) epilogue(tile - 1, std::integral_constant<int, 3>{});
-    } else {
-      if (kt == KT - 1) epilogue(tile, std::integral_constant<int, j - 1>{});
-    }
-    {  // the piece freed by the previous phase, of the K-tile two ahead of it
-      constexpr int x = j == 0 ? 1 : (j == 1 ? 0 : (j == 2 ? 3 : 2));  // PB0, PA0, PB1, PA1
-      int t1 = tile;
-      int k1 = kt;
-      if constexpr (j != 0) advance(t1, k1);
-      advance(t1, k1);
-      if constexpr (!(ABL & 128))
-        issue_piece(t1, k1, (j == 0 ? T + 1 : T) & 1, std::integral_constant<int, x>{});
-      if constexpr (j == 1) {
-        if (kt == 0) issue_norms(tile);
-      }
-    }
-    const uint32_t buf = (uint32_t)((T & 1) * kP8Buf);
-    if constexpr (!(ABL & 256)) {
-      if constexpr (j == 0) { read_a(buf + 0 * kP8Piece); read_b(buf + 1 * kP8Piece); }
-      if constexpr (j == 1) read_b(buf + 3 * kP8Piece);
-      if constexpr (j == 2) read_a(buf + 2 * kP8Piece);
-      if constexpr (j == 3) read_b(buf + 1 * kP8Piece);
-    }
-    // retire this wave's pieces older than the 3 youngest phases and the fragment reads (so the
-    // next phase's DMA may overwrite what was read here)
-    if constexpr (ABL & 1) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
-    // ---- MATH: 2 row tiles x 1 query tile x 4 k-steps
-    if constexpr (!(ABL & 16)) __builtin_amdgcn_s_setprio(1);
-    f32x16& c0 = acc[2 * mh][nh];
-    f32x16& c1 = acc[2 * mh + 1][nh];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if constexpr (ABL & 4) {
-        asm volatile("" :: "v"(fa[0][ks]), "v"(fa[1][ks]), "v"(fb[ks]));
-      } else if constexpr (ABL & 512) {
-        mfma16_acc(c0, fa[0][ks], fb[ks]);
-        mfma16_acc(c1, fa[1][ks], fb[ks]);
-      } else {
-        c0 = mfma16(fa[0][ks], fb[ks], c0);
-        c1 = mfma16(fa[1][ks], fb[ks], c1);
-      }
-    }
-    if constexpr (!(ABL & 16)) __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  if (n_tiles > 0) {
-    {  // prologue: K-tile 0 whole, K-tile 1's PA0, PB1, PA1 (phase 0 issues its PB0)
-      int t1 = 0;
-      int k1 = 0;
-      advance(t1, k1);
-      issue_piece(0, 0, 0, std::integral_constant<int, 0>{});
-      issue_piece(0, 0, 0, std::integral_constant<int, 1>{});
-      issue_piece(0, 0, 0, std::integral_constant<int, 3>{});
-      issue_piece(0, 0, 0, std::integral_constant<int, 2>{});
-      issue_piece(t1, k1, 1, std::integral_constant<int, 0>{});
-      issue_piece(t1, k1, 1, std::integral_constant<int, 3>{});
-      issue_piece(t1, k1, 1, std::integral_constant<int, 2>{});
-    }
-    // K-tile 0's PA0 and PB0 retired: the 5 youngest pieces stay in flight
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // waves 4-7 run one barrier behind (ABL 32: the odd waves instead; ABL 64: no stagger)
-    const bool late = (ABL & 32) ? (wave & 1) : ((ABL & 64) ? false : wr != 0);
-    if (!(ABL & 8) && late) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    int T = 0;
-    for (int tile = 0; tile < n_tiles; ++tile) {
-      for (int kt = 0; kt < KT; ++kt, ++T) {
-        phase(T, tile, kt, std::integral_constant<int, 0>{});
-        phase(T, tile, kt, std::integral_constant<int, 1>{});
-        phase(T, tile, kt, std::integral_constant<int, 2>{});
-        phase(T, tile, kt, std::integral_constant<int, 3>{});
-      }
-    }
-    if (!(ABL & 8) && !(ABL & 64) && !late) __builtin_amdgcn_s_barrier();  // balance the count
-    epilogue(n_tiles - 1, std::integral_constant<int, 3>{});
-  }
-
-  // workgroup lists (as dense_gemm_scan_glds_kernel); the DMA of the clamped tail pieces must
-  // land before the stage buffers are reused
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + kGQB * 16 * 4);   // [256][16]
-  float* ldisc = reinterpret_cast<float*>(smem + kGQB * 16 * 8);      // [256][4]
-  {
-    const int qa = wq * 64 + r, qc = wq * 64 + 32 + r;
-    const int slot = (wr * 2 + h) * kLaneList;
-#pragma unroll
-    for (int j = 0; j < kLaneList; ++j) {
-      lkey[qa * 16 + slot + j] = s0[j];
-      lrow[qa * 16 + slot + j] = i0[j];
-      lkey[qc * 16 + slot + j] = s1[j];
-      lrow[qc * 16 + slot + j] = i1[j];
-    }
-    ldisc[qa * 4 + wr * 2 + h] = d0;
-    ldisc[qc * 4 + wr * 2 + h] = d1;
-  }
-  __syncthreads();
-  for (int round = 0; round < kGQB / (kWaves * 4); ++round) {
-    const int ql = (round * kWaves + wave) * 4 + (lane >> 4);
-    float key = lkey[ql * 16 + (lane & 15)];
-    int32_t row = lrow[ql * 16 + (lane & 15)];
-#pragma unroll
-    for (int size = 2; size <= 16; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const float ok = __shfl_xor(key, stride);
-        const int32_t orow = __shfl_xor(row, stride);
-        const bool lower = (lane & stride) == 0;
-        const bool desc = (lane & size) == 0;
-        const bool other_better = armi::approx_better(ok, orow, key, row);
-        const bool take_other = (lower == desc) ? other_better : !other_better;
-        if (take_other) { key = ok; row = orow; }
-      }
-    }
-    const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
-    const int qg = q_base + ql;
-    if (qg < nq) {
-      const size_t base = (size_t)rp * nq + qg;
-      cand_key[base * kKW + rank] = key;
-      cand_row[base * kKW + rank] = row;
-      if (rank == 0) {
-        const float* dd = ldisc + ql * 4;
-        cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
-      }
-    }
-  }
-}
 
 // Four-wave tiled scan: one wave per SIMD, each wave owning a 128-row x 128-query block of the
 // 256 x 256 tile (16 v_mfma_f32_32x32x16_f16 accumulators = 256 AccVGPRs), so a k-step carries
@@ -2047,7 +793,7 @@ void dense_gemm_scan_w4_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
     int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound, int guard) {
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
   constexpr int KT = DIM / 32;  // k-steps per row tile
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -2364,383 +1110,6 @@ void dense_gemm_scan_w4_kernel(
         cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
       }
     }
-  }
-}
-
-// Tiled scan on the GEMM mainloop of gemm.hip (armi_enc_linear_f16): the > 128-query form
-// (round 3, ARMI_GEMM_FORM=g8 / default once measured). Workgroup = (256-query block, row range),
-// 512 threads = 8 waves as 2 (rows, 128 each) x 4 (queries, 64 each), tiles of 256 rows x 256
-// queries, v_mfma_f32_16x16x32_f16 (lane (l & 15) = row / query of a 16-block, 8 k values per
-// lane): per wave 8 x 4 accumulator blocks, the accumulator register j of lane l is
-// D[row 4 (l >> 4) + j][query l & 15]. K-tiles of 64, four quadrant phases each, operand halves
-// staged by LDS-DMA (one half-tile per phase, >= 4 phases ahead, one counted vmcnt per K-tile;
-// see gemm.hip). The K-tile stream runs across the range's tiles, so the next tile's first
-// K-tiles are in flight during a tile's epilogue.
-// Tile epilogue (per lane and query, over its 32 rows of the tile): score = fma(acc, inv_norm,
-// bias) with (0, -FLT_MAX) for dead rows (past the range, filtered, invalid), row code pm*4 + j in
-// the 5 low mantissa bits (<= 2^-18 relative: kEncodeSlack), compare-free best-two + third chain;
-// the best two enter a 2-deep lane list, the third and every eviction the lane's discarded bound.
-// Per query 8 lanes (2 waves x 4 lane groups) x 2 entries = the workgroup's 16 candidates.
-constexpr int kG8Threads = 512;
-constexpr int kG8Img = 256 * 64 * 2;       // one operand image of a K-tile (32 KB)
-constexpr int kG8Buf = 2 * kG8Img;         // rows + queries
-constexpr int kG8Norm = 2 * kG8Buf;        // two 1-KB inverse-norm slots (tile parity)
-constexpr int kG8List = kG8Norm + 2 * 1024;  // lane lists: [qn 4][field 3][thread 512] dwords
-constexpr size_t kG8Lds = kG8List + 4 * 3 * kG8Threads * 4;
-
-struct G8Src {
-  const unsigned char* p;  // first row of the tile (scalar base)
-  int32_t last;            // last row of the store relative to the tile (clamp of the DMA rows)
-  int64_t r0;              // first row of the tile
-};
-
-template <int DIM>
-__global__ __launch_bounds__(kG8Threads) void dense_gemm_scan_g8_kernel(
-    const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
-    const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
-    int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
-  constexpr int nK = DIM / 64;
-  static_assert(nK >= 2, "the stream needs >= 2 K-tiles per tile");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int id = blockIdx.x;
-  int qb, rp;
-  if (n_qb == 2) {
-    qb = (id >> 3) & 1;
-    rp = (id >> 4) * 8 + (id & 7);
-  } else {
-    qb = id % n_qb;
-    rp = id / n_qb;
-  }
-  if (rp >= n_ranges) return;  // workgroup-uniform
-  const int64_t lo = (int64_t)rp * rows_per_range;
-  const int64_t hi = min(lo + rows_per_range, n_rows);
-  const int q_base = qb * 256;
-  const int n_tiles = (int)((hi - lo + 255) / 256);
-  const int64_t total = (int64_t)n_tiles * nK;
-  const int64_t n_pad = (n_rows + 31) / 32 * 32;  // inverse norms are padded to 32-row tiles
-
-  const int tid = threadIdx.x;
-  const int wave = armi::wave_id();
-  const int lane = tid & 63;
-  const int wp = wave >> 2;
-  const int wq = wave & 3;
-  const int prow = lane >> 3;
-  const int pchunk = (lane & 7) ^ prow;
-  // piece geometry (wave-uniform) of half h, piece jj: first image row of the 8-row piece
-  auto bp_of = [&](int h, int jj) {
-    const int i = 2 * wave + jj;
-    return i < 8 ? 64 * h + 8 * i : 128 + 64 * h + 8 * (i - 8);
-  };
-  auto bq_of = [&](int h, int jj) {
-    const int i = 2 * wave + jj;
-    return 64 * (i >> 2) + 32 * h + 8 * (i & 3);
-  };
-  const int qlast = nq - 1 - q_base;
-  const unsigned char* qsrc = reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
-  auto tile_src = [&](int j) {
-    G8Src ts;
-    ts.r0 = lo + (int64_t)j * 256;
-    ts.p = reinterpret_cast<const unsigned char*>(rows + (size_t)ts.r0 * DIM);
-    const int64_t last = n_rows - 1 - ts.r0;
-    ts.last = (int32_t)(last < 255 ? last : 255);
-    return ts;
-  };
-  G8Src cur = tile_src(0), nxt = tile_src(1);
-  // DMA offsets are formed at issue time (a few VALU) instead of held in registers
-  auto issue_half = [&](int64_t sidx, int kt_s, int d, int op, int h) {
-    if (sidx >= total) return;  // uniform
-    int kt2 = kt_s + d;
-    const bool next = kt2 >= nK;
-    kt2 -= next ? nK : 0;
-    unsigned char* buf = smem + (sidx & 1) * kG8Buf + op * kG8Img;
-    if (op == 0) {
-      const unsigned char* src = (next ? nxt.p : cur.p) + kt2 * 128;
-      const int32_t lim = next ? nxt.last : cur.last;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int bp = bp_of(h, jj);
-        const int row = min(bp + prow, lim);
-        __builtin_amdgcn_global_load_lds(src + (uint32_t)((row * DIM + 8 * pchunk) * 2),
-                                         (lds_ptr_t)(buf + bp * 128), 16, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int bq = bq_of(h, jj);
-        const int row = min(bq + prow, qlast);
-        __builtin_amdgcn_global_load_lds(qsrc + kt2 * 128 + (uint32_t)((row * DIM + 8 * pchunk) * 2),
-                                         (lds_ptr_t)(buf + bq * 128), 16, 0, 0);
-      }
-    }
-  };
-  // inverse norms of tile j's 256 rows -> LDS slot j & 1 (wave 0; clamped to the padded array,
-  // rows past the range are dead anyway)
-  auto issue_norms = [&](int j, int64_t r0) {
-    if (wave == 0 && j < n_tiles) {
-      const int64_t src = min(r0 + 4 * lane, n_pad - 4);
-      __builtin_amdgcn_global_load_lds(inv_norm32 + src,
-                                       (lds_ptr_t)(smem + kG8Norm + (j & 1) * 1024), 16, 0, 0);
-    }
-  };
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  const uint32_t co0 = (uint32_t)((((lane >> 4)) ^ (lane & 7)) << 4);
-  const uint32_t co1 = co0 ^ 64u;
-  const uint32_t rowP = (uint32_t)(128 * wp + (lane & 15)) * 128u;
-  const uint32_t rowQ = (uint32_t)(64 * wq + (lane & 15)) * 128u + kG8Img;
-  u32x4 pf[4][2], qf[2][2];
-  auto read_p = [&](int par, int ph) {
-    const uint32_t a0 = lds0 + par * kG8Buf + rowP + co0 + ph * 64 * 128;
-    const uint32_t a1 = lds0 + par * kG8Buf + rowP + co1 + ph * 64 * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pf[i][0]) : "v"(a0), "i"(i * 2048));
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pf[i][1]) : "v"(a1), "i"(i * 2048));
-    }
-  };
-  auto read_q = [&](int par, int qh) {
-    const uint32_t a0 = lds0 + par * kG8Buf + rowQ + co0 + qh * 32 * 128;
-    const uint32_t a1 = lds0 + par * kG8Buf + rowQ + co1 + qh * 32 * 128;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(qf[i][0]) : "v"(a0), "i"(i * 2048));
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(qf[i][1]) : "v"(a1), "i"(i * 2048));
-    }
-  };
-  auto frags_ready = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(pf[0][0]), "+v"(pf[0][1]), "+v"(pf[1][0]), "+v"(pf[1][1]),
-                   "+v"(pf[2][0]), "+v"(pf[2][1]), "+v"(pf[3][0]), "+v"(pf[3][1]),
-                   "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[1][0]), "+v"(qf[1][1])::"memory");
-  };
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  f32x4v acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  auto quadrant = [&](int ph, int qh) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          acc[4 * ph + i][2 * qh + jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-              __builtin_bit_cast(half8, pf[i][s2]), __builtin_bit_cast(half8, qf[jj][s2]),
-              acc[4 * ph + i][2 * qh + jj], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // per lane and query block qn (query 64 wq + 16 qn + (l & 15)): a 2-deep list in LDS (the
-  // lane's own dwords: key 0, key 1 with the row code in the low mantissa bits, and the two
-  // entries' tile indices as 16-bit halves; 12 live registers less than a register list, which
-  // the 128 accumulator + 48 fragment registers cannot spare) + the discarded bound in a register
-  float dl[4];
-  const uint32_t lst = lds0 + kG8List + (uint32_t)tid * 4u;
-#pragma unroll
-  for (int qn = 0; qn < 4; ++qn) {
-    dl[qn] = kNegInf;
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(kNegInf), "i"((qn * 3 + 0) * 2048) : "memory");
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(kNegInf), "i"((qn * 3 + 1) * 2048) : "memory");
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(lst), "v"(0u), "i"((qn * 3 + 2) * 2048) : "memory");
-  }
-  constexpr float kDead = -1.0e38f;
-  const uint32_t norm_lane = lds0 + kG8Norm + (uint32_t)(128 * wp + 4 * (lane >> 4)) * 4u;
-  auto epilogue = [&](int j) {
-    const int64_t r0 = cur.r0;
-    const int64_t live_rows = hi - r0;  // rows of the tile inside the range
-    uint64_t mw0 = ~0ull, mw1 = ~0ull;  // filter bits of rows r0 + 128 wp + [0, 128)
-    if (row_mask) {
-      const int64_t rb = r0 + 128 * wp;  // a multiple of 32 (ranges start on 32-row tiles)
-      const int64_t w0 = rb >> 6;
-      const int sh = (int)(rb & 63);
-      const int64_t n_words = (n_rows + 63) >> 6;
-      const uint64_t a = w0 < n_words ? row_mask[w0] : 0ull;
-      const uint64_t b = w0 + 1 < n_words ? row_mask[w0 + 1] : 0ull;
-      const uint64_t c = w0 + 2 < n_words ? row_mask[w0 + 2] : 0ull;
-      mw0 = sh ? (a >> sh) | (b << (64 - sh)) : a;
-      mw1 = sh ? (b >> sh) | (c << (64 - sh)) : b;
-    }
-    const uint32_t na = norm_lane + (uint32_t)(j & 1) * 1024u;
-    // live bit pm*4 + e of the lane's 32 rows (range end, filter); NaN norms are checked per read
-    uint32_t lbits = 0;
-#pragma unroll
-    for (int pm = 0; pm < 8; ++pm) {
-      const int rl = 128 * wp + 16 * pm + 4 * (lane >> 4);  // tile row of register 0
-      const uint64_t mw = pm < 4 ? mw0 : mw1;
-      const int sh = 16 * (pm & 3) + 4 * (lane >> 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        lbits |= ((rl + e < live_rows) && ((mw >> (sh + e)) & 1ull)) ? (1u << (pm * 4 + e)) : 0u;
-    }
-    // one query block at a time (3 chain registers live, not 12); the 8 inverse-norm reads per
-    // block are repeated per block (LDS, cheap). The opaque copy of the live bits keeps the
-    // compiler from hoisting 32 per-row (scale, bias) selects out of the qn loop (register spill).
-#pragma unroll
-    for (int qn = 0; qn < 4; ++qn) {
-      float b1 = kNegInf, b2 = kNegInf, b3 = kNegInf;
-      uint32_t lq = lbits;
-      asm volatile("" : "+v"(lq));
-#pragma unroll
-      for (int pm = 0; pm < 8; ++pm) {
-        f32x4v iv;
-        asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(iv) : "v"(na), "i"(pm * 64) : "memory");
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = iv[e];
-          const bool live = ((lq >> (pm * 4 + e)) & 1u) && x == x;
-          const float y = __builtin_fmaf(acc[pm][qn][e], live ? x : 0.0f,
-                                         live ? 0.0f : -3.4028234663852886e38f);
-          const float en = __uint_as_float((__float_as_uint(y) & ~31u) | (uint32_t)(pm * 4 + e));
-          const float t = fminf(b1, en);
-          b1 = fmaxf(b1, en);
-          const float t2 = fminf(b2, t);
-          b2 = fmaxf(b2, t);
-          b3 = fmaxf(b3, t2);
-        }
-        acc[pm][qn] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      }
-      if (b1 > kDead) {  // (b2, b3 <= b1: nothing to do for a dead or empty b1)
-        float sl[2];
-        uint32_t pj;
-        asm volatile("ds_read_b32 %0, %3 offset:%4\n\tds_read_b32 %1, %3 offset:%5\n\t"
-                     "ds_read_b32 %2, %3 offset:%6\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(sl[0]), "=v"(sl[1]), "=v"(pj)
-                     : "v"(lst), "i"((qn * 3 + 0) * 2048), "i"((qn * 3 + 1) * 2048),
-                       "i"((qn * 3 + 2) * 2048)
-                     : "memory");
-        int32_t il[2] = {(int32_t)(pj & 0xffffu), (int32_t)(pj >> 16)};
-        topm_insert<2>(b1, j, sl, il, dl[qn]);
-        if (b2 > kDead) topm_insert<2>(b2, j, sl, il, dl[qn]);
-        if (b3 > kDead) dl[qn] = fmaxf(dl[qn], b3);
-        pj = (uint32_t)il[0] | ((uint32_t)il[1] << 16);
-        asm volatile("ds_write_b32 %0, %1 offset:%3\n\tds_write_b32 %0, %2 offset:%4\n\t"
-                     "ds_write_b32 %0, %5 offset:%6"
-                     ::"v"(lst), "v"(sl[0]), "v"(sl[1]), "i"((qn * 3 + 0) * 2048),
-                       "i"((qn * 3 + 1) * 2048), "v"(pj), "i"((qn * 3 + 2) * 2048)
-                     : "memory");
-      }
-    }
-  };
-
-  issue_norms(0, cur.r0);
-  issue_half(0, 0, 0, 0, 0);
-  issue_half(0, 0, 0, 1, 0);
-  issue_half(0, 0, 0, 1, 1);
-  issue_half(0, 0, 0, 0, 1);
-  issue_half(1, 0, 1, 0, 0);
-  issue_half(1, 0, 1, 1, 1);
-  if (total > 1) {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  int j = 0, kt = 0;
-  for (int64_t st = 0; st < total; ++st) {
-    const int par = (int)(st & 1);
-    read_p(par, 0);
-    read_q(par, 0);
-    issue_half(st + 1, kt, 1, 0, 1);
-    if (kt == 1) issue_norms(j + 1, nxt.r0);  // slot (j+1)&1 was last read by epilogue(j-1)
-    __builtin_amdgcn_s_barrier();
-    frags_ready();
-    quadrant(0, 0);
-    __builtin_amdgcn_s_barrier();
-    read_q(par, 1);
-    issue_half(st + 1, kt, 1, 1, 0);
-    frags_ready();
-    quadrant(0, 1);
-    __builtin_amdgcn_s_barrier();
-    read_p(par, 1);
-    issue_half(st + 2, kt, 2, 0, 0);
-    frags_ready();
-    quadrant(1, 1);
-    __builtin_amdgcn_s_barrier();
-    read_q(par, 0);
-    issue_half(st + 2, kt, 2, 1, 1);
-    frags_ready();
-    quadrant(1, 0);
-    if (st + 2 < total) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (++kt == nK) {
-      epilogue(j);
-      kt = 0;
-      ++j;
-      cur = nxt;
-      nxt = tile_src(j + 1);
-    }
-  }
-
-  // Workgroup merge: per query the 8 lanes' 2-deep lists (16 entries) sorted descending + the
-  // largest discarded score, through LDS (buffer 0: every DMA has landed, the loop ended on a
-  // vmcnt(0) and a barrier)
-  float* lkey = reinterpret_cast<float*>(smem);                       // [256][16]
-  int32_t* lrow = reinterpret_cast<int32_t*>(smem + 256 * 16 * 4);     // [256][16]
-  float* lbnd = reinterpret_cast<float*>(smem + 256 * 16 * 8);        // [256][8]
-  const int grp = 4 * wp + (lane >> 4);
-  const int64_t rbase = lo + 128 * wp + 4 * (lane >> 4);
-  const float* lsf = reinterpret_cast<const float*>(smem + kG8List);
-  const uint32_t* lsu = reinterpret_cast<const uint32_t*>(smem + kG8List);
-#pragma unroll
-  for (int qn = 0; qn < 4; ++qn) {
-    const int ql = 64 * wq + 16 * qn + (lane & 15);
-    const uint32_t pj = lsu[(qn * 3 + 2) * kG8Threads + tid];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float key = lsf[(qn * 3 + e) * kG8Threads + tid];
-      const uint32_t code = __float_as_uint(key) & 31u;
-      const int64_t tile = e ? (pj >> 16) : (pj & 0xffffu);
-      const int64_t row = rbase + 256 * tile + 16 * (code >> 2) + (code & 3);
-      lkey[ql * 16 + 2 * grp + e] = key;
-      lrow[ql * 16 + 2 * grp + e] = key > kDead ? (int32_t)row : -1;
-    }
-    lbnd[ql * 8 + grp] = dl[qn];
-  }
-  __syncthreads();
-  if (tid < 256 && q_base + tid < nq) {
-    float key[16];
-    int32_t row[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      key[e] = lkey[tid * 16 + e];
-      row[e] = lrow[tid * 16 + e];
-    }
-    // bitonic sort of 16 in registers: descending by (key, row ascending)
-#pragma unroll
-    for (int size = 2; size <= 16; size <<= 1)
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int o = e ^ stride;
-          if (o > e) {
-            const bool desc = (e & size) == 0;
-            const bool o_better = armi::approx_better(key[o], row[o], key[e], row[e]);
-            if (o_better == desc) {
-              const float tk = key[e]; key[e] = key[o]; key[o] = tk;
-              const int32_t tr = row[e]; row[e] = row[o]; row[o] = tr;
-            }
-          }
-        }
-    float bnd = kNegInf;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bnd = fmaxf(bnd, lbnd[tid * 8 + e]);
-    const size_t base = (size_t)rp * nq + q_base + tid;
-#pragma unroll
-    for (int e = 0; e < kKW; ++e) {
-      cand_key[base * kKW + e] = key[e];
-      cand_row[base * kKW + e] = row[e];
-    }
-    cand_bound[base] = bnd;
   }
 }
 
@@ -3458,16 +1827,13 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
   }
 }
 
-// First kernel of an int8-scan call: zeroes the dynamic tile schedule's 8 head counters (heads,
-// one per 128-B line; nullptr = static schedule) and, with a row filter (mask), writes it in
-// int8 image order: bit p of the output = bit img_to_ord(p) of the caller's ordinal mask (0 for
-// padding positions), one wave per 64 image positions (T = 0: heads only).
+// First kernel of a filtered int8-scan call: the caller's row filter in int8 image order: bit p
+// of the output = bit img_to_ord(p) of the caller's ordinal mask (0 for padding positions), one
+// wave per 64 image positions.
 __global__ __launch_bounds__(256) void scan_prep_kernel(const uint64_t* __restrict__ mask,
                                                         int64_t n_rows, int64_t T,
                                                         const int32_t* __restrict__ tile_ord,
-                                                        uint64_t* __restrict__ out,
-                                                        int32_t* __restrict__ heads) {
-  if (heads && blockIdx.x == 0 && threadIdx.x < 8) heads[32 * threadIdx.x] = 0;
+                                                        uint64_t* __restrict__ out) {
   const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool bit = false;
   if (pos < T * 32) {
@@ -3660,146 +2026,26 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
 }
 
 // Multi-block calls (more than kQB queries): up to 2 blocks the XCD-grouped dense_scan_kernel
-// (HBM-bound, rows shared through L2), beyond that the LDS-tiled dense_gemm_scan_kernel (rows
-// read once per 256 queries). Measured per-GPU call times, 1M rows / G with G*64 queries:
-// G=2 366 vs 497 us, G=4 326 vs 272-318 us, G=8 308 vs 251-269 us (grouped vs register-staged
-// tiled); with the LDS-DMA tiled scan G=2 377 vs 459 us, G=4 357 vs 281 us
-// (profiles/r01f_scan_form_ab.txt), so the switch stays above two blocks.
-// ARMI_DENSE_SCAN=grouped|tiled forces one of them (A/B measurements).
-// Tile schedule of the one-block int8 scan (dense_scan_i8_kernel): static split (default) or,
-// with ARMI_I8_SCHED=dynamic, static first tiles + per-XCD dequeue. Round-3 A/B at 1M rows
-// (profiles/r03d_*): the first dynamic form (contiguous per-XCD parts) scanned in 0.248 ms vs
-// 0.231 ms static: its loop ran slower and its final steal round trips kept a tail.
-bool i8_dynamic_schedule() {
-  static const bool dyn = [] {
-    const char* e = getenv("ARMI_I8_SCHED");
-    return e && e[0] == 'd';
-  }();
-  return dyn;
-}
-
-// Intra-workgroup tile counter of the int8 first pass (default on); ARMI_I8_WGSPLIT=fixed keeps
-// the fixed tile-per-wave split (A/B).
-bool i8_wg_counter() {
-  static const bool on = [] {
-    const char* e = getenv("ARMI_I8_WGSPLIT");
-    return !(e && e[0] == 'f');
-  }();
-  return on;
-}
-
-bool use_gemm_scan(int nq) {
-  static const int force = [] {
-    const char* e = getenv("ARMI_DENSE_SCAN");
-    if (!e) return 0;
-    return e[0] == 't' ? 1 : (e[0] == 'g' ? 2 : 0);
-  }();
-  if (nq <= kQB) return false;
-  if (force) return force == 1;
-  return nq > 2 * kQB;
-}
-
-// Staging of the tiled scan: LDS-DMA (default) or registers. ARMI_GEMM_STAGE=reg|glds forces
-// one of them (A/B measurements).
-bool use_glds_staging() {
-  static const bool glds = [] {
-    const char* e = getenv("ARMI_GEMM_STAGE");
-    return !(e && e[0] == 'r');
-  }();
-  return glds;
-}
-
-// Lane-list epilogues skip (wave-uniformly) the insertion of a score no lane list takes, instead
-// of running the insertion network on all 16 scores of a tile; ARMI_INSERT_GUARD=0 disables it
-// (A/B). Both forms produce identical lists and bounds.
-int insert_guard() {
-  static const int g = [] {
-    const char* e = getenv("ARMI_INSERT_GUARD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return g;
-}
-
-// k-step width of the LDS-DMA tiled scan: 32 (four stages) or 64 (two stages of full 128-B row
-// segments); ARMI_GEMM_KSTEP=32|64 (A/B).
-int gemm_kstep() {
-  static const int k = [] {
-    const char* e = getenv("ARMI_GEMM_KSTEP");
-    return (e && atoi(e) == 64) ? 64 : 32;
-  }();
-  return k;
-}
-
-// Diagnostic ablations of the LDS-DMA tiled scan (results are wrong when set), ARMI_GEMM_ABLATE
-// bits: 8 re-reads the range's first row tile (row loads hit L2), 16 skips the vmcnt waits,
-// 32 the MFMAs, 64 the per-step barrier. Only a probe build (-DARMI_PROBE_BUILD) reads the
-// variable and carries the ablating instantiation; the shipped library ignores it, so a stray
-// environment variable can never produce wrong certified results.
-int gemm_ablate() {
-#ifdef ARMI_PROBE_BUILD
-  static const int a = [] {
-    const char* e = getenv("ARMI_GEMM_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  return a;
-#else
-  return 0;
-#endif
-}
-
-// Schedule of the LDS-DMA tiled scan: the four-wave kernel (default), the eight-wave four-stage
-// kernel (ARMI_GEMM_FORM=glds) or the phase-pipelined one (ARMI_GEMM_FORM=p8). Measured at the
-// 10M / 8-way per-rank shape: w4 1.49 ms, glds 1.67-1.78 ms, p8 2.00 ms; at 1M rows G = 4 / 8:
-// w4 196 / 171-186 us, glds 243 / 243 us (profiles/r02_w4_scan_ab.txt, r02_p8_scan_ab.txt).
-enum class GemmForm { W4, GLDS, P8, G8 };
-GemmForm gemm_form() {
-  static const GemmForm f = [] {
-    const char* e = getenv("ARMI_GEMM_FORM");
-    if (e && e[0] == 'g' && e[1] == '8') return GemmForm::G8;
-    if (e && e[0] == 'g') return GemmForm::GLDS;
-    if (e && e[0] == 'p') return GemmForm::P8;
-    return GemmForm::W4;
-  }();
-  return f;
-}
+// (HBM-bound, rows shared through L2), beyond that the LDS-DMA tiled dense_gemm_scan_w4_kernel
+// (rows read once per 256 queries). Measured per-GPU call times, 1M rows / G with G*64 queries
+// (profiles/r01f_scan_form_ab.txt, r02_w4_scan_ab.txt): the grouped scan wins at G = 2, the
+// tiled one from G = 4 on.
+bool use_gemm_scan(int nq) { return nq > 2 * kQB; }
 
 // The 64-query scan reads the int8 filter image (dense_scan_i8_kernel) for k <= 64, with the
-// merge rescoring the kc_i8 best upper bounds; ARMI_DENSE_FILTER=fp16 forces the fp16 scan (A/B).
+// merge rescoring the kc_i8 best upper bounds; larger k takes the fp16 scan (dense_scan_kernel).
 // k = 40 is the reference's default hybrid prefetch (QueryPipeline.query -> search(top_k=20) ->
 // dense prefetch limit 2 * 20, src/audio_rag/retrieval/qdrant.py:281-293).
 constexpr int kI8MaxK = 64;
-bool use_i8_filter(const armi_index* idx, int k) {
-  static const bool off = [] {
-    const char* e = getenv("ARMI_DENSE_FILTER");
-    return e && e[0] == 'f';
-  }();
-  return !off && idx->rows8 != nullptr && k <= kI8MaxK;
-}
-// int8 queries and the int8 MFMA too (ARMI_DENSE_QUERY=int8, k <= 6; A/B only): parity-green
-// but not faster (scan 0.286 vs 0.275 ms at 1M x 1024: the pass is bound by its loads, not by
-// the int8 -> fp16 conversion), and its looser keys (~45-85 rows reach the 5th cosine) leave
-// some queries uncertified at kc = 128 (exact fallback: 1.40 vs 0.35 ms mean step,
-// profiles/r02_int8_filter_ab.txt).
-bool use_q8(int k) {
-  static const bool on = [] {
-    const char* e = getenv("ARMI_DENSE_QUERY");
-    return e && e[0] == 'i';
-  }();
-  return on && k <= 6;
-}
+bool use_i8_filter(const armi_index* idx, int k) { return idx->rows8 != nullptr && k <= kI8MaxK; }
 // Rows rescored per query after the int8 pass: the rows whose key (an upper bound) reaches the
 // k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008). k <= 10
 // rescores 64 (hybrid's dense prefetch of 10: 6 400 of 6 400 queries certified at 1M rows, step
 // 0.255 vs 0.273 ms with 128, tools/probes/kc_ab.sh); a query whose k-th cosine sits among more
 // near-equal bounds takes the exact fallback, so only its time depends on this choice.
-// ARMI_DENSE_KC=64|128 forces either (A/B).
 // k = 40 at 1M random unit rows: ~110 rows reach the 40th cosine (bound slack 0.26 sigma at
 // 3.94 sigma), so 256; the collect pass catches whatever a smaller pool misses.
-int kc_i8(int k) {
-  static const int forced = getenv("ARMI_DENSE_KC") ? atoi(getenv("ARMI_DENSE_KC")) : 0;
-  if (forced == 64 || forced == 128 || forced == 256) return forced;
-  return use_q8(k) ? 128 : (k <= 10 ? 64 : (k <= 20 ? 128 : 256));
-}
+int kc_i8(int k) { return k <= 10 ? 64 : (k <= 20 ? 128 : 256); }
 
 // dense_merge_kernel's rescore: fp32 keys of the kc best, exact keys only for the rows within the
 // fp32 error of the k-th, when kc > 64 (k > 10: hybrid's prefetch of 40 rescores 256); else every
@@ -3841,6 +2087,11 @@ GemmPlan plan_gemm(const armi_index* idx, int nq) {
   const int64_t rows = std::max<int64_t>(idx->n_rows, 1);
   int want = std::max(1, (cus + p.n_qb - 1) / p.n_qb);
   want = (int)std::min<int64_t>(want, (rows + kGRT - 1) / kGRT);  // >= one row tile per range
+  // dense_gemm_scan_w4_kernel addresses a range's rows (plus one tile of clamped reads) with
+  // 32-bit byte offsets: enough ranges that every range stays below 4 GiB (<= 256 ranges, the
+  // merge's pool, cover 512M rows at dim 1024 - more than 288 GB of HBM holds)
+  const int64_t max_rows = ((int64_t(1) << 32) / (2 * (int64_t)idx->dim) - 2 * kG2Rows) / 32 * 32;
+  want = (int)std::max<int64_t>(want, (rows + max_rows - 1) / max_rows);
   p.rows_per_range = ((rows + want - 1) / want + 31) / 32 * 32;
   p.n_ranges = (int)((rows + p.rows_per_range - 1) / p.rows_per_range);
   p.grid = p.n_qb == 2 ? 16 * ((p.n_ranges + 7) / 8) : p.n_qb * p.n_ranges;
@@ -3878,9 +2129,6 @@ struct Workspace {
   int32_t* col_cnt;    // [nq] rows appended by the collect pass
   int32_t* col_list;   // [nq][kCollectCap] image positions
   uint64_t* mask_img;  // row filter in int8 image order
-  int32_t* heads;      // [8][32] dynamic tile schedule of the int8 scan (one counter per line)
-  u32x4* qimg;         // [n_qb][2 dim / 16][64] fragment image of each 64-query block
-  float* qnorm_img;    // [n_qb][64] |q| rounded up (the int8 key's bound term)
   size_t bytes;
 };
 
@@ -3896,10 +2144,6 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.col_cnt = cv.take<int32_t>(nq);
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
-    w.heads = cv.take<int32_t>(8 * 32);
-    const size_t n_qb = (size_t)(nq + kQB - 1) / kQB;
-    w.qimg = cv.take<u32x4>(n_qb * (size_t)(idx->dim / 16) * 2 * kQB);
-    w.qnorm_img = cv.take<float>(n_qb * kQB);
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -3948,167 +2192,49 @@ template <int DIM>
 int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, int k,
                       const uint64_t* row_mask, const uint64_t* mask_i8, float* out_scores,
                       int64_t* out_ids, double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                      const Workspace& w, hipStream_t stream, hipStream_t merge_stream,
-                      hipEvent_t merge_done, hipEvent_t pass_done);
+                      const Workspace& w, hipStream_t stream);
 
 template <int DIM>
 int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int k,
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                    const Workspace& w, hipStream_t stream, hipEvent_t scan_done,
-                    hipStream_t merge_stream, int phases = 3, hipEvent_t merge_done = nullptr,
-                    hipEvent_t pass_done = nullptr) {
+                    const Workspace& w, hipStream_t stream) {
   const ScanPlan sp = plan_scan(idx, k, nq);
   int n_wg = sp.n_wg;
   int kc = sp.kc;
   const int64_t T = std::max<int64_t>(idx->n_tiles, 1);
   // the int8 passes (first pass and collect pass) read the filter in image order
   const uint64_t* mask_i8 = nullptr;
-  if (!(phases & 1)) {  // armi_dense_second_pass: the first call built the filter image
-    mask_i8 = row_mask ? w.mask_img : nullptr;
-    return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,
-                                  out_rank, out_count, out_flags, w, stream, merge_stream,
-                                  merge_done, pass_done);
-  }
-  const bool i8_path = !use_gemm_scan(nq) && use_i8_filter(idx, k);
-  int32_t* heads = i8_path && sp.n_qb == 1 && i8_dynamic_schedule() ? w.heads : nullptr;
-  if (row_mask || heads) {
-    const int64_t Tm = row_mask ? T : 0;
-    scan_prep_kernel<<<dim3((unsigned)std::max<int64_t>(1, (Tm * 32 + 255) / 256)), dim3(256), 0,
-                       stream>>>(row_mask, idx->n_rows, Tm, idx->tile_ord, w.mask_img, heads);
+  if (row_mask) {
+    scan_prep_kernel<<<dim3((unsigned)std::max<int64_t>(1, (T * 32 + 255) / 256)), dim3(256), 0,
+                       stream>>>(row_mask, idx->n_rows, T, idx->tile_ord, w.mask_img);
     ARMI_LAUNCHED("scan_prep_kernel");
-    if (row_mask) mask_i8 = w.mask_img;
+    mask_i8 = w.mask_img;
   }
-  bool i8_first = false;
   if (use_gemm_scan(nq)) {
     const GemmPlan gp = plan_gemm(idx, nq);
     n_wg = gp.n_ranges;
-    const bool glds = use_glds_staging();
-    if (glds) {
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32, false>,
-                             gemm_glds_lds_bytes<DIM, 32>()))
-        return rc;
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 64, false>,
-                             gemm_glds_lds_bytes<DIM, 64>()))
-        return rc;
-#ifdef ARMI_PROBE_BUILD
-      if (int rc = allow_lds(dense_gemm_scan_glds_kernel<DIM, 32, true>,
-                             gemm_glds_lds_bytes<DIM, 32>()))
-        return rc;
-#endif
-    } else {
-      if (int rc = allow_lds(dense_gemm_scan_kernel<DIM>, gemm_scan_lds_bytes<DIM>())) return rc;
-    }
+    ARMI_REQUIRE((gp.rows_per_range + kG2Rows) * (int64_t)DIM * 2 < (int64_t(1) << 32),
+                 "armi_dense_topk: row range too large for the tiled scan");
+    auto kern = dense_gemm_scan_w4_kernel<DIM, 0>;
+    if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    // the four-wave kernel addresses a range's rows with 32-bit byte offsets
-    const bool w4_fits = (gp.rows_per_range + kG2Rows) * (int64_t)DIM * 2 < (int64_t(1) << 32);
-    if (glds && gemm_form() == GemmForm::G8) {
-      if (int rc = allow_lds(dense_gemm_scan_g8_kernel<DIM>, kG8Lds)) return rc;
-      dense_gemm_scan_g8_kernel<DIM><<<dim3(gp.grid), dim3(kG8Threads), kG8Lds, stream>>>(
-          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
-          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
-      ARMI_LAUNCHED("dense_gemm_scan_g8_kernel");
-    } else if (glds && gemm_form() == GemmForm::W4 && w4_fits) {
-      auto kern = dense_gemm_scan_w4_kernel<DIM, 0>;
-#ifdef ARMI_PROBE_BUILD
-      switch (gemm_ablate()) {
-        case 1: kern = dense_gemm_scan_w4_kernel<DIM, 1>; break;
-        case 2: kern = dense_gemm_scan_w4_kernel<DIM, 2>; break;
-        case 3: kern = dense_gemm_scan_w4_kernel<DIM, 3>; break;
-        case 4: kern = dense_gemm_scan_w4_kernel<DIM, 4>; break;
-        case 8: kern = dense_gemm_scan_w4_kernel<DIM, 8>; break;
-        case 9: kern = dense_gemm_scan_w4_kernel<DIM, 9>; break;
-        default: break;
-      }
-#endif
-      if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
-      kern<<<dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(), stream>>>(
-          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
-          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
-      ARMI_LAUNCHED("dense_gemm_scan_w4_kernel");
-    } else if (glds && gemm_form() == GemmForm::P8) {
-      auto kern = dense_gemm_scan_p8_kernel<DIM, 0>;
-#ifdef ARMI_PROBE_BUILD
-      switch (gemm_ablate()) {
-        case 1: kern = dense_gemm_scan_p8_kernel<DIM, 1>; break;
-        case 2: kern = dense_gemm_scan_p8_kernel<DIM, 2>; break;
-        case 3: kern = dense_gemm_scan_p8_kernel<DIM, 3>; break;
-        case 4: kern = dense_gemm_scan_p8_kernel<DIM, 4>; break;
-        case 8: kern = dense_gemm_scan_p8_kernel<DIM, 8>; break;
-        case 12: kern = dense_gemm_scan_p8_kernel<DIM, 12>; break;
-        case 13: kern = dense_gemm_scan_p8_kernel<DIM, 13>; break;
-        case 16: kern = dense_gemm_scan_p8_kernel<DIM, 16>; break;
-        case 32: kern = dense_gemm_scan_p8_kernel<DIM, 32>; break;
-        case 64: kern = dense_gemm_scan_p8_kernel<DIM, 64>; break;
-        case 68: kern = dense_gemm_scan_p8_kernel<DIM, 68>; break;
-        case 196: kern = dense_gemm_scan_p8_kernel<DIM, 196>; break;
-        case 324: kern = dense_gemm_scan_p8_kernel<DIM, 324>; break;
-        case 452: kern = dense_gemm_scan_p8_kernel<DIM, 452>; break;
-        case 192: kern = dense_gemm_scan_p8_kernel<DIM, 192>; break;
-        case 320: kern = dense_gemm_scan_p8_kernel<DIM, 320>; break;
-        case 512: kern = dense_gemm_scan_p8_kernel<DIM, 512>; break;
-        case 576: kern = dense_gemm_scan_p8_kernel<DIM, 576>; break;
-        case 1024: kern = dense_gemm_scan_p8_kernel<DIM, 1024>; break;
-        case 1088: kern = dense_gemm_scan_p8_kernel<DIM, 1088>; break;
-        default: break;
-      }
-#endif
-      if (int rc = allow_lds(kern, gemm_p8_lds_bytes<DIM>())) return rc;
-      kern<<<dim3(gp.grid), dim3(kGThreads), gemm_p8_lds_bytes<DIM>(), stream>>>(
-          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
-          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
-      ARMI_LAUNCHED("dense_gemm_scan_p8_kernel");
-    } else if (glds) {
-      auto kern = gemm_kstep() == 64 ? dense_gemm_scan_glds_kernel<DIM, 64, false>
-                                     : dense_gemm_scan_glds_kernel<DIM, 32, false>;
-#ifdef ARMI_PROBE_BUILD
-      if (gemm_ablate()) kern = dense_gemm_scan_glds_kernel<DIM, 32, true>;
-#endif
-      const size_t lds = gemm_kstep() == 64 ? gemm_glds_lds_bytes<DIM, 64>()
-                                            : gemm_glds_lds_bytes<DIM, 32>();
-      kern<<<dim3(gp.grid), dim3(kGThreads), lds, stream>>>(
-          idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
-          gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-          gemm_ablate());
-      ARMI_LAUNCHED("dense_gemm_scan_glds_kernel");
-    } else {
-      dense_gemm_scan_kernel<DIM><<<dim3(gp.grid), dim3(kGThreads), gemm_scan_lds_bytes<DIM>(),
-                                    stream>>>(idx->rows, idx->inv_norm32, row_mask, idx->n_rows,
-                                              gp.rows_per_range, gp.n_ranges, gp.n_qb, queries,
-                                              nq, w.cand_key, w.cand_row, w.cand_bound,
-                                              insert_guard());
-      ARMI_LAUNCHED("dense_gemm_scan_kernel");
-    }
+    kern<<<dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(), stream>>>(
+        idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
+        gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
+    ARMI_LAUNCHED("dense_gemm_scan_w4_kernel");
     if (int rc = tl.end()) return rc;
   } else if (use_i8_filter(idx, k)) {
     kc = kc_i8(k);
-    i8_first = true;
-    const bool qi8 = use_q8(k);
-    // ARMI_I8_IMAGE=dma: the query image built once by query_image_kernel and copied by LDS-DMA
-    // (A/B; the scan kernel is 4 % faster that way, but the extra launch costs more than that on
-    // the step: 0.262 vs 0.260 ms at 1M rows, 0.081 vs 0.075 ms at 100k, profiles/r03m_*), else
-    // every scan workgroup builds it itself (default)
-    static const bool img_pre = [] {
-      const char* e = getenv("ARMI_I8_IMAGE");
-      return e && e[0] == 'd';
-    }();
-    const bool pre = !qi8 && img_pre;
-    if (pre) {
-      query_image_kernel<DIM><<<dim3(sp.n_qb), dim3(kThreads), 0, stream>>>(queries, nq, w.qimg,
-                                                                          w.qnorm_img);
-      ARMI_LAUNCHED("query_image_kernel");
-    }
-    auto kern = qi8 ? dense_scan_i8_kernel<DIM, true, false> : dense_scan_i8_kernel<DIM, false, false>;
-    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, true, false>, scan_i8_lds_bytes<DIM>())) return rc;
-    if (int rc = allow_lds(dense_scan_i8_kernel<DIM, false, false>, scan_i8_lds_bytes<DIM>())) return rc;
+    auto kern = dense_scan_i8_kernel<DIM, false>;
+    if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard(),
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, heads, i8_wg_counter() ? 1 : 0,
-        pre ? w.qimg : nullptr, pre ? w.qnorm_img : nullptr);
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, idx->tile_ord,
+        nullptr, nullptr, nullptr, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -4117,14 +2243,9 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     dense_scan_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
         idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, insert_guard());
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
     ARMI_LAUNCHED("dense_scan_kernel");
     if (int rc = tl.end()) return rc;
-  }
-  if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
-  if (merge_stream != stream) {  // armi_dense_topk_split: the rest of the call on merge_stream
-    ARMI_HIP(hipStreamWaitEvent(merge_stream, scan_done, 0));
-    stream = merge_stream;
   }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)
@@ -4138,38 +2259,28 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
       idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt,
       merge_two_stage(kc) ? 1 : 0);
   ARMI_LAUNCHED("dense_merge_kernel");
-  if (!(phases & 2)) return ARMI_OK;  // armi_dense_topk_first
   return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,
-                                out_rank, out_count, out_flags, w, stream, stream, nullptr, nullptr);
+                                out_rank, out_count, out_flags, w, stream);
 }
 
 // Second pass for the uncertified queries (both kernels exit at once when every query of the
-// call is certified): int8 collect over the whole shard on `stream`, then exact rescore of the
-// lists on merge_stream. merge_done (nullable): `stream` waits on it first; pass_done (needed when
-// the streams differ): recorded after the collect pass, merge_stream waits on it.
+// call is certified): int8 collect over the whole shard, then exact rescore of the lists.
 template <int DIM>
 int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, int k,
                       const uint64_t* row_mask, const uint64_t* mask_i8, float* out_scores,
                       int64_t* out_ids, double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                      const Workspace& w, hipStream_t stream, hipStream_t merge_stream,
-                      hipEvent_t merge_done, hipEvent_t pass_done) {
-  if (merge_done) ARMI_HIP(hipStreamWaitEvent(stream, merge_done, 0));
+                      const Workspace& w, hipStream_t stream) {
   {
     const ScanPlan cp = plan_scan(idx, k, 1);  // one block's ranges; blocks of one range share an XCD
     const int n_qb = (nq + kQB - 1) / kQB;
     const int grid = n_qb == 1 ? cp.n_wg : n_qb * 8 * ((cp.n_wg + 7) / 8);
-    auto kern = dense_scan_i8_kernel<DIM, false, true>;
+    auto kern = dense_scan_i8_kernel<DIM, true>;
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
-        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, 0, idx->tile_ord, out_flags, w.thr,
-        w.col_cnt, w.col_list, kCollectCap, nullptr, 0, nullptr, nullptr);
+        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord, out_flags, w.thr,
+        w.col_cnt, w.col_list, kCollectCap);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
-  }
-  if (merge_stream != stream) {
-    ARMI_HIP(hipEventRecord(pass_done, stream));
-    ARMI_HIP(hipStreamWaitEvent(merge_stream, pass_done, 0));
-    stream = merge_stream;
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
   dense_collect_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kColMergeLds, stream>>>(
@@ -4189,49 +2300,6 @@ int dispatch_dim(int dim, F&& f) {
     case 1024: return f(std::integral_constant<int, 1024>{});
     default: return armi::fail(ARMI_ERR_INVALID, "unsupported dim");
   }
-}
-
-int dense_topk_entry(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
-                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                     double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
-                     size_t workspace_bytes, hipStream_t stream, hipStream_t merge_stream,
-                     hipEvent_t scan_done, int phases, hipEvent_t merge_done,
-                     hipEvent_t pass_done) {
-  ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
-  ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
-  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
-  if (n_queries == 0) return ARMI_OK;
-  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && out_flags && workspace,
-               "armi_dense_topk: null pointer argument");
-  ARMI_REQUIRE(workspace_bytes >= armi_dense_workspace_bytes(idx, n_queries, k),
-               "armi_dense_topk: workspace too small");
-  ARMI_HIP(hipSetDevice(idx->device));
-  if (idx->n_rows == 0) {
-    if (phases & 1) {
-      ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
-      ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
-      ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
-      if (scan_done) ARMI_HIP(hipEventRecord(scan_done, stream));
-      if (merge_stream != stream) ARMI_HIP(hipStreamWaitEvent(merge_stream, scan_done, 0));
-    } else {
-      if (merge_done) ARMI_HIP(hipStreamWaitEvent(stream, merge_done, 0));
-      if (merge_stream != stream) {
-        ARMI_HIP(hipEventRecord(pass_done, stream));
-        ARMI_HIP(hipStreamWaitEvent(merge_stream, pass_done, 0));
-      }
-    }
-    return ARMI_OK;
-  }
-  const Workspace w = carve(workspace, idx, n_queries, k, true);
-  double* rank = out_rank;
-  if (!rank)
-    rank = reinterpret_cast<double*>(static_cast<char*>(workspace) + armi::align_up(w.bytes, 256));
-  return dispatch_dim(idx->dim, [&](auto D) {
-    constexpr int DIM = decltype(D)::value;
-    return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
-                                out_count, out_flags, w, stream, scan_done, merge_stream, phases,
-                                merge_done, pass_done);
-  });
 }
 
 }  // namespace
@@ -4258,41 +2326,30 @@ int armi_dense_topk(const armi_index* idx, const uint16_t* queries, int n_querie
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
                     size_t workspace_bytes, hipStream_t stream) {
-  return armi_dense_topk_ex(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
-                            out_count, out_flags, workspace, workspace_bytes, stream, nullptr);
-}
-
-int armi_dense_topk_ex(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
-                       const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                       double* out_rank, int32_t* out_count, uint32_t* out_flags, void* workspace,
-                       size_t workspace_bytes, hipStream_t stream, hipEvent_t scan_done) {
-  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
-                          out_count, out_flags, workspace, workspace_bytes, stream, stream,
-                          scan_done, 3, nullptr, nullptr);
-}
-
-int armi_dense_topk_first(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
-                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                          double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                          void* workspace, size_t workspace_bytes, hipStream_t stream,
-                          hipStream_t merge_stream, hipEvent_t scan_done) {
-  ARMI_REQUIRE(merge_stream == stream || scan_done != nullptr,
-               "armi_dense_topk_first: a separate merge stream needs the scan_done event");
-  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
-                          out_count, out_flags, workspace, workspace_bytes, stream, merge_stream,
-                          scan_done, 1, nullptr, nullptr);
-}
-
-int armi_dense_second_pass(const armi_index* idx, const uint16_t* queries, int n_queries, int k,
-                           const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                           double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                           void* workspace, size_t workspace_bytes, hipStream_t stream,
-                           hipStream_t merge_stream, hipEvent_t merge_done, hipEvent_t pass_done) {
-  ARMI_REQUIRE(merge_stream == stream || pass_done != nullptr,
-               "armi_dense_second_pass: a separate merge stream needs the pass_done event");
-  return dense_topk_entry(idx, queries, n_queries, k, row_mask, out_scores, out_ids, out_rank,
-                          out_count, out_flags, workspace, workspace_bytes, stream, merge_stream,
-                          nullptr, 2, merge_done, pass_done);
+  ARMI_REQUIRE(idx != nullptr, "armi_dense_topk: index is null");
+  ARMI_REQUIRE(n_queries >= 0, "armi_dense_topk: n_queries < 0");
+  ARMI_REQUIRE(k >= 1 && k <= kMaxK, "armi_dense_topk: k must be in [1, 240]");
+  if (n_queries == 0) return ARMI_OK;
+  ARMI_REQUIRE(queries && out_scores && out_ids && out_count && out_flags && workspace,
+               "armi_dense_topk: null pointer argument");
+  ARMI_REQUIRE(workspace_bytes >= armi_dense_workspace_bytes(idx, n_queries, k),
+               "armi_dense_topk: workspace too small");
+  ARMI_HIP(hipSetDevice(idx->device));
+  if (idx->n_rows == 0) {
+    ARMI_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_queries, stream));
+    ARMI_HIP(hipMemsetAsync(out_flags, 0, sizeof(uint32_t) * n_queries, stream));
+    ARMI_HIP(hipMemsetAsync(out_ids, 0xff, sizeof(int64_t) * n_queries * k, stream));
+    return ARMI_OK;
+  }
+  const Workspace w = carve(workspace, idx, n_queries, k, true);
+  double* rank = out_rank;
+  if (!rank)
+    rank = reinterpret_cast<double*>(static_cast<char*>(workspace) + armi::align_up(w.bytes, 256));
+  return dispatch_dim(idx->dim, [&](auto D) {
+    constexpr int DIM = decltype(D)::value;
+    return dense_topk_impl<DIM>(idx, queries, n_queries, k, row_mask, out_scores, out_ids, rank,
+                                out_count, out_flags, w, stream);
+  });
 }
 
 size_t armi_dense_exact_workspace_bytes(const armi_index* idx, int n_queries, int k) {

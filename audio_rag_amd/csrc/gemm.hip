@@ -449,22 +449,7 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
     ARMI_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const int grid = (int)std::min<int64_t>(n_tiles, cus);
-  static const int nbar = [] {
-    const char* e = getenv("ARMI_GEMM_BARRIERS");
-    return (e && e[0] == '2') ? 2 : 4;
-  }();
-  // ARMI_LINEAR_STAGE=vgpr: register-staged operands (A/B against the LDS-DMA default)
-  static const bool vg = [] {
-    const char* e = getenv("ARMI_LINEAR_STAGE");
-    return e && e[0] == 'v';
-  }();
-  auto kern = linear_f16_kernel<0, 4>;
-  if (vg)
-    kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_f16_kernel<1, 4, 1> : linear_f16_kernel<0, 4, 1>;
-  else if (epilogue == ARMI_EPI_BIAS_GELU)
-    kern = nbar == 4 ? linear_f16_kernel<1, 4> : linear_f16_kernel<1, 2>;
-  else if (nbar == 2)
-    kern = linear_f16_kernel<0, 2>;
+  auto kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_f16_kernel<1, 4> : linear_f16_kernel<0, 4>;
   ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
   armi::TimedLaunch tl;

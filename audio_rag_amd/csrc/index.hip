@@ -242,39 +242,6 @@ int64_t armi_index_rows(const armi_index* idx) { return idx ? idx->n_rows : -1; 
 
 int armi_index_dim(const armi_index* idx) { return idx ? idx->dim : -1; }
 
-int armi_index_set_scan_cus(armi_index* idx, int cus) {
-  ARMI_REQUIRE(idx != nullptr, "armi_index_set_scan_cus: index is null");
-  ARMI_REQUIRE(cus >= 0, "armi_index_set_scan_cus: cus < 0");
-  idx->num_cus = cus == 0 ? idx->device_cus : std::min(cus, idx->device_cus);
-  return ARMI_OK;
-}
-
-int armi_cu_split_streams(int device, int reserve, hipStream_t* scan_stream,
-                          hipStream_t* merge_stream) {
-  ARMI_REQUIRE(scan_stream && merge_stream, "armi_cu_split_streams: null output");
-  hipDeviceProp_t prop;
-  ARMI_HIP(hipGetDeviceProperties(&prop, device));
-  const int n = prop.multiProcessorCount;
-  ARMI_REQUIRE(reserve >= 1 && reserve < n, "armi_cu_split_streams: reserve must be in [1, CUs)");
-  // the reserved CUs are the mask's top `reserve` bits: the runtime deals mask bits to the XCDs
-  // round-robin (bit c -> XCD c % 8 on MI355X: measured, reserving bits 31, 63, ... took 8 CUs
-  // of one XCD and its scan workgroups ran a second round), so consecutive bits spread the
-  // reservation over the XCDs and each XCD keeps as many scan CUs as the others (+-1)
-  const int words = (n + 31) / 32;
-  std::vector<uint32_t> scan(words, 0u), merge(words, 0u);
-  for (int c = 0; c < n; ++c) {
-    const bool reserved = c >= n - reserve;
-    (reserved ? merge : scan)[c / 32] |= 1u << (c % 32);
-  }
-  ARMI_HIP(hipSetDevice(device));
-  ARMI_HIP(hipExtStreamCreateWithCUMask(scan_stream, (uint32_t)words, scan.data()));
-  const hipError_t e = hipExtStreamCreateWithCUMask(merge_stream, (uint32_t)words, merge.data());
-  if (e != hipSuccess) {
-    (void)hipStreamDestroy(*scan_stream);
-    return armi::hip_fail(e, "hipExtStreamCreateWithCUMask");
-  }
-  return ARMI_OK;
-}
 
 int64_t armi_index_invalid_rows(const armi_index* idx) {
   if (!idx) return -1;

@@ -48,10 +48,14 @@ inline int64_t now_ns() {
 
 constexpr int kSlots = 3;           // batches in flight (GPU running / collected / collecting)
 constexpr int kMaxTerms = 256;      // sparse terms per query (armi_sparse_topk's limit)
-// Result ring entries (tickets whose results stay readable): max(2^14, 64 * max_batch) rounded up
-// to a power of two, i.e. 3.9 MB of host memory at k = 10, max_batch 64 (include/armi.h).
-int64_t ring_entries(int max_batch) {
+// Result ring entries (tickets whose results stay readable): the largest power of two whose
+// payload fits 128 MiB of host memory (2^19 tickets at k = 10), at least 2^14 and 64 * max_batch.
+// A caller that lets a ticket fall a whole ring behind gets "result overwritten" from
+// armi_stream_wait, never another ticket's results (the entries are published seqlock-style).
+int64_t ring_entries(int max_batch, int k) {
+  const int64_t per = (int64_t)k * (4 + 8 + 8) + (int64_t)sizeof(int64_t) * 6;
   int64_t r = 1 << 14;
+  while (r * 2 * per <= (int64_t(128) << 20)) r <<= 1;
   while (r < 64 * (int64_t)max_batch) r <<= 1;
   return r;
 }
@@ -73,6 +77,8 @@ struct Slot {
   int32_t* h_count = nullptr;
   hipEvent_t done = nullptr;
   int status = ARMI_OK;
+  std::vector<int64_t> t_submit;     // [max_batch] submit time of each query
+  std::vector<int32_t> qmode;        // [max_batch] branch (0 dense, 1 hybrid, 2 sparse)
   const uint64_t* mask = nullptr;    // the batch's row filter (every query of the batch)
   bool sealed = false;               // closed early: the next query needs another mask
   // hybrid servers: the batch's sparse query CSR (pinned + device), prefetch lists, fusion
@@ -99,6 +105,11 @@ struct Slot {
   int32_t* h_f_count = nullptr;
 };
 
+// A ring entry is published seqlock-style: the completion thread sets ticket to kWriting, writes
+// the payload (fields + the r_* arrays), then stores the ticket with release; a reader copies the
+// payload after an acquire load equal to its ticket and re-checks the ticket afterwards.
+constexpr int64_t kWriting = -2;
+
 struct Entry {
   std::atomic<int64_t> ticket{-1};   // ticket whose result this entry holds (complete when set)
   int64_t t_submit = 0;
@@ -116,7 +127,6 @@ struct armi_stream {
   int rrf_k = 2;
   int kp = 0;                               // dense prefetch limit (2k hybrid, k dense)
   size_t sws_bytes = 0;
-  std::vector<int32_t> qmode;               // per ring entry: branch (0 dense, 1 hybrid, 2 sparse)
   int k = 0, max_batch = 0, dim = 0;
   int64_t max_wait_ns = 0;
   size_t ws_bytes = 0;
@@ -249,8 +259,24 @@ void completer_main(armi_stream* s) {
       const int64_t tk = sl.first_ticket + i;
       Entry& e = s->ring[tk % s->ring_n];
       const size_t o = (size_t)(tk % s->ring_n) * s->k;
-      const int qm = s->qmode[tk % s->ring_n];
-      if (status == ARMI_OK && qm == 2) {
+      const int qm = sl.qmode[i];
+      e.ticket.store(kWriting, std::memory_order_relaxed);
+      std::atomic_thread_fence(std::memory_order_release);
+      // (sl.nnz == 0: the batch's sparse pass did not run; its hybrid / sparse-only queries
+      // carry empty sparse vectors: RRF over the dense list alone / an empty result, exactly
+      // what the device pass gives an empty query)
+      if (status == ARMI_OK && qm != 0 && sl.nnz == 0) {
+        const size_t d = (size_t)i * s->kp;
+        e.count = qm == 1 ? std::min(sl.h_count[i], s->k) : 0;
+        for (int j = 0; j < s->k; ++j) {
+          const bool v = j < e.count;
+          const double rrf = 1.0 / (double)(s->rrf_k + j);
+          s->r_ids[o + j] = v ? sl.h_ids[d + j] : -1;
+          s->r_rank[o + j] = v ? rrf : 0.0;
+          s->r_scores[o + j] = v ? (float)rrf : 0.0f;
+        }
+        e.mode = qm;
+      } else if (status == ARMI_OK && qm == 2) {
         // sparse-only branch: the first k of the sparse prefetch list, hit.score = the dot
         const size_t d = (size_t)i * s->kp;
         e.count = std::min(sl.h_sp_count[i], s->k);
@@ -282,6 +308,7 @@ void completer_main(armi_stream* s) {
         e.count = 0;
       }
       e.status = status;
+      e.t_submit = sl.t_submit[i];
       e.t_done = t;
       e.ticket.store(tk, std::memory_order_release);
     }
@@ -354,6 +381,8 @@ int alloc_slot(armi_stream* s, Slot& sl) {
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&sl.d_flags), nq * sizeof(uint32_t)));
   ARMI_HIP(hipMalloc(&sl.d_ws, s->ws_bytes));
   ARMI_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  sl.t_submit.assign(nq, 0);
+  sl.qmode.assign(nq, 0);
   if (s->sidx) {
     const size_t nt = nq * kMaxTerms, nf = nq * s->k;
     ARMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.h_sp_ptr), (nq + 1) * sizeof(int32_t)));
@@ -405,9 +434,8 @@ int create_impl(const armi_index* idx, const armi_sparse_index* sidx, int k, int
   s->device = idx->device;
   s->ws_bytes = armi_dense_workspace_bytes(idx, max_batch, s->kp);
   if (sidx) s->sws_bytes = armi_sparse_workspace_bytes(sidx, max_batch, s->kp);
-  s->ring_n = ring_entries(max_batch);
+  s->ring_n = ring_entries(max_batch, k);
   s->ring = std::vector<Entry>(s->ring_n);
-  s->qmode.assign(s->ring_n, 0);
   s->r_scores.assign((size_t)s->ring_n * k, 0.f);
   s->r_ids.assign((size_t)s->ring_n * k, -1);
   s->r_rank.assign((size_t)s->ring_n * k, 0.0);
@@ -456,8 +484,12 @@ int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
                "armi_stream_submit: sparse terms need a hybrid server and both arrays");
   ARMI_REQUIRE(mode == ARMI_STREAM_AUTO || mode == ARMI_STREAM_DENSE || mode == ARMI_STREAM_SPARSE,
                "armi_stream_submit: unknown mode");
-  // the branch (QdrantRetriever.search): terms decide between hybrid / sparse-only and dense
-  const int qm = nnz == 0 || mode == ARMI_STREAM_DENSE ? 0 : (mode == ARMI_STREAM_SPARSE ? 2 : 1);
+  // the branch (QdrantRetriever.search, qdrant.py:272/299): a query that carries a sparse vector
+  // (the arrays are non-null, even with nnz = 0: `if query.sparse` is true for an empty
+  // SparseVector object) takes the hybrid / sparse-only branch, else the dense one
+  const bool has_sparse = sp_idx != nullptr && sp_val != nullptr;
+  const int qm = !has_sparse || !s->sidx || mode == ARMI_STREAM_DENSE
+                     ? 0 : (mode == ARMI_STREAM_SPARSE ? 2 : 1);
   if (qm == 0) nnz = 0;  // a dense-branch query adds nothing to the batch's sparse pass
   std::unique_lock<std::mutex> lk(s->mu);
   for (;;) {
@@ -486,14 +518,56 @@ int submit_impl(armi_stream* s, const uint16_t* query, const int32_t* sp_idx,
     c.nnz += nnz;
     c.h_sp_ptr[c.n + 1] = c.nnz;
   }
-  s->qmode[tk % s->ring_n] = qm;
-  Entry& e = s->ring[tk % s->ring_n];
-  e.t_submit = now_ns();
+  c.qmode[c.n] = qm;
+  c.t_submit[c.n] = now_ns();
   ++c.n;
   const bool wake = c.n == 1 || c.n == s->max_batch;
   lk.unlock();
   if (wake) s->cv_dispatch.notify_one();
   *ticket = tk;
+  return ARMI_OK;
+}
+
+// Waits for `ticket` and copies its result out; t_submit / t_done (nullable) receive its submit
+// and completion times. The copy is validated after the fact: if the completion thread reused
+// the entry meanwhile (the caller fell a whole ring behind), the call fails instead of returning
+// another ticket's results.
+int wait_impl(armi_stream* s, int64_t ticket, float* scores, int64_t* ids, double* rank,
+              int32_t* count, int32_t* mode, double timeout_us, int64_t* t_submit,
+              int64_t* t_done) {
+  ARMI_REQUIRE(s && count, "armi_stream_wait: null pointer argument");
+  ARMI_REQUIRE(ticket >= 0, "armi_stream_wait: bad ticket");
+  Entry& e = s->ring[ticket % s->ring_n];
+  if (e.ticket.load(std::memory_order_acquire) != ticket) {
+    std::unique_lock<std::mutex> lk(s->mu);
+    const auto until = Clock::now() + std::chrono::nanoseconds((int64_t)(timeout_us * 1e3));
+    while (e.ticket.load(std::memory_order_acquire) != ticket) {
+      if (ticket >= s->next_ticket) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: unknown ticket");
+      if (e.ticket.load(std::memory_order_acquire) > ticket)
+        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: result overwritten (ring wrapped)");
+      if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: server stopped");
+      if (s->cv_done.wait_until(lk, until) == std::cv_status::timeout &&
+          e.ticket.load(std::memory_order_acquire) != ticket)
+        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: timeout");
+    }
+  }
+  const int status = e.status;
+  const int32_t cnt = e.count, md = e.mode;
+  const int64_t ts = e.t_submit, td = e.t_done;
+  const size_t o = (size_t)(ticket % s->ring_n) * s->k;
+  if (status == ARMI_OK) {
+    if (scores) std::memcpy(scores, &s->r_scores[o], s->k * sizeof(float));
+    if (ids) std::memcpy(ids, &s->r_ids[o], s->k * sizeof(int64_t));
+    if (rank) std::memcpy(rank, &s->r_rank[o], s->k * sizeof(double));
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if (e.ticket.load(std::memory_order_relaxed) != ticket)
+    return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: result overwritten (ring wrapped)");
+  if (status != ARMI_OK) return armi::fail(status, "armi_stream_wait: the batch failed");
+  if (mode) *mode = md;
+  *count = cnt;
+  if (t_submit) *t_submit = ts;
+  if (t_done) *t_done = td;
   return ARMI_OK;
 }
 
@@ -555,31 +629,8 @@ int armi_stream_submit_ex(armi_stream* s, const uint16_t* query, const int32_t* 
 
 int armi_stream_wait(armi_stream* s, int64_t ticket, float* scores, int64_t* ids, double* rank,
                      int32_t* count, int32_t* mode, double timeout_us) {
-  ARMI_REQUIRE(s && count, "armi_stream_wait: null pointer argument");
-  ARMI_REQUIRE(ticket >= 0, "armi_stream_wait: bad ticket");
   Active a(s);
-  Entry& e = s->ring[ticket % s->ring_n];
-  if (e.ticket.load(std::memory_order_acquire) != ticket) {
-    std::unique_lock<std::mutex> lk(s->mu);
-    const auto until = Clock::now() + std::chrono::nanoseconds((int64_t)(timeout_us * 1e3));
-    while (e.ticket.load(std::memory_order_acquire) != ticket) {
-      if (ticket >= s->next_ticket) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: unknown ticket");
-      if (e.ticket.load(std::memory_order_acquire) > ticket)
-        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: result overwritten (ring wrapped)");
-      if (s->stop) return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: server stopped");
-      if (s->cv_done.wait_until(lk, until) == std::cv_status::timeout &&
-          e.ticket.load(std::memory_order_acquire) != ticket)
-        return armi::fail(ARMI_ERR_INVALID, "armi_stream_wait: timeout");
-    }
-  }
-  if (e.status != ARMI_OK) return armi::fail(e.status, "armi_stream_wait: the batch failed");
-  const size_t o = (size_t)(ticket % s->ring_n) * s->k;
-  if (scores) std::memcpy(scores, &s->r_scores[o], s->k * sizeof(float));
-  if (ids) std::memcpy(ids, &s->r_ids[o], s->k * sizeof(int64_t));
-  if (rank) std::memcpy(rank, &s->r_rank[o], s->k * sizeof(double));
-  if (mode) *mode = e.mode;
-  *count = e.count;
-  return ARMI_OK;
+  return wait_impl(s, ticket, scores, ids, rank, count, mode, timeout_us, nullptr, nullptr);
 }
 
 int armi_stream_stats(armi_stream* s, int64_t* batches, int64_t* queries) {
@@ -618,15 +669,15 @@ int armi_stream_loadgen(armi_stream* s, const uint16_t* queries, const int32_t* 
       }
       const int64_t tk = tickets[(size_t)i];
       int64_t* ids = out_ids ? out_ids + (size_t)i * s->k : nullptr;
-      if (int rc = armi_stream_wait(s, tk, nullptr, ids, nullptr, &cnt, nullptr, 60e6)) {
+      int64_t ts = 0, td = 0;
+      if (int rc = wait_impl(s, tk, nullptr, ids, nullptr, &cnt, nullptr, 60e6, &ts, &td)) {
         rc_col.store(rc);
         return;
       }
       if (out_count) out_count[i] = cnt;
-      const Entry& e = s->ring[tk % s->ring_n];
-      latency_us[i] = (double)(e.t_done - e.t_submit) * 1e-3;
-      t_last = std::max(t_last, e.t_done);
-      if (t_first < 0) t_first = e.t_submit;
+      latency_us[i] = (double)(td - ts) * 1e-3;
+      t_last = std::max(t_last, td);
+      if (t_first < 0) t_first = ts;
     }
   });
   const int64_t t0 = now_ns();

@@ -288,10 +288,11 @@ class StreamServer:
         st = search_type or self.search_type
         if st not in self._MODES:
             raise RetrievalError(f"unknown search_type {st!r}")
-        has_terms = sparse is not None and len(sparse[0]) > 0
-        # the sparse lists exist only on a hybrid collection (else search() takes the dense
-        # branch whatever search_type says)
-        wants_sparse = st != "dense" and has_terms and self.collection.hybrid
+        # a query carrying a sparse vector, even an empty one, takes the hybrid / sparse-only
+        # branch as search() does (`sparse is not None`; the reference's `if query.sparse` is
+        # true for any SparseVector object, qdrant.py:272/299). The sparse lists exist only on a
+        # hybrid collection (else search() takes the dense branch whatever search_type says)
+        wants_sparse = st != "dense" and sparse is not None and self.collection.hybrid
         if wants_sparse and not self.hybrid:
             raise RetrievalError(f"search_type {st!r} needs a server created with search_type "
                                  "'hybrid' or 'sparse'")
@@ -302,6 +303,8 @@ class StreamServer:
             if idx.size > 256:
                 raise RetrievalError("a sparse query may hold at most 256 terms")
             nnz = idx.size
+            if nnz == 0:  # non-null arrays mark "has a (empty) sparse vector" for the server
+                idx, val = np.zeros(1, dtype=np.int32), np.zeros(1, dtype=np.float32)
         mask = self.collection.filter_mask(filter_metadata)
         ticket = self._armi.ctypes.c_int64()
         self._call("armi_stream_submit_ex", q.ctypes.data,

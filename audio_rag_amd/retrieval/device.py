@@ -7,7 +7,6 @@ memory and the stream. Results stay on the device until the caller materialises 
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -124,11 +123,6 @@ class DenseIndex:
             _device_copy(dst.data_ptr(), src.value, dst.numel() * dst.element_size())
         return out
 
-    def set_scan_cus(self, cus: int) -> None:
-        """First-pass scan workgroups: one per CU it may use (0 = every CU of the device); size
-        workspaces after changing it (armi_index_set_scan_cus)."""
-        call("armi_index_set_scan_cus", self._handle, int(cus))
-
     def scan_form(self, n_queries: int, k: int) -> int:
         """Which scan armi_dense_topk runs for this call shape (_armi.SCAN_*)."""
         return int(query("armi_dense_scan_form", self._handle, n_queries, k))
@@ -139,11 +133,9 @@ class DenseIndex:
 
     def topk(self, queries: torch.Tensor, k: int, row_mask: torch.Tensor | None = None,
              exact: bool = False, workspace: torch.Tensor | None = None,
-             out: TopK | None = None, scan_done: torch.cuda.Event | None = None) -> TopK:
+             out: TopK | None = None) -> TopK:
         """Cosine top-k of every query row. row_mask: int64 tensor holding a bitmask of enabled
-        rows (bit r of word r // 64), or None. scan_done (fast path): an event recorded on the
-        current stream after the first-pass scan, before the merge (armi_dense_topk_ex), for
-        callers that pipeline batches on two streams."""
+        rows (bit r of word r // 64), or None."""
         _check_fp16_2d(queries, "queries", self.dim)
         if not 1 <= k <= MAX_K:
             raise ValueError(f"k must be in [1, {MAX_K}]")
@@ -169,62 +161,11 @@ class DenseIndex:
                  workspace.numel(), s)
             if out.flags is not None:
                 out.flags.fill_(_armi.ARMI_FLAG_FALLBACK)
-        elif scan_done is not None:
-            if scan_done.cuda_event == 0:  # torch creates the event at its first record
-                scan_done.record()
-            call("armi_dense_topk_ex", self._handle, ptr(queries), b, k, ptr(row_mask),
-                 ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(out.flags),
-                 ptr(workspace), workspace.numel(), s, scan_done.cuda_event)
         else:
             call("armi_dense_topk", self._handle, ptr(queries), b, k, ptr(row_mask),
                  ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count), ptr(out.flags),
                  ptr(workspace), workspace.numel(), s)
         return out
-
-
-def cu_split_streams(device: torch.device, reserve: int) -> tuple[torch.cuda.ExternalStream,
-                                                                    torch.cuda.ExternalStream]:
-    """(scan_stream, merge_stream) over disjoint CU sets: merge_stream on `reserve` CUs, the scan
-    stream on the rest (armi_cu_split_streams; the streams live for the process)."""
-    a, b = ctypes.c_void_p(), ctypes.c_void_p()
-    call("armi_cu_split_streams", device.index or 0, int(reserve), ctypes.byref(a), ctypes.byref(b))
-    return (torch.cuda.ExternalStream(a.value, device=device),
-            torch.cuda.ExternalStream(b.value, device=device))
-
-
-def _event_handle(ev: torch.cuda.Event | None):
-    if ev is None:
-        return None
-    if ev.cuda_event == 0:  # torch creates the event at its first record
-        ev.record()
-    return ev.cuda_event
-
-
-def dense_topk_first(index: "DenseIndex", queries: torch.Tensor, k: int, workspace: torch.Tensor,
-                     out: TopK, merge_stream: torch.cuda.Stream, scan_done: torch.cuda.Event,
-                     row_mask: torch.Tensor | None = None) -> TopK:
-    """First half of a CU-split dense call (armi_dense_topk_first): the scan on the current
-    stream, the merge on merge_stream after scan_done. `out` holds the certified answers; the
-    call is complete after dense_second_pass with the same workspace and outputs."""
-    _check_fp16_2d(queries, "queries", index.dim)
-    call("armi_dense_topk_first", index.handle, ptr(queries), int(queries.shape[0]), k,
-         ptr(row_mask), ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count),
-         ptr(out.flags), ptr(workspace), workspace.numel(), stream_handle(),
-         merge_stream.cuda_stream, _event_handle(scan_done))
-    return out
-
-
-def dense_second_pass(index: "DenseIndex", queries: torch.Tensor, k: int, workspace: torch.Tensor,
-                      out: TopK, merge_stream: torch.cuda.Stream,
-                      merge_done: torch.cuda.Event | None, pass_done: torch.cuda.Event,
-                      row_mask: torch.Tensor | None = None) -> TopK:
-    """Second half (armi_dense_second_pass): the collect pass on the current stream after
-    merge_done, the collect merge on merge_stream after pass_done."""
-    call("armi_dense_second_pass", index.handle, ptr(queries), int(queries.shape[0]), k,
-         ptr(row_mask), ptr(out.scores), ptr(out.ids), ptr(out.rank), ptr(out.count),
-         ptr(out.flags), ptr(workspace), workspace.numel(), stream_handle(),
-         merge_stream.cuda_stream, _event_handle(merge_done), _event_handle(pass_done))
-    return out
 
 
 class SparseIndex:
@@ -356,22 +297,15 @@ class ConcurrentHybrid:
         self.side = torch.cuda.Stream(device=device)
 
     def __call__(self, dense_fn, sparse_fn, sparse_inputs, limit: int, rrf_k: int = 2) -> TopK:
-        if os.environ.get("ARMI_HYBRID_SERIAL"):
-            return rrf_fuse(dense_fn(), sparse_fn(), limit, rrf_k=rrf_k)
         main = torch.cuda.current_stream()
         self.side.wait_stream(main)
         for t in sparse_inputs:
             if isinstance(t, torch.Tensor) and t.is_cuda:
                 t.record_stream(self.side)
-        # issue order (A/B, ARMI_HYBRID_ORDER=dense): the sparse chain first by default
-        if os.environ.get("ARMI_HYBRID_ORDER", "sparse").startswith("d"):
-            d = dense_fn()
-            with torch.cuda.stream(self.side):
-                s = sparse_fn()
-        else:
-            with torch.cuda.stream(self.side):
-                s = sparse_fn()
-            d = dense_fn()
+        # the sparse chain is issued first (round-3 A/B: profiles/r03x_*)
+        with torch.cuda.stream(self.side):
+            s = sparse_fn()
+        d = dense_fn()
         main.wait_stream(self.side)
         for t in s.tensors():
             t.record_stream(main)

@@ -194,6 +194,9 @@ def cpu_baseline(wl: str, ref: CpuReference, queries: np.ndarray, q_csr: list | 
         "value": 1.0 / p50,
         "unit": "queries/sec",
         "cores": ref.threads,
+        "host_cores": os.cpu_count(),
+        "cores_note": (f"{ref.threads} threads used (the box's OMP_NUM_THREADS share) on a host "
+                       f"with {os.cpu_count()} logical CPUs"),
         "kind": "port",
         "mode": "reference-shaped: one query per call, as AudioRAG.query() issues it",
         "p50_ms": p50 * 1e3,
@@ -212,16 +215,29 @@ def cpu_baseline(wl: str, ref: CpuReference, queries: np.ndarray, q_csr: list | 
     return res
 
 
-def read_traffic(form: int = 0) -> float | None:
-    """HBM bytes per launch of the 64-query scan from the committed PMC pass (FETCH_SIZE +
-    WRITE_SIZE, gfx950-corrected) for the scan form armi_dense_scan_form reports."""
-    p = ROOT / "profiles" / ("dense_scan_i8_traffic.json" if form == 1 else "dense_scan_traffic.json")
-    if p.exists():
-        try:
-            return float(json.loads(p.read_text())["hbm_bytes_per_launch"])
-        except Exception:
-            return None
-    return None
+TRAFFIC_DIR = ROOT / "profiles" / "traffic"
+
+
+def traffic_key(form: int, n_rows: int, dim: int, n_queries: int, corpus: str) -> str:
+    """Name of the committed PMC measurement of one scan shape (tools/pmc_dense_traffic.sh)."""
+    name = {0: "fp16", 1: "i8", 2: "tiled"}.get(form, f"form{form}")
+    return f"dense_{name}_{corpus}_n{n_rows}_d{dim}_q{n_queries}"
+
+
+def read_traffic(key: str) -> tuple[float | None, str | None]:
+    """HBM bytes per launch of the scan measured by rocprofv3 PMC passes (FETCH_SIZE and
+    WRITE_SIZE in separate runs, gfx950-corrected) for exactly this shape, or (None, None) when no
+    such measurement is committed: a traffic figure of another shape says nothing here."""
+    p = TRAFFIC_DIR / f"{key}.json"
+    if not p.exists():
+        return None, None
+    try:
+        d = json.loads(p.read_text())
+        if d.get("key") != key:
+            return None, None
+        return float(d["hbm_bytes_per_launch"]), str(p.relative_to(ROOT))
+    except Exception:
+        return None, None
 
 
 def main() -> None:
@@ -238,13 +254,8 @@ def main() -> None:
                     help="dense headline at N=1 only: skip the secondary configs1 / configs2 "
                          "objects (each measured by a child bench.py run)")
     ap.add_argument("--latency-iters", type=int, default=30)
-    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=1,
-                    help="dense, 1 GPU: batches in flight on their own HIP streams (2: batch i+1's "
-                         "scan starts when batch i's scan ends, batch i's merge runs beside it)")
-    ap.add_argument("--merge-cus", type=int, default=0,
-                    help="dense, 1 GPU, --pipeline 2: reserve this many CUs for the merge / second "
-                         "pass (a CU-masked stream pair, armi_cu_split_streams): every scan runs on "
-                         "the other CUs, batch i's merge on the reserved ones beside batch i+1's scan")
+    ap.add_argument("--cpu-budget", type=float, default=20.0,
+                    help="seconds per timed leg of the cpu_baseline (single-query, batched, rerank)")
     ap.add_argument("--workload", choices=["dense", "hybrid", "hybrid_rerank", "stream", "pipeline",
                                            "ingest"],
                     default="dense",
@@ -383,88 +394,10 @@ def main() -> None:
                     rank=torch.gather(probs, 1, order).double(),
                     count=torch.clamp(fused.count, max=k))
 
-    # dense, one GPU: two batches in flight (armi_dense_topk_ex's scan-done event): batch i+1's
-    # stream waits for batch i's first-pass scan, so the scans run back to back while batch i's
-    # merge / second-pass launches run beside batch i+1's scan. Every batch still runs its whole
-    # call (scan, merge, exact rescore, second pass); only the overlap is new.
-    pipe = wl == "dense" and sharded is None and args.pipeline == 2
-    split = pipe and args.merge_cus > 0
-    if split:
-        # CU split: every scan (and every collect pass) on the scan stream's CUs, back to back;
-        # batch i's merge on the reserved CUs (merge stream) beside batch i+1's scan; batch i's
-        # second pass (collect pass + collect merge, both exit at once when every query is
-        # certified) issued after batch i+1's scan. Three workspaces / output sets rotate: batch
-        # i+3's scan waits until batch i's last kernel is done. Every batch still runs its whole
-        # call; finish() completes the last one inside the timed region.
-        from audio_rag_amd.retrieval.device import (cu_split_streams, dense_second_pass,
-                                                    dense_topk_first)
-        s_scan, s_merge = cu_split_streams(dev, args.merge_cus)
-        n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        index.set_scan_cus(n_cus - args.merge_cus)
-        ws = torch.empty(index.workspace_bytes(batch, pre_k), dtype=torch.uint8, device=dev)
-        p_ws = [ws, torch.empty_like(ws), torch.empty_like(ws)]
-        p_out = [TopK(scores=torch.empty((batch, k), dtype=torch.float32, device=dev),
-                      ids=torch.empty((batch, k), dtype=torch.int64, device=dev),
-                      rank=torch.empty((batch, k), dtype=torch.float64, device=dev),
-                      count=torch.empty(batch, dtype=torch.int32, device=dev),
-                      flags=torch.empty(batch, dtype=torch.int32, device=dev)) for _ in range(3)]
-        p_scan_ev = [torch.cuda.Event() for _ in range(3)]
-        p_pass_ev = [torch.cuda.Event() for _ in range(3)]
-        p_merge_ev = [None] * 3
-        p_done_ev = [None] * 3
-        p_pending = [None]  # (slot, queries) of the batch whose second pass is not issued yet
-        s_scan.wait_stream(torch.cuda.current_stream())
-        s_merge.wait_stream(torch.cuda.current_stream())
-
-        def finish():
-            """Issue the pending batch's second pass (collect on the scan CUs, collect merge on
-            the reserved ones)."""
-            if p_pending[0] is None:
-                return
-            slot, qp = p_pending[0]
-            with torch.cuda.stream(s_scan):
-                dense_second_pass(index, qp, k, p_ws[slot], p_out[slot], s_merge,
-                                  p_merge_ev[slot], p_pass_ev[slot])
-            ev = torch.cuda.Event()
-            ev.record(s_merge)
-            p_done_ev[slot] = ev
-            torch.cuda.current_stream().wait_event(ev)  # consumers on the default stream
-            p_pending[0] = None
-    elif pipe:
-        p_streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
-        p_ws = [ws, torch.empty_like(ws)]
-        p_ev = [torch.cuda.Event() for _ in range(2)]
-        p_prev = [None]
-        p_synced = [False, False]
-
     def step(i: int, q_local: torch.Tensor | None = None):
         j = i % n_q_batches
         ql = q_local if q_local is not None else queries[j]
         if wl == "dense":
-            if split and ql.shape[0] == batch:
-                slot = i % 3
-                if p_done_ev[slot] is not None:  # batch i-3's workspace / outputs released
-                    s_scan.wait_event(p_done_ev[slot])
-                with torch.cuda.stream(s_scan):
-                    out = dense_topk_first(index, ql, k, p_ws[slot], p_out[slot], s_merge,
-                                           p_scan_ev[slot])
-                ev = torch.cuda.Event()
-                ev.record(s_merge)
-                p_merge_ev[slot] = ev
-                finish()  # the previous batch's second pass, behind this batch's scan
-                p_pending[0] = (slot, ql)
-                return out
-            if sharded is None and pipe and not split:
-                st, ev = p_streams[i % 2], p_ev[i % 2]
-                if not p_synced[i % 2]:  # the inputs were made on the default stream
-                    st.wait_stream(torch.cuda.current_stream())
-                    p_synced[i % 2] = True
-                if p_prev[0] is not None:
-                    st.wait_event(p_prev[0])
-                with torch.cuda.stream(st):
-                    out = index.topk(ql, k, workspace=p_ws[i % 2], scan_done=ev)
-                p_prev[0] = ev
-                return out
             if sharded is None:
                 return index.topk(ql, k, workspace=ws)
             return sharded.dense(ql, k)
@@ -487,8 +420,6 @@ def main() -> None:
 
     for i in range(args.warmup):
         step(i)
-    if split:
-        finish()
     barrier()
     _armi.call("armi_scan_timing_enable", 1)
     for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN):
@@ -500,8 +431,6 @@ def main() -> None:
     last = None
     for i in range(args.steps):
         last = step(i)
-    if split:
-        finish()
     barrier()
     elapsed = time.perf_counter() - t0
     rr_timing["on"] = False
@@ -518,10 +447,8 @@ def main() -> None:
         # over every query batch of the run (first-pass certificate; the rest took the second pass)
         if sharded is None:
             fls = []
-            for i in range(n_q_batches):  # (pipelined modes: outputs land on other streams)
+            for i in range(n_q_batches):
                 o = step(i)
-                if split:
-                    finish()
                 torch.cuda.synchronize()
                 fls.append(o.flags.clone())
             fl = torch.cat(fls)
@@ -535,8 +462,6 @@ def main() -> None:
         barrier()
         t1 = time.perf_counter()
         step(i)
-        if split:
-            finish()
         barrier()
         lat.append(time.perf_counter() - t1)
     for i in range(args.latency_iters):
@@ -560,17 +485,18 @@ def main() -> None:
     if form == _armi.SCAN_INT8_FILTER:
         # int8 filter image (1 B / component) + a32, e32 (8 B / row) + the fp16 queries
         alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim * 2
-        scan_kernel = f"dense_scan_i8_kernel<{dim}>"
+        scan_kernel = f"dense_scan_i8_kernel<{dim}, false>"
     else:
         alg_bytes = shard_rows * dim * 2 + shard_rows * 4 + nq_scan * dim * 2
         scan_kernel = (f"dense_scan_kernel<{dim}>" if form == _armi.SCAN_FP16
-                       else f"dense_gemm_scan_w4_kernel<{dim}>")
+                       else f"dense_gemm_scan_w4_kernel<{dim}, 0>")
     alg_flops = 2.0 * shard_rows * dim * nq_scan
     # the scan's bound: HBM while the batch is small (arithmetic intensity ~ queries/pass flop/B),
     # the fp16 MFMA once the all-gathered batch of a multi-GPU step passes the ridge
     mfma_bound = alg_flops / (MFMA_PEAK_TFLOPS["fp16"] * 1e12) > alg_bytes / (HBM_PEAK_GBS * 1e9)
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic = read_traffic(form)
+    traffic, traffic_src = (read_traffic(traffic_key(form, shard_rows, dim, nq_scan, args.corpus))
+                            if world == 1 else (None, None))
     result = {
         "metric": METRIC,
         "value": total_queries / elapsed,
@@ -602,8 +528,6 @@ def main() -> None:
                                   f"queries per GPU per step"),
             }[wl],
             "n_chunks": n, "dim": dim, "batch_per_gpu": batch, "top_k": k, "corpus": args.corpus,
-            "batches_in_flight": 2 if pipe else 1,
-            "merge_cus": args.merge_cus if split else 0,
             "parallelism": f"corpus-shard{world}" + ("" if backend == "nccl" or world == 1
                                                       else f" ({backend} rehearsal, shared GPUs)"),
         },
@@ -617,7 +541,9 @@ def main() -> None:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic if nq_scan <= 64 else None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_over_algorithmic": traffic / alg_bytes if traffic else None,
             "algorithmic_bytes_per_launch": alg_bytes,
             "avg_launch_ms": scan_avg_ms,
             "launches_timed": launches.value,
@@ -699,7 +625,8 @@ def main() -> None:
             eos = torch.full((nr, kc, 1), 2, dtype=torch.int64)
             pairs = (hf_reranker, torch.cat([bos, qt[:, None, :].expand(nr, kc, qt.shape[1]), eos, eos,
                                              doc_tokens(ords, 236).to(torch.int64), eos], dim=2))
-        result["cpu_baseline"] = cpu_baseline(wl, ref, qn, q_csr, k, search_k, pairs)
+        result["cpu_baseline"] = cpu_baseline(wl, ref, qn, q_csr, k, search_k, pairs,
+                                              budget_s=args.cpu_budget)
         del ref
     if wl == "dense" and world == 1 and not args.no_extras and args.corpus == "random":
         result.update(secondary_configs(args))
@@ -716,11 +643,14 @@ def secondary_configs(args) -> dict:
     "chunks_10k" / "chunks_10M" (value, ms_per_step, p50, rooflines)."""
     import subprocess
 
+    # configs1 / configs2 carry their own cpu_baseline (dense at 100k; the reference's hybrid +
+    # cross-encoder path at 1M), each leg bounded by a shorter budget
+    cpu = ["--cpu-budget", "10"]
     runs = {
         "configs1": ["--chunks", "100000", "--steps", "200", "--warmup", "10",
-                     "--latency-iters", "20"],
+                     "--latency-iters", "20", *cpu],
         "configs2": ["--workload", "hybrid_rerank", "--chunks", str(args.chunks), "--steps", "10",
-                     "--warmup", "2", "--latency-iters", "3"],
+                     "--warmup", "2", "--latency-iters", "3", *cpu],
         # north_star's size sweep (10k / 100k / 1M / 10M chunks): the two ends besides configs1
         # and the headline
         "chunks_10k": ["--chunks", "10000", "--steps", "200", "--warmup", "10",
@@ -730,9 +660,11 @@ def secondary_configs(args) -> dict:
     }
     out = {}
     for key, extra in runs.items():
-        cmd = [sys.executable, str(ROOT / "bench.py"), "--no-extras", "--no-cpu-baseline", *extra]
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--no-extras", *extra]
+        if key not in ("configs1", "configs2"):
+            cmd.append("--no-cpu-baseline")
         try:
-            res = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
             line = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else ""
             d = json.loads(line) if res.returncode == 0 and line.startswith("{") else None
         except (subprocess.TimeoutExpired, json.JSONDecodeError):
@@ -742,7 +674,7 @@ def secondary_configs(args) -> dict:
             continue
         keep = ("value", "unit", "ms_per_step", "steps", "p50_ms", "p50_single_query_ms",
                 "certified_frac", "config", "roofline", "roofline_scan", "roofline_sparse",
-                "rerank_share_of_step", "dtype")
+                "rerank_share_of_step", "dtype", "cpu_baseline")
         out[key] = {kk: d[kk] for kk in keep if kk in d}
         if key in ("configs1", "configs2"):
             out[key]["baseline_config"] = {"configs1": 1, "configs2": 2}[key]

@@ -59,6 +59,9 @@ extern "C" {
 
 const char* armi_last_error(void);
 int armi_abi_version(void);
+/* sha256 prefix of the sources the library was built from (audio_rag_amd/_armi.py
+ * source_digest); the Python loader refuses a library whose digest differs from csrc/. */
+const char* armi_source_digest(void);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Dense chunk store                                                                          */
@@ -119,50 +122,6 @@ int armi_dense_topk(const armi_index* index, const uint16_t* queries, int n_quer
                     const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                     double* out_rank, int32_t* out_count, uint32_t* out_flags,
                     void* workspace, size_t workspace_bytes, hipStream_t stream);
-
-/* armi_dense_topk that also records scan_done (a hipEvent_t, nullable) on `stream` right after
- * the call's first-pass scan kernel, before its merge / second-pass kernels: a pipelined caller
- * (two batches on two streams) makes the next batch's stream wait on it, so the next scan starts
- * as this one ends and this call's merge runs beside it. */
-int armi_dense_topk_ex(const armi_index* index, const uint16_t* queries, int n_queries, int k,
-                       const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                       double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                       void* workspace, size_t workspace_bytes, hipStream_t stream,
-                       hipEvent_t scan_done);
-
-/* armi_dense_topk_ex in two calls over two streams, for a caller that keeps one batch's merge off
- * the next batch's scan CUs (CU-split stream pair of armi_cu_split_streams, scan CUs set with
- * armi_index_set_scan_cus):
- *   armi_dense_topk_first: the first-pass scan on `stream`, scan_done recorded there, then the
- *     merge on merge_stream after waiting on scan_done (required when the streams differ). The
- *     outputs hold the certified answers; uncertified queries need the second pass.
- *   armi_dense_second_pass: `stream` waits on merge_done (nullable: recorded by the caller on
- *     merge_stream after the first call), runs the collect pass (exits at once when every query
- *     is certified), records pass_done; merge_stream waits on it and rescores the collect lists.
- * Both calls take the same workspace, which stays in use until the second call's work on
- * merge_stream is done (bench.py rotates three). The answers equal armi_dense_topk's. */
-int armi_dense_topk_first(const armi_index* index, const uint16_t* queries, int n_queries, int k,
-                          const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                          double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                          void* workspace, size_t workspace_bytes, hipStream_t stream,
-                          hipStream_t merge_stream, hipEvent_t scan_done);
-int armi_dense_second_pass(const armi_index* index, const uint16_t* queries, int n_queries, int k,
-                           const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
-                           double* out_rank, int32_t* out_count, uint32_t* out_flags,
-                           void* workspace, size_t workspace_bytes, hipStream_t stream,
-                           hipStream_t merge_stream, hipEvent_t merge_done, hipEvent_t pass_done);
-
-/* Scan workgroups of the index's dense first pass: one per CU it may use; cus = 0 restores every
- * CU of the device, cus > device CUs clamps. Changes armi_dense_workspace_bytes (size workspaces
- * after calling it). */
-int armi_index_set_scan_cus(armi_index* index, int cus);
-
-/* Two streams over disjoint CU sets of `device` (hipExtStreamCreateWithCUMask): merge_stream on
- * `reserve` CUs (the mask's top bits, which the runtime spreads over the XCDs), scan_stream on
- * all the others. The caller
- * destroys both with hipStreamDestroy. */
-int armi_cu_split_streams(int device, int reserve, hipStream_t* scan_stream,
-                          hipStream_t* merge_stream);
 
 size_t armi_dense_exact_workspace_bytes(const armi_index* index, int n_queries, int k);
 /* Exhaustive exact scan with the same outputs and ranking as armi_dense_topk. */
@@ -241,10 +200,13 @@ int armi_stream_submit_hybrid(armi_stream* server, const uint16_t* query,
                               const int32_t* sp_indices, const float* sp_values, int nnz,
                               int64_t* ticket);
 /* Branch and filter per query (QdrantRetriever.search's choice, qdrant.py:262-332):
- * mode ARMI_STREAM_AUTO = hybrid when the query carries terms (hybrid server), else dense;
- * ARMI_STREAM_DENSE = the dense branch whatever the terms; ARMI_STREAM_SPARSE = sparse-only
- * (top-k of the sparse dot, hit.score = that dot) when the query carries terms, else dense (the
- * reference's fallback). Sparse terms need a hybrid server. row_mask (nullable) = a device
+ * a query "carries a sparse vector" when sp_indices and sp_values are both non-null, even with
+ * nnz = 0 (the reference's `if query.sparse` is true for an empty SparseVector object).
+ * mode ARMI_STREAM_AUTO = hybrid when the query carries a sparse vector (hybrid server), else
+ * dense; ARMI_STREAM_DENSE = the dense branch whatever the terms; ARMI_STREAM_SPARSE =
+ * sparse-only (top-k of the sparse dot, hit.score = that dot) when the query carries a sparse
+ * vector, else dense (the reference's fallback). An empty sparse vector gives RRF over the dense
+ * list alone (hybrid) or an empty result (sparse-only). Sparse terms need a hybrid server. row_mask (nullable) = a device
  * bitmask over the store's ordinals (armi_dense_topk's row_mask: the Qdrant payload filter),
  * caller-owned, unchanged and alive until the ticket's wait has returned; it applies to every
  * list of the query (dense, sparse, both prefetches). A batch holds queries of one row_mask: a
@@ -258,9 +220,10 @@ int armi_stream_submit_ex(armi_stream* server, const uint16_t* query, const int3
 /* Blocks until the ticket's result is published (at most timeout_us), then copies its k
  * scores / ids / rank keys (each nullable), the valid count and the branch taken (mode:
  * 0 dense, 1 hybrid, 2 sparse-only; nullable). Results stay readable until R later tickets have been
- * submitted, R = max(2^14, 64 max_batch) rounded up to a power of two (the result ring: R k
- * (4 + 8 + 8) B + 48 R B of host memory, 3.9 MB at k = 10, max_batch 64); an older ticket fails
- * with "result overwritten". */
+ * published, R = the largest power of two whose ring (R (k (4 + 8 + 8) + 48) B of host memory)
+ * fits 128 MiB, at least max(2^14, 64 max_batch): 2^19 tickets at k = 10. An older ticket fails
+ * with "result overwritten"; the copy is re-validated after it is taken, so a caller never
+ * receives another ticket's results. */
 int armi_stream_wait(armi_stream* server, int64_t ticket, float* scores, int64_t* ids,
                      double* rank, int32_t* count, int32_t* mode, double timeout_us);
 int armi_stream_stats(armi_stream* server, int64_t* batches, int64_t* queries);

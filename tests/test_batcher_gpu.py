@@ -288,3 +288,68 @@ def test_stream_server_filters_and_search_types(gpu, oracle_mod, store):
     with StreamServer(ret, max_batch=8, max_wait_ms=0.5) as dense_srv:
         with pytest.raises(Exception, match="needs a server"):
             dense_srv.submit(queries[1], None, "sparse")
+
+
+def test_stream_server_empty_sparse_vector(gpu, oracle_mod, store):
+    """A query carrying an EMPTY SparseVector takes the hybrid / sparse-only branch, as
+    MI355XRetriever.search and the reference do (`if query.sparse` is true for any SparseVector
+    object, qdrant.py:272/299): hybrid = RRF over the dense 2k prefetch alone (RRF scores),
+    sparse-only = no results. Checked in batches with and without other queries' terms (the
+    native server skips the batch's sparse pass when no query has a term)."""
+    from audio_rag_amd.core import EmbeddingResult, SparseVector
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    rows, _, (qi, qx, qv), qd = store
+    qf = qd.view(np.float16).astype(np.float32)
+    empty = [EmbeddingResult(dense=qf[i].tolist(), sparse=SparseVector([], [])) for i in range(6)]
+    d = oracle_mod.dense_topk(rows, qd[:6], 2 * K)
+    want = [[(f"c{p}", s) for p, s in oracle_mod.rrf([d.ids[i, :d.count[i]].tolist(), []], K)]
+            for i in range(6)]
+    for i in range(6):  # the reference path (device search, one query at a time)
+        via_search = ret.search(empty[i], search_type="hybrid")
+        assert [(r.chunk.text, r.score) for r in via_search] == want[i], i
+        assert ret.search(empty[i], search_type="sparse") == []
+    with StreamServer(ret, max_batch=8, max_wait_ms=2.0, search_type="hybrid") as srv:
+        # batch 1: only empty vectors (no sparse pass); batch 2: mixed with a query with terms
+        t_h = [srv.submit(empty[i], None, "hybrid") for i in range(6)]
+        got_h = [srv.result(t) for t in t_h]
+        t_s = [srv.submit(empty[i], None, "sparse") for i in range(3)]
+        got_s = [srv.result(t) for t in t_s]
+        with_terms = EmbeddingResult(dense=qf[1].tolist(),
+                                     sparse=SparseVector(qx[qi[1]:qi[2]].tolist(),
+                                                         qv[qi[1]:qi[2]].tolist()))
+        mixed = [srv.submit(empty[i], None, "hybrid") for i in range(3)]
+        t_w = srv.submit(with_terms, None, "hybrid")
+        got_m = [srv.result(t) for t in mixed]
+        got_w = srv.result(t_w)
+    for i in range(6):
+        assert [(r.chunk.text, r.score) for r in got_h[i]] == want[i], i
+    assert got_s == [[], [], []]
+    for i in range(3):
+        assert [(r.chunk.text, r.score) for r in got_m[i]] == want[i], i
+    assert [(r.chunk.text, r.score) for r in got_w] == _expected(oracle_mod, store, 1, "hybrid", None)
+
+
+def test_stream_server_ring_wrap_is_detected(gpu, oracle_mod, store):
+    """A caller that lets a ticket fall a whole result ring behind gets "result overwritten",
+    never another ticket's results (the ring entries are published and read seqlock-style). At
+    k = 240 the ring holds 2^14 tickets; 2^14 + 200 submissions wrap it."""
+    from audio_rag_amd.core.exceptions import RetrievalError
+    from audio_rag_amd.retrieval.batcher import StreamServer
+
+    ret = _retriever(store)
+    rows, _, _, qd = store
+    k = 240
+    n = (1 << 14) + 200
+    with StreamServer(ret, top_k=k, max_batch=64, max_wait_ms=0.2) as srv:
+        tickets = [srv.submit_arrays(qd[i % NQ].view(np.float16)) for i in range(n)]
+        _, ids_last, c_last = srv.raw_result(tickets[-1])  # every earlier batch is published
+        with pytest.raises(RetrievalError, match="overwritten"):
+            srv.raw_result(tickets[0])
+        _, ids_kept, c_kept = srv.raw_result(tickets[-(1 << 13)])
+    want = oracle_mod.dense_topk(rows, qd, k)
+    j_last, j_kept = (n - 1) % NQ, (n - (1 << 13)) % NQ
+    assert c_last == want.count[j_last] and c_kept == want.count[j_kept]
+    np.testing.assert_array_equal(ids_last[:c_last], want.ids[j_last, :c_last])
+    np.testing.assert_array_equal(ids_kept[:c_kept], want.ids[j_kept, :c_kept])

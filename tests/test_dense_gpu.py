@@ -217,57 +217,17 @@ def test_full_size_fast_equals_exact(gpu, oracle_mod):
     np.testing.assert_array_equal(fast.rank[:2].cpu().numpy(), ref.rank)
 
 
-def test_pipelined_batches_on_two_streams(gpu, oracle_mod):
-    """armi_dense_topk_ex: batches alternating over two streams, each waiting for the previous
-    batch's scan-done event (bench.py's pipelined dense step), with a row filter on every other
-    batch: every answer equals the oracle's (the dynamic tile schedule's heads live in each
-    call's own workspace)."""
-    rows = oracle_mod.unit_fp16(30000, 1024, seed=71)
-    idx = _index(rows, gpu)
-    streams = [torch.cuda.Stream(device=gpu) for _ in range(2)]
-    evs = [torch.cuda.Event() for _ in range(2)]
-    ws = [torch.empty(idx.workspace_bytes(64, 10), dtype=torch.uint8, device=gpu) for _ in range(2)]
-    mask = np.zeros((30000 + 63) // 64, dtype=np.uint64)
-    mask[::3] = np.uint64(0xF0F0F0F0F0F0F0F0)
-    m_dev = _dev(mask.view(np.int64), gpu)
-    qs = [oracle_mod.unit_fp16(64, 1024, seed=72 + i) for i in range(6)]
-    q_dev = [_dev(q.view(np.float16), gpu) for q in qs]
-    torch.cuda.synchronize()
-    outs, prev = [], None
-    for i in range(6):
-        st = streams[i % 2]
-        if prev is not None:
-            st.wait_event(prev)
-        with torch.cuda.stream(st):
-            outs.append(idx.topk(q_dev[i], 10, row_mask=m_dev if i % 2 else None,
-                                 workspace=ws[i % 2], scan_done=evs[i % 2]))
-        prev = evs[i % 2]
-    torch.cuda.synchronize()
-    for i in range(6):
-        ref = oracle_mod.dense_topk(rows, qs[i], 10, row_mask=mask if i % 2 else None)
-        got = {f: getattr(outs[i], f).cpu().numpy() for f in ("ids", "scores", "rank", "count")}
-        _assert_same(got, ref, 10)
-
-
-def test_cu_split_scan_and_merge_streams(gpu, oracle_mod):
-    """armi_dense_topk_first / armi_dense_second_pass over armi_cu_split_streams, as bench.py
-    --pipeline 2 --merge-cus 8 runs them: every scan and collect pass on the scan stream's CUs
-    (armi_index_set_scan_cus: one workgroup per such CU), each batch's merge and collect merge on
-    the 8 reserved CUs, batch i's second pass issued after batch i+1's scan, three workspaces
-    rotating; a row filter on every other batch and one batch whose queries sit on a pile of 100
+def test_batches_on_two_streams(gpu, oracle_mod):
+    """Batches alternating over two HIP streams with their own workspaces (a serving front end's
+    pattern), a row filter on every other batch and one batch whose queries sit on a pile of 100
     exact duplicate rows (more than the 64 rescored: the second pass finds them). Every answer
-    equals the oracle's; restoring every CU (cus = 0) answers the same on one stream."""
-    from audio_rag_amd.retrieval.device import (TopK, cu_split_streams, dense_second_pass,
-                                                dense_topk_first)
-
+    equals the oracle's."""
     n = 40000
     rows = oracle_mod.unit_fp16(n, 1024, seed=81)
     rows[1000:1100] = rows[1000]
     idx = _index(rows, gpu)
-    n_cus = torch.cuda.get_device_properties(gpu).multi_processor_count
-    s_scan, s_merge = cu_split_streams(gpu, 8)
-    idx.set_scan_cus(n_cus - 8)
-    ws = [torch.empty(idx.workspace_bytes(64, 10), dtype=torch.uint8, device=gpu) for _ in range(3)]
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(2)]
+    ws = [torch.empty(idx.workspace_bytes(64, 10), dtype=torch.uint8, device=gpu) for _ in range(2)]
     mask = np.zeros((n + 63) // 64, dtype=np.uint64)
     mask[::3] = np.uint64(0xF0F0F0F0F0F0F0F0)
     m_dev = _dev(mask.view(np.int64), gpu)
@@ -275,48 +235,19 @@ def test_cu_split_scan_and_merge_streams(gpu, oracle_mod):
     qs[2][:8] = rows[1000]  # queries equal to the duplicated row (an unfiltered batch)
     q_dev = [_dev(q.view(np.float16), gpu) for q in qs]
     torch.cuda.synchronize()
-
-    def fresh():
-        return TopK(scores=torch.empty((64, 10), dtype=torch.float32, device=gpu),
-                    ids=torch.empty((64, 10), dtype=torch.int64, device=gpu),
-                    rank=torch.empty((64, 10), dtype=torch.float64, device=gpu),
-                    count=torch.empty(64, dtype=torch.int32, device=gpu),
-                    flags=torch.empty(64, dtype=torch.int32, device=gpu))
-
-    outs = [fresh() for _ in range(7)]
-    scan_ev = [torch.cuda.Event() for _ in range(3)]
-    pass_ev = [torch.cuda.Event() for _ in range(3)]
-    merge_ev, done_ev = [None] * 3, [None] * 3
-
-    def second(j):
-        sl = j % 3
-        with torch.cuda.stream(s_scan):
-            dense_second_pass(idx, q_dev[j], 10, ws[sl], outs[j], s_merge, merge_ev[sl],
-                              pass_ev[sl], row_mask=m_dev if j % 2 else None)
-        done_ev[sl] = torch.cuda.Event()
-        done_ev[sl].record(s_merge)
-
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    outs = []
     for i in range(7):
-        sl = i % 3
-        if done_ev[sl] is not None:
-            s_scan.wait_event(done_ev[sl])
-        with torch.cuda.stream(s_scan):
-            dense_topk_first(idx, q_dev[i], 10, ws[sl], outs[i], s_merge, scan_ev[sl],
-                             row_mask=m_dev if i % 2 else None)
-        merge_ev[sl] = torch.cuda.Event()
-        merge_ev[sl].record(s_merge)
-        if i:
-            second(i - 1)
-    second(6)
+        with torch.cuda.stream(streams[i % 2]):
+            outs.append(idx.topk(q_dev[i], 10, row_mask=m_dev if i % 2 else None,
+                                 workspace=ws[i % 2]))
     torch.cuda.synchronize()
     for i in range(7):
         ref = oracle_mod.dense_topk(rows, qs[i], 10, row_mask=mask if i % 2 else None)
         got = {f: getattr(outs[i], f).cpu().numpy() for f in ("ids", "scores", "rank", "count")}
         _assert_same(got, ref, 10)
     assert (outs[2].flags[:8].cpu().numpy() != 1).all()  # the duplicate pile: second pass taken
-    idx.set_scan_cus(0)
-    got = _run(idx, qs[2], 10, gpu)
-    _assert_same(got, oracle_mod.dense_topk(rows, qs[2], 10), 10)
 
 
 @pytest.mark.parametrize("mode", ["two_stage", "exact"])

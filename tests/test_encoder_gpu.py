@@ -195,27 +195,6 @@ def test_attention_f16_matches_fp32_reference(gpu, L):
     torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
 
 
-@pytest.mark.parametrize("L", [7, 100, 256])
-def test_attention_f16_persistent_matches_fp32_reference(gpu, L, monkeypatch):
-    """The persistent double-buffered attention (>= 2 (sequence, head) pairs per CU, L <= 256:
-    next pair's K / V / Q loads in flight during the current pair's compute) on ragged masks,
-    against fp32 eager attention; every sequence is checked."""
-    g = torch.Generator().manual_seed(500 + L)
-    n, H, dh = 45, 12, 64  # 540 pairs > 2 x 256 CUs
-    monkeypatch.setenv("ARMI_ATTENTION", "persist")  # (the one-shot kernel is the default)
-    qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
-    mask = torch.ones(n, L, dtype=torch.int32)
-    for i in range(0, n, 3):
-        mask[i, max(1, (L * (i + 1)) // (n + 1)):] = 0
-    mask[1, 1:] = 0  # one key only
-    ref = _attention_ref(qkv, mask, H, dh)
-    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
-    out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
-    _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
-          1 / math.sqrt(dh))
-    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
-
-
 def test_attention_f16_peaked_scores(gpu):
     """Large, one-hot-like scores (the running max jumps late in the key sweep)."""
     n, L, H, dh = 2, 160, 12, 64

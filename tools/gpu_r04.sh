@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-4 GPU session: full -m gpu suite + smoke, the default bench line (driver shape, with the
+# configs1 / configs2 children and their CPU baselines), the single-query search breakdown,
+# rocprofv3 kernel stats of the dense bench and the per-shape PMC traffic passes.
+# Each GPU step has its own limit; any failure ends the session.
+TAG=${1:-r04a}
+STEPS=${2:-all}
+R="$GRAFT_REPO_ROOT"
+cd "$R" || exit 1
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+if [[ $STEPS == all || $STEPS == *tests* ]]; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
+  echo "pytest rc=$rc: $(tail -1 gpurun_out/${TAG}_pytest.log)"
+  grep -E "FAILED|ERROR" gpurun_out/${TAG}_pytest.log | head -20
+  ok $rc || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+  echo "smoke: $(tail -1 gpurun_out/${TAG}_smoke.log)"
+fi
+if [[ $STEPS == all || $STEPS == *bench* ]]; then
+  /usr/bin/time -f "bench wall %e s" timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
+  tail -1 gpurun_out/${TAG}_bench.err
+  python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_bench.json'));print('dense',round(d['value']),'ms',round(d['ms_per_step'],4),'frac',round(d['roofline']['frac'],3),'traffic',d['roofline']['traffic'],'cpu',d['cpu_baseline']['value']);[print(k,round(d[k].get('value',0)),d[k].get('cpu_baseline',{}) and d[k]['cpu_baseline']['value'],d[k].get('roofline',{}).get('traffic')) for k in ('configs1','configs2','chunks_10k','chunks_10M')]"
+fi
+if [[ $STEPS == all || $STEPS == *lat* ]]; then
+  timeout -k 10 300 python tools/search_latency.py > gpurun_out/${TAG}_search_latency.json 2>&1 || exit $?
+  cat gpurun_out/${TAG}_search_latency.json
+fi
+if [[ $STEPS == all || $STEPS == *prof* ]]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof_dense" -o run -- \
+    python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-extras --latency-iters 3 > "$R/gpurun_out/${TAG}_prof_dense.log" 2>&1 || exit $?
+  echo "prof dense done"
+  cd "$R"
+fi
+if [[ $STEPS == all || $STEPS == *pmc* ]]; then
+  bash tools/pmc_traffic.sh ${TAG}_t1m roofline || exit $?
+  bash tools/pmc_traffic.sh ${TAG}_t100k roofline --chunks 100000 || exit $?
+  bash tools/pmc_traffic.sh ${TAG}_tsp roofline_sparse --workload hybrid || exit $?
+fi
+exit 0
