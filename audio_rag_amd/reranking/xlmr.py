@@ -74,7 +74,8 @@ class CrossEncoderXLMR:
             ))
         self.gemm_dtype = torch.float32
         self.residual = "fp32"
-        self.head = (sd["classifier.dense.weight"], sd["classifier.dense.bias"],
+        # dense weight transposed ([in][out]): armi_enc_cls_head_sigmoid reads it coalesced
+        self.head = (sd["classifier.dense.weight"].t().contiguous(), sd["classifier.dense.bias"],
                      sd["classifier.out_proj.weight"].reshape(-1).contiguous(),
                      sd["classifier.out_proj.bias"])
 

@@ -316,8 +316,10 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
                    int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
 /* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)
- * hidden [n_seq][L][width] -> out [n_seq]; width <= 2048 (8 sequences per workgroup). */
-int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_w, const float* dense_b,
+ * hidden [n_seq][L][width] -> out [n_seq]; dense_wt = dense_w transposed, [width_in][width_out]
+ * row-major (nn.Linear's weight.t()); width a multiple of 4, <= 1024 (8 sequences per
+ * workgroup, one thread per output feature). */
+int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_wt, const float* dense_b,
                               const float* out_w, const float* out_b, float* out, int n_seq,
                               int L, int width, hipStream_t stream);
 
