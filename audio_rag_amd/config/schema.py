@@ -53,6 +53,10 @@ class RetrievalConfig(BaseModel):
     device: int = 0
     rrf_k: int = Field(default=2, ge=1)
     reproduce_sparse_drop: bool = True
+    # unfiltered single-query search() replays a HIP graph captured per (collection, branch,
+    # top_k): one host->device copy of the query, one replay of the search kernels, one
+    # device->host copy of the packed result
+    query_graphs: bool = True
 
 
 class RerankingConfig(BaseModel):

@@ -13,12 +13,15 @@ stream with fp32 LayerNorm statistics: max |score error| 6.5e-5 - 9.6e-5 vs the 
 
 from __future__ import annotations
 
+import logging
 import math
-import os
+from collections import OrderedDict
 
 import torch
 
 from audio_rag_amd._armi import call, ptr, stream_handle
+
+logger = logging.getLogger(__name__)
 
 # XLM-RoBERTa-base as used by BAAI/bge-reranker-base
 RERANKER_ARCH = dict(vocab_size=250002, hidden_size=768, num_hidden_layers=12,
@@ -139,8 +142,8 @@ class CrossEncoderXLMR:
     # hipBLASLt linear + armi_enc_gelu_f16. "mixed" (default) = armi for the FFN-up GEMM only, whose
     # fused GELU saves the activation round trip (2.14 ms vs 2.22 + 0.55 ms per layer at 1,280 x
     # 256 tokens), hipBLASLt for the other three, where it is 18-28 % faster than the hand-written
-    # GEMM (profiles/r03c_gemm.log). ARMI_RERANK_GEMM selects.
-    gemm_impl = os.environ.get("ARMI_RERANK_GEMM", "mixed")
+    # GEMM (profiles/r03c_gemm.log). A class attribute (tests set it per instance).
+    gemm_impl = "mixed"
 
     def _lin(self, x: torch.Tensor, ly: dict, name: str, gelu: bool = False) -> torch.Tensor:
         """y = x . W^T + b (+ exact GELU) for weight `name` of layer ly, fp16 in / out."""
@@ -158,49 +161,13 @@ class CrossEncoderXLMR:
             call("armi_enc_gelu_f16", ptr(y), None, y.shape[0], y.shape[1], stream_handle())
         return y
 
-    # Two-stream form (A/B, off by default): at or above this many tokens the sequences split into
-    # two halves whose layer ops interleave on two streams. Measured slower at the configs[2]
-    # shape (912 vs 929 q/s, profiles/r02h_rerank_ab.txt): the GEMMs hold every CU, so the other
-    # half's HBM-bound kernels find nothing to overlap. ARMI_RERANK_SPLIT_MIN_TOKENS enables it.
-    split_min_tokens = int(os.environ.get("ARMI_RERANK_SPLIT_MIN_TOKENS", str(1 << 62)))
-
     def _layers_f16_residual(self, h16: torch.Tensor, mask: torch.Tensor, n: int,
                              L: int) -> torch.Tensor:
         """Encoder layers with an all-fp16 residual stream (armi_enc_add_layernorm_f16: fp16 in
-        and out, fp32 statistics), then the classification head on the fp32 <s> rows.
-        Large batches run as two half-batches on two streams with their ops issued alternately,
-        so one half's HBM-bound kernels (attention, GELU, add + LayerNorm) overlap the other
-        half's MFMA-bound GEMMs; every sequence's arithmetic is unchanged."""
-        if n < 2 or n * L < self.split_min_tokens:
-            gen = self._layer_ops(h16, mask, n, L)
-            for _ in gen:
-                pass
-            return self._result
-        main = torch.cuda.current_stream()
-        if getattr(self, "_streams", None) is None:
-            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
-        half = n // 2
-        parts = [(h16[:half * L], mask[:half], half), (h16[half * L:], mask[half:], n - half)]
-        gens, outs = [], [None, None]
-        for i, (st, (hh, mm, nn)) in enumerate(zip(self._streams, parts)):
-            st.wait_stream(main)
-            hh.record_stream(st)
-            mm.record_stream(st)
-            gens.append((i, st, self._layer_ops(hh, mm, nn, L)))
-        while gens:
-            alive = []
-            for i, st, g in gens:
-                with torch.cuda.stream(st):
-                    try:
-                        next(g)
-                        alive.append((i, st, g))
-                    except StopIteration as e:
-                        outs[i] = e.value
-            gens = alive
-        for st, o in zip(self._streams, outs):
-            main.wait_stream(st)
-            o.record_stream(main)
-        return torch.cat(outs)
+        and out, fp32 statistics), then the classification head on the fp32 <s> rows."""
+        for _ in self._layer_ops(h16, mask, n, L):
+            pass
+        return self._result
 
     def _layer_ops(self, h16: torch.Tensor, mask: torch.Tensor, n: int, L: int):
         """Generator over the launches of _layers_f16_residual on the caller's current stream
@@ -272,9 +239,69 @@ class CrossEncoderXLMR:
         y = torch.mm(x.to(self.gemm_dtype), ly[name + "_g"]).float()
         return y.add_(bias) if bias is not None else y
 
+    # Captured forwards (HIP graphs through torch.cuda.CUDAGraph), keyed by (n, L bucket): one
+    # replay issues every kernel of the forward with no host work between them (the eager
+    # forward's ~130 launches, hipBLASLt's per-call argument uploads and allocator calls
+    # otherwise leave the GPU idle between kernels). Sequences are right-padded with <pad>
+    # (mask 0) to the bucket: the real tokens' outputs, and so the <s> row the head reads, are
+    # those of the unpadded batch.
+    use_graphs = True
+    GRAPH_L_STEP = 32
+    MAX_GRAPHS = 8
+
+    def _graph_for(self, n: int, L: int):
+        key = (n, L)
+        g = self._graphs.get(key) if hasattr(self, "_graphs") else None
+        if g is not None:
+            self._graphs.move_to_end(key)
+            return g
+        if not hasattr(self, "_graphs"):
+            self._graphs = OrderedDict()
+        ids_t = torch.full((n, L), self.pad, dtype=torch.int32, device=self.device)
+        mask_t = torch.zeros((n, L), dtype=torch.int32, device=self.device)
+        ids_t[:, 0] = 0
+        mask_t[:, 0] = 1
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm-up: library handles, kernel attributes, allocator blocks
+                self._forward_eager(ids_t, mask_t)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            probs = self._forward_eager(ids_t, mask_t)
+        g = (graph, ids_t, mask_t, probs)
+        self._graphs[key] = g
+        while len(self._graphs) > self.MAX_GRAPHS:
+            self._graphs.popitem(last=False)
+        return g
+
+    def _forward_graphed(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        n, L = ids.shape
+        Lb = min(-(-L // self.GRAPH_L_STEP) * self.GRAPH_L_STEP, self.pos.shape[0] - self.pad - 1)
+        if Lb < L:
+            return self._forward_eager(ids, mask)
+        graph, ids_t, mask_t, probs = self._graph_for(n, Lb)
+        if Lb > L:
+            ids_t[:, L:].fill_(self.pad)
+            mask_t[:, L:].zero_()
+        ids_t[:, :L].copy_(ids)
+        mask_t[:, :L].copy_(mask)
+        graph.replay()
+        return probs.clone()
+
     @torch.inference_mode()
     def forward(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
         """ids, mask: int32 [n, L] on the device -> sigmoid scores float32 [n]."""
+        if self.use_graphs and self.gemm_dtype == torch.float16 and self.residual == "fp16":
+            try:
+                return self._forward_graphed(ids, mask)
+            except RuntimeError as e:  # capture refused: the same kernels, launched eagerly
+                logger.warning(f"cross-encoder graph capture failed ({e}); running eagerly")
+                self.use_graphs = False
+        return self._forward_eager(ids, mask)
+
+    def _forward_eager(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
         if self.gemm_dtype == torch.float16:
             return self._forward_f16(ids, mask)
         n, L = ids.shape

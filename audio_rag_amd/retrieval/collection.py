@@ -75,6 +75,9 @@ class ChunkCollection:
     _lock: threading.Lock = field(default_factory=threading.Lock)
     _frozen: bool = False
     _servers: weakref.WeakSet = field(default_factory=weakref.WeakSet)  # open StreamServers
+    # captured single-query searches over the current indexes (MI355XRetriever._graph_search),
+    # dropped whenever the indexes are rebuilt or closed
+    _graphs: dict = field(default_factory=dict)
 
     @property
     def count(self) -> int:
@@ -113,6 +116,7 @@ class ChunkCollection:
             rows = (np.concatenate(self.dense_rows) if self.dense_rows
                     else np.zeros((0, self.dim), dtype=np.float16))
             old_dense, old_sparse = self._dense, self._sparse
+            self._graphs = {}
             self._dense = DenseIndex(torch.from_numpy(rows).to(self.device))
             if self.hybrid:
                 indptr = np.zeros(self.count + 1, dtype=np.int64)
@@ -130,6 +134,11 @@ class ChunkCollection:
             # this rebuild may still be using them. Dropping the reference frees each one (its
             # __del__ closes it) once the last such search lets go of it.
             del old_dense, old_sparse
+
+    def query_graphs(self) -> dict:
+        """The captured single-query searches of the current indexes (key -> graph)."""
+        self._ensure_built()
+        return self._graphs
 
     @property
     def dense_index(self) -> DenseIndex:
@@ -250,6 +259,7 @@ class ChunkCollection:
         # before the indexes are freed
         for srv in list(self._servers):
             srv.close()
+        self._graphs = {}
         for ix in (self._dense, self._sparse):
             if ix is not None:
                 ix.close()

@@ -299,16 +299,19 @@ class ConcurrentHybrid:
     def __call__(self, dense_fn, sparse_fn, sparse_inputs, limit: int, rrf_k: int = 2) -> TopK:
         main = torch.cuda.current_stream()
         self.side.wait_stream(main)
+        # (under graph capture the graph's pool owns every block: no cross-stream bookkeeping)
+        capturing = torch.cuda.is_current_stream_capturing()
         for t in sparse_inputs:
-            if isinstance(t, torch.Tensor) and t.is_cuda:
+            if isinstance(t, torch.Tensor) and t.is_cuda and not capturing:
                 t.record_stream(self.side)
         # the sparse chain is issued first (round-3 A/B: profiles/r03x_*)
         with torch.cuda.stream(self.side):
             s = sparse_fn()
         d = dense_fn()
         main.wait_stream(self.side)
-        for t in s.tensors():
-            t.record_stream(main)
+        if not capturing:
+            for t in s.tensors():
+                t.record_stream(main)
         return rrf_fuse(d, s, limit, rrf_k=rrf_k)
 
 

@@ -11,6 +11,7 @@ falls back to the CPU. search_batch() is the batched device API the pipeline and
 from __future__ import annotations
 
 import logging
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -76,6 +77,71 @@ def fp16_rows(vectors: list[list[float]] | np.ndarray, dim: int) -> np.ndarray:
     if a.ndim != 2 or a.shape[1] != dim:
         raise ValueError(f"dense vectors must have dimension {dim}, got shape {a.shape}")
     return a.astype(np.float16)
+
+
+class _QueryGraph:
+    """One unfiltered single-query search of a collection, captured as a HIP graph for one
+    (branch, top_k): the query's dense fp16 vector and sparse terms (<= 256) are written into a
+    pinned staging buffer and sent in one host->device copy, the graph replays every search
+    kernel (dense scan / merge / second pass, the sparse chain on its side stream, RRF) plus the
+    packing of (count, ids, scores) into one fp64 row, and one device->host copy brings that row
+    back. The eager path launches the same kernels one Python call at a time, with a copy per
+    input array and a packing step per result."""
+
+    def __init__(self, ret: "MI355XRetriever", coll: ChunkCollection, mode: str, top_k: int):
+        dev, dim = ret.device, coll.dim
+        self.indexes = (coll.dense_index, coll.sparse_index)  # the graph's kernels read them
+        self.mode, self.k, self.dim = mode, top_k, dim
+        self.lock = threading.Lock()
+        off_ptr = dim * 2
+        off_idx = off_ptr + 16
+        off_val = off_idx + 4 * MAX_QUERY_TERMS
+        total = off_val + 4 * MAX_QUERY_TERMS
+        self.host = torch.zeros(total, dtype=torch.uint8, pin_memory=True)
+        self.stage = torch.zeros(total, dtype=torch.uint8, device=dev)
+        h = self.host.numpy()
+        self.h_dense = h[:off_ptr].view(np.float16)
+        self.h_ptr = h[off_ptr:off_ptr + 8].view(np.int32)
+        self.h_idx = h[off_idx:off_val].view(np.int32)
+        self.h_val = h[off_val:].view(np.float32)
+        d = self.stage
+        batch = QueryBatch(dense=d[:off_ptr].view(torch.float16).view(1, dim))
+        if mode in ("hybrid", "sparse"):
+            batch = QueryBatch(dense=batch.dense, sparse_indptr=d[off_ptr:off_ptr + 8].view(torch.int32),
+                               sparse_indices=d[off_idx:off_val].view(torch.int32),
+                               sparse_values=d[off_val:].view(torch.float32))
+        self.out_host = torch.zeros(1 + 2 * top_k, dtype=torch.float64, pin_memory=True)
+
+        def run():
+            out = ret._search_device(coll, batch, top_k, mode, None)
+            sc = out.rank if mode == "hybrid" else out.scores
+            return torch.cat([out.count[:1].double(), out.ids[0].double(), sc[0].double()])
+
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                run()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.packed = run()
+
+    def search(self, dense, sparse: tuple[np.ndarray, np.ndarray] | None) -> np.ndarray:
+        """The packed result row (count, ids[k], scores[k]) of one query."""
+        with self.lock:
+            self.h_dense[:] = dense
+            if sparse is not None:
+                n = sparse[0].size
+                self.h_ptr[0], self.h_ptr[1] = 0, n
+                self.h_idx[:n] = sparse[0]
+                self.h_val[:n] = sparse[1]
+            stream = torch.cuda.current_stream(self.stage.device)
+            self.stage.copy_(self.host, non_blocking=True)
+            self.graph.replay()
+            self.out_host.copy_(self.packed, non_blocking=True)
+            stream.synchronize()
+            return self.out_host.numpy().copy()
 
 
 @RetrievalRegistry.register("mi355x")
@@ -235,6 +301,11 @@ class MI355XRetriever(BaseRetriever):
         coll = self._collections[resolved]
         mode = self._mode(coll, search_type, queries.has_sparse)
         mask = coll.filter_mask(filter_metadata)
+        return self._search_device(coll, queries, top_k, mode, mask), mode
+
+    def _search_device(self, coll: ChunkCollection, queries: QueryBatch, top_k: int, mode: str,
+                       mask: torch.Tensor | None) -> TopK:
+        """The device work of search_batch for a resolved collection and branch."""
         if mode == "hybrid":
             if self._hybrid is None:
                 self._hybrid = ConcurrentHybrid(self.device)
@@ -243,11 +314,11 @@ class MI355XRetriever(BaseRetriever):
                 lambda: coll.dense_index.topk(queries.dense, 2 * top_k, row_mask=mask),
                 lambda: coll.sparse_index.topk(*sq, 2 * top_k, row_mask=mask),
                 sq + ((mask,) if mask is not None else ()), top_k, rrf_k=self.config.rrf_k)
-            return fused, mode
+            return fused
         if mode == "sparse":
             return coll.sparse_index.topk(queries.sparse_indptr, queries.sparse_indices,
-                                          queries.sparse_values, top_k, row_mask=mask), mode
-        return coll.dense_index.topk(queries.dense, top_k, row_mask=mask), mode
+                                          queries.sparse_values, top_k, row_mask=mask)
+        return coll.dense_index.topk(queries.dense, top_k, row_mask=mask)
 
     def to_query_batch(self, query_embeddings: list[EmbeddingResult]) -> QueryBatch:
         dense = torch.from_numpy(fp16_rows([q.dense for q in query_embeddings],
@@ -310,6 +381,43 @@ class MI355XRetriever(BaseRetriever):
             batch.append(results)
         return batch
 
+    def _graph_search(self, coll: ChunkCollection, query: EmbeddingResult, top_k: int,
+                      search_type: str) -> tuple[np.ndarray, str] | None:
+        """search() of one unfiltered query through the collection's captured graph for its
+        branch (captured on first use); None when the path does not apply."""
+        if not self.config.query_graphs or coll.count == 0:
+            return None
+        mode = self._mode(coll, search_type, query.sparse is not None)
+        sparse = query_sparse_arrays(query.sparse) if mode in ("hybrid", "sparse") else None
+        dense = np.asarray(query.dense, dtype=np.float32)
+        if dense.shape != (self.embedding_dim,):
+            raise ValueError(f"dense vectors must have dimension {self.embedding_dim}, "
+                             f"got shape {(1,) + dense.shape}")
+        graphs = coll.query_graphs()
+        key = (mode, top_k, self.config.rrf_k)
+        g = graphs.get(key)
+        if g is None:
+            g = _QueryGraph(self, coll, mode, top_k)
+            graphs[key] = g
+        return g.search(dense, sparse), mode
+
+    def _materialize_packed(self, packed: np.ndarray, resolved: str, k: int,
+                            threshold: float | None) -> list[RetrievalResult]:
+        coll = self._collections[resolved]
+        count = int(packed[0])
+        ids = packed[1:1 + count].astype(np.int64).tolist()
+        scores = packed[1 + k:1 + k + count].tolist()
+        results = []
+        for pid, score in zip(ids, scores):
+            if threshold is not None and score < threshold:
+                continue
+            p = coll.payloads[pid]
+            chunk = AudioChunk(text=p.get("text", ""), start=p.get("start", 0.0),
+                               end=p.get("end", 0.0), speaker=p.get("speaker"),
+                               metadata=p.get("metadata"))
+            results.append(RetrievalResult(chunk=chunk, score=float(score), source=resolved))
+        return results
+
     @timed
     def search(self, query_embedding: EmbeddingResult, top_k: int | None = None,
                collection_name: str | None = None, filter_metadata: dict | None = None,
@@ -318,6 +426,17 @@ class MI355XRetriever(BaseRetriever):
         top_k = top_k or self.config.top_k
         search_type = search_type or self.config.search_type
         try:
+            if not filter_metadata:
+                coll = self._collections[resolved]
+                got = self._graph_search(coll, query_embedding, top_k, search_type)
+                if got is not None:
+                    packed, mode = got
+                    thr = None
+                    if mode == "legacy_dense" and self.config.score_threshold > 0:
+                        thr = self.config.score_threshold
+                    results = self._materialize_packed(packed, resolved, top_k, thr)
+                    logger.debug(f"Search returned {len(results)} results")
+                    return results
             batch = self.to_query_batch([query_embedding])
             out, mode = self.search_batch(batch, top_k, resolved, filter_metadata, search_type)
             thr = None
