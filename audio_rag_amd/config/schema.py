@@ -57,6 +57,10 @@ class RetrievalConfig(BaseModel):
     # top_k): one host->device copy of the query, one replay of the search kernels, one
     # device->host copy of the packed result
     query_graphs: bool = True
+    # GPUs the corpus is sharded over: > 1 runs one process per GPU
+    # (torchrun), torch.distributed initialised before the retriever; searches are collective
+    # calls (MI355XRetriever._search_sharded)
+    num_gpus: int = Field(default=1, ge=1)
 
 
 class RerankingConfig(BaseModel):

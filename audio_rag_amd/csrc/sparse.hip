@@ -1382,24 +1382,28 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
 #ifdef ARMI_SPARSE_PROFILE
   static const int dbg = getenv("ARMI_SPARSE_DBG") ? atoi(getenv("ARMI_SPARSE_DBG")) : 0;
 #else
-  // ARMI_SPARSE_CLEAR=all: clear every staged row each step (the round-2 form; A/B)
-  static const int dbg = [] {
-    const char* e = getenv("ARMI_SPARSE_CLEAR");
-    return (e && e[0] == 'a') ? 16 : 0;
-  }();
+  constexpr int dbg = 0;
 #endif
   const size_t lds_collect = (size_t)kCollectCap * 8;
-  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect));
-  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepLds));
-  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_bitmap_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepBmLds));
-  static const bool sort_terms = getenv("ARMI_SPARSE_PASS") && getenv("ARMI_SPARSE_PASS")[0] == 's';
-  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds));
-  ARMI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds));
+  // dynamic-LDS limits raised once (no runtime calls but stream work per search: graph-capturable)
+  static const hipError_t raised = [&] {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepLds);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_bitmap_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepBmLds);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds);
+    return e;
+  }();
+  ARMI_HIP(raised);
   for (int q0 = 0; q0 < n_queries; q0 += kQB) {
     const int nqp = std::min(kQB, n_queries - q0);
     uint32_t* pflags = out_flags + q0;
@@ -1410,7 +1414,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       continue;
     }
     ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
-    if (idx->vocab <= kBitmapVocab && !sort_terms)
+    if (idx->vocab <= kBitmapVocab)
       pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
           w.qcount, w.qof, pflags);

@@ -78,6 +78,16 @@ class ChunkCollection:
     # captured single-query searches over the current indexes (MI355XRetriever._graph_search),
     # dropped whenever the indexes are rebuilt or closed
     _graphs: dict = field(default_factory=dict)
+    # (rank, world): this process's shard of the corpus when it is spread over `world` GPUs
+    # (RetrievalConfig.num_gpus): every rank stages every point on the host and builds device
+    # indexes over its contiguous ordinal range only (retrieval/shards.shard_range)
+    shard: tuple = (0, 1)
+
+    def shard_bounds(self, n: int | None = None) -> tuple[int, int]:
+        """[lo, hi) ordinals of this rank's shard of n (default: every) points."""
+        from audio_rag_amd.retrieval.shards import shard_range
+
+        return shard_range(self.count if n is None else n, self.shard[0], self.shard[1])
 
     @property
     def count(self) -> int:
@@ -115,20 +125,26 @@ class ChunkCollection:
                 return
             rows = (np.concatenate(self.dense_rows) if self.dense_rows
                     else np.zeros((0, self.dim), dtype=np.float16))
+            lo, hi = self.shard_bounds()
             old_dense, old_sparse = self._dense, self._sparse
             self._graphs = {}
-            self._dense = DenseIndex(torch.from_numpy(rows).to(self.device))
+            self._dense = DenseIndex(torch.from_numpy(np.ascontiguousarray(rows[lo:hi])).to(self.device),
+                                     ordinal_base=lo)
             if self.hybrid:
-                indptr = np.zeros(self.count + 1, dtype=np.int64)
-                lens = [0 if s is None else len(s[0]) for s in self.sparse_rows]
+                mine = self.sparse_rows[lo:hi]
+                indptr = np.zeros(hi - lo + 1, dtype=np.int64)
+                lens = [0 if s is None else len(s[0]) for s in mine]
                 np.cumsum(lens, out=indptr[1:])
-                idx = np.concatenate([s[0] for s in self.sparse_rows if s is not None] or
+                idx = np.concatenate([s[0] for s in mine if s is not None] or
                                      [np.zeros(0, np.int32)]).astype(np.int32)
-                val = np.concatenate([s[1] for s in self.sparse_rows if s is not None] or
+                val = np.concatenate([s[1] for s in mine if s is not None] or
                                      [np.zeros(0, np.float32)]).astype(np.float32)
-                vocab = max(BGE_M3_VOCAB, int(idx.max(initial=-1)) + 1)
+                # the vocabulary of the whole corpus: every shard answers the same term ids
+                vmax = max((int(s[0].max(initial=-1)) for s in self.sparse_rows if s is not None),
+                           default=-1)
+                vocab = max(BGE_M3_VOCAB, vmax + 1)
                 t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
-                self._sparse = SparseIndex(t(indptr), t(idx), t(val), vocab)
+                self._sparse = SparseIndex(t(indptr), t(idx), t(val), vocab, ordinal_base=lo)
             self._built_rows = self.count
             # The superseded indexes are not closed here: a search that fetched them before
             # this rebuild may still be using them. Dropping the reference frees each one (its
@@ -155,7 +171,7 @@ class ChunkCollection:
     def filter_mask(self, filter_metadata: dict | None) -> torch.Tensor | None:
         """Bitmask (int64 words on the device) of points whose payload metadata matches every
         condition: Filter(must=[FieldCondition(key=f"metadata.{k}", match=MatchValue(v))])
-        (qdrant.py:263-269)."""
+        (qdrant.py:263-269). Bit r = row r of this rank's shard (ordinal lo + r)."""
         if not filter_metadata:
             return None
         key = tuple(sorted((k, repr(v)) for k, v in filter_metadata.items()))
@@ -166,7 +182,9 @@ class ChunkCollection:
         ok = np.ones(n, dtype=bool)
         for k, v in filter_metadata.items():
             ok &= self._key_matches(k, v, n)
-        words = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        lo, hi = self.shard_bounds(n)
+        ok = ok[lo:hi]
+        words = np.zeros(max((hi - lo + 63) // 64, 1), dtype=np.uint64)
         idx = np.nonzero(ok)[0]
         np.bitwise_or.at(words, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
         mask = torch.from_numpy(words.view(np.int64)).to(self.device)
@@ -212,13 +230,17 @@ class ChunkCollection:
 
     @classmethod
     def from_indexes(cls, name: str, dense: DenseIndex, payloads: list[dict],
-                     sparse: SparseIndex | None = None) -> "ChunkCollection":
+                     sparse: SparseIndex | None = None, shard: tuple = (0, 1)) -> "ChunkCollection":
         """A read-only collection over device indexes built elsewhere (a loaded store shard, a
         synthetic benchmark corpus). Nothing is staged on the host, so it cannot be saved or
-        extended with upsert()."""
-        if len(payloads) != dense.n_rows:
-            raise ValueError("one payload per row is required")
+        extended with upsert(). Sharded (shard = (rank, world)): the indexes hold this rank's
+        shard_range of the corpus (ordinal_base = its first ordinal), payloads every point."""
         coll = cls(name, dense.dim, sparse is not None, dense.device)
+        coll.shard = tuple(shard)
+        lo, hi = coll.shard_bounds(len(payloads))
+        if dense.n_rows != hi - lo or dense.ordinal_base != lo:
+            raise ValueError("the dense index must hold this rank's shard of the payloads "
+                             f"(ordinals [{lo}, {hi}))")
         coll.payloads = payloads
         coll._dense, coll._sparse = dense, sparse
         coll._built_rows = len(payloads)

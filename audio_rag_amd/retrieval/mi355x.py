@@ -154,6 +154,21 @@ class MI355XRetriever(BaseRetriever):
         self.device = torch.device("cuda", config.device)
         self._collections: dict[str, ChunkCollection] = {}
         self._hybrid: ConcurrentHybrid | None = None
+        # num_gpus > 1: the corpus is sharded by ordinal over the ranks of the default process
+        # group (one process per GPU, launched by torchrun, torch.distributed initialised and
+        # the process's GPU selected before the retriever is built): see _search_sharded
+        self._rank, self._world = 0, 1
+        if config.num_gpus > 1:
+            import torch.distributed as dist
+
+            if not dist.is_available() or not dist.is_initialized():
+                raise RetrievalError("num_gpus > 1 needs torch.distributed initialised (one "
+                                     "process per GPU, e.g. torchrun) before the retriever")
+            if dist.get_world_size() != config.num_gpus:
+                raise RetrievalError(f"num_gpus = {config.num_gpus} but the process group has "
+                                     f"{dist.get_world_size()} ranks")
+            self._rank, self._world = dist.get_rank(), dist.get_world_size()
+            self.device = torch.device("cuda", torch.cuda.current_device())
         logger.info(f"MI355XRetriever initialized: collection={config.collection_name}, "
                     f"search_type={config.search_type}, device={self.device}")
 
@@ -173,8 +188,9 @@ class MI355XRetriever(BaseRetriever):
                                "Re-index required for hybrid search.")
             return resolved
         try:
-            self._collections[resolved] = ChunkCollection(resolved, self.embedding_dim, hybrid,
-                                                          self.device)
+            coll = ChunkCollection(resolved, self.embedding_dim, hybrid, self.device)
+            coll.shard = (self._rank, self._world)
+            self._collections[resolved] = coll
             logger.info(f"Creating {'hybrid' if hybrid else 'dense'} collection: {resolved}")
             return resolved
         except Exception as e:
@@ -272,6 +288,7 @@ class MI355XRetriever(BaseRetriever):
 
             resolved = collection_name or read_meta(path)["name"]
             coll = ChunkCollection.load(path, self.device, resolved)
+            coll.shard = (self._rank, self._world)
         except Exception as e:
             raise RetrievalError(f"Failed to load chunk store '{path}': {e}")
         old = self._collections.pop(resolved, None)
@@ -301,7 +318,35 @@ class MI355XRetriever(BaseRetriever):
         coll = self._collections[resolved]
         mode = self._mode(coll, search_type, queries.has_sparse)
         mask = coll.filter_mask(filter_metadata)
+        if self._world > 1:
+            return self._search_sharded(coll, queries, top_k, mode, mask), mode
         return self._search_device(coll, queries, top_k, mode, mask), mode
+
+    def _search_sharded(self, coll: ChunkCollection, queries: QueryBatch, top_k: int, mode: str,
+                        mask: torch.Tensor | None) -> TopK:
+        """search_batch over the corpus sharded across the process group (num_gpus > 1), a
+        COLLECTIVE call: every rank calls it with its own B queries (B equal on every rank) and
+        the same top_k, branch and filter, and gets the global top-k of its own queries.
+        retrieval/shards.ShardedSearch: one RCCL all-gather of all ranks' queries, the local
+        kernels over this rank's shard for all of them, one all-gather of the per-shard lists,
+        the merge of this rank's queries (armi_topk_merge_shards_packed), RRF after the merge
+        for hybrid. Keys are exact and tie-broken by the global ordinal, so the answer equals
+        the single-GPU one. Reranking stays local: each rank reranks its own queries' candidates
+        (the query slice), with no further exchange."""
+        from audio_rag_amd.retrieval.device import merge_shards, merge_shards_packed, rrf_fuse
+        from audio_rag_amd.retrieval.shards import ShardedSearch
+
+        sh = ShardedSearch(lambda q, k: coll.dense_index.topk(q, k, row_mask=mask), merge_shards,
+                           local_sparse=(lambda c, k: coll.sparse_index.topk(*c, k, row_mask=mask))
+                           if coll.hybrid else None,
+                           rrf=lambda a, b, k: rrf_fuse(a, b, k, rrf_k=self.config.rrf_k),
+                           merge_packed=merge_shards_packed)
+        csr = (queries.sparse_indptr, queries.sparse_indices, queries.sparse_values)
+        if mode == "hybrid":
+            return sh.hybrid(queries.dense, csr, top_k)
+        if mode == "sparse":
+            return sh.sparse(csr, top_k)
+        return sh.dense(queries.dense, top_k)
 
     def _search_device(self, coll: ChunkCollection, queries: QueryBatch, top_k: int, mode: str,
                        mask: torch.Tensor | None) -> TopK:
@@ -385,7 +430,7 @@ class MI355XRetriever(BaseRetriever):
                       search_type: str) -> tuple[np.ndarray, str] | None:
         """search() of one unfiltered query through the collection's captured graph for its
         branch (captured on first use); None when the path does not apply."""
-        if not self.config.query_graphs or coll.count == 0:
+        if not self.config.query_graphs or coll.count == 0 or self._world > 1:
             return None
         mode = self._mode(coll, search_type, query.sparse is not None)
         sparse = query_sparse_arrays(query.sparse) if mode in ("hybrid", "sparse") else None

@@ -10,7 +10,7 @@ cd "$R" || exit 1
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -v --timeout 300 --timeout-method thread \
     > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
   echo "pytest rc=$rc: $(tail -1 gpurun_out/${TAG}_pytest.log)"
   grep -E "FAILED|ERROR" gpurun_out/${TAG}_pytest.log | head -20
@@ -19,8 +19,9 @@ if [[ $STEPS == all || $STEPS == *tests* ]]; then
   echo "smoke: $(tail -1 gpurun_out/${TAG}_smoke.log)"
 fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
-  /usr/bin/time -f "bench wall %e s" timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
-  tail -1 gpurun_out/${TAG}_bench.err
+  t0=$(date +%s)
+  timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
+  echo "bench wall $(( $(date +%s) - t0 )) s"
   python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_bench.json'));print('dense',round(d['value']),'ms',round(d['ms_per_step'],4),'frac',round(d['roofline']['frac'],3),'traffic',d['roofline']['traffic'],'cpu',d['cpu_baseline']['value']);[print(k,round(d[k].get('value',0)),d[k].get('cpu_baseline',{}) and d[k]['cpu_baseline']['value'],d[k].get('roofline',{}).get('traffic')) for k in ('configs1','configs2','chunks_10k','chunks_10M')]"
 fi
 if [[ $STEPS == all || $STEPS == *lat* ]]; then
@@ -38,5 +39,19 @@ if [[ $STEPS == all || $STEPS == *pmc* ]]; then
   bash tools/pmc_traffic.sh ${TAG}_t1m roofline || exit $?
   bash tools/pmc_traffic.sh ${TAG}_t100k roofline --chunks 100000 || exit $?
   bash tools/pmc_traffic.sh ${TAG}_tsp roofline_sparse --workload hybrid || exit $?
+fi
+if [[ $STEPS == *sqsparse* ]]; then
+  bash tools/probes/pmc_sparse.sh ${TAG}_sqsp || exit $?
+fi
+if [[ $STEPS == *rerankprof* ]]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof_rerank" -o run -- \
+    python3 "$R/bench.py" --workload hybrid_rerank --steps 3 --warmup 2 --latency-iters 1 --no-cpu-baseline > "$R/gpurun_out/${TAG}_prof_rerank.log" 2>&1 || exit $?
+  echo "prof rerank done"; tail -1 "$R/gpurun_out/${TAG}_prof_rerank.log" | cut -c1-300
+  cd "$R"
+fi
+if [[ $STEPS == *pipeline* ]]; then
+  timeout -k 10 500 python bench.py --workload pipeline --queries 200 > gpurun_out/${TAG}_bench_pipeline.json 2>&1 || exit $?
+  python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_bench_pipeline.json').read().strip().splitlines()[-1]);print('pipeline p50',d['p50_ms'],d['stage_p50_ms'])"
 fi
 exit 0
