@@ -18,7 +18,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 def per_dispatch(path: str, kernel: str, counter: str) -> list[float]:
     acc = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter:
+        if kernel + "(" in r["Kernel_Name"] and r["Counter_Name"] == counter:
             acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(acc.values())
 
