@@ -35,9 +35,14 @@ if [[ $STEPS == all || $STEPS == *prof* ]]; then
   echo "prof dense done"
   cd "$R"
 fi
-if [[ $STEPS == all || $STEPS == *pmc* ]]; then
+if [[ $STEPS == all || $STEPS == *pmc1m* ]]; then
   bash tools/pmc_traffic.sh ${TAG}_t1m roofline || exit $?
+fi
+if [[ $STEPS == all || $STEPS == *pmc100k* ]]; then
   bash tools/pmc_traffic.sh ${TAG}_t100k roofline --chunks 100000 || exit $?
+  bash tools/pmc_traffic.sh ${TAG}_t10k roofline --chunks 10000 || exit $?
+fi
+if [[ $STEPS == all || $STEPS == *pmcsp* ]]; then
   bash tools/pmc_traffic.sh ${TAG}_tsp roofline_sparse --workload hybrid || exit $?
 fi
 if [[ $STEPS == *sqsparse* ]]; then
