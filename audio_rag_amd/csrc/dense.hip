@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     int sel_rank, int64_t ordinal_base,
     float* __restrict__ out_scores, int64_t* __restrict__ out_ids, double* __restrict__ out_rank,
     int32_t* __restrict__ out_count, uint32_t* __restrict__ out_flags, float* __restrict__ thr_out,
-    int32_t* __restrict__ col_cnt, int two_stage) {
+    int32_t* __restrict__ col_cnt, int32_t* __restrict__ help_done, int two_stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* skey = reinterpret_cast<float*>(smem);                              // [kSelCap]
   int32_t* srow = reinterpret_cast<int32_t*>(smem + kSelCap * 4);            // [kSelCap]
@@ -1730,6 +1730,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     out_flags[qg] = certified ? ARMI_FLAG_CERTIFIED : 0u;
     thr_out[qg] = certified ? __builtin_inff() : thr;
     col_cnt[qg] = 0;
+    help_done[qg] = 0;
   }
   MERGE_STAMP(7);
 }
@@ -1737,42 +1738,37 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 constexpr size_t kMergeLds = kSelCap * 8 + 256 * 16 + 64 + 16 + 256 * 4;
 
 // Second-pass merge, one workgroup per query (certified queries exit at once): exact keys of the
-// rows dense_scan_i8_kernel<COLLECT> appended (image positions -> ordinals), top-k by (key desc,
+// rows dense_scan_i8_kernel<COLLECT> appended (local rows -> ordinals), top-k by (key desc,
 // ordinal asc). The list holds every row of the true top-k (see the collect pass), so this top-k
-// is the exact answer. More appends than the list holds (> cap rows within delta + the int8 slack
-// of the k-th key: a pathological pile of duplicates) -> this workgroup scores every row itself.
-// Rows go through LDS 512 at a time: [0, 512) the best so far, [512, 1024) the next chunk, one
-// bitonic sort per chunk; a list of <= 512 rows is scored and sorted once.
+// is the exact answer. Rows go through LDS 512 at a time: [0, 512) the best so far, [512, 1024)
+// the next chunk, one bitonic sort per chunk; a list of <= 512 rows is scored and sorted once.
+// A query whose list overflowed (more than cap rows within delta + the int8 slack of its k-th key:
+// a pile of near-duplicates) is answered by the grid's n_help helper workgroups instead: helper h
+// scores its 1/n_help of the shard exactly and writes its slice's top-k rows into the query's
+// list (slot h * k ...), and the last helper to finish (a per-query counter, zeroed by
+// dense_merge_kernel) merges those n_help * k <= cap rows as above. The shard is read once per
+// such query, spread over n_help CUs. Helpers find nothing to do, and exit, on every other call.
 constexpr int kColChunk = 512;
-constexpr size_t kColMergeLds = 2 * kColChunk * 16;
+constexpr size_t kColMergeLds = 2 * kColChunk * 16 + 16;
+constexpr int kMaxHelp = 64;
 
+// Top of n rows (list entries, or rows r0 .. r0 + n - 1 of the shard when list == nullptr) left
+// sorted by (key desc, ordinal asc) in key / ord [0, max(n, k)); filtered / invalid rows skipped.
 template <int DIM>
-__global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel(
-    const int32_t* __restrict__ col_cnt, const int32_t* __restrict__ col_list, int col_cap,
-    const uint16_t* __restrict__ rows,
-    const double* __restrict__ inv_norm, const int64_t* __restrict__ norm2,
-    const uint64_t* __restrict__ row_mask, int64_t n_rows, const uint16_t* __restrict__ queries,
-    const double* __restrict__ inv_q, int k, int64_t ordinal_base, float* __restrict__ out_scores,
-    int64_t* __restrict__ out_ids, double* __restrict__ out_rank, int32_t* __restrict__ out_count,
-    uint32_t* __restrict__ flags) {
-  const int qg = blockIdx.x;
-  if (flags[qg] & ARMI_FLAG_CERTIFIED) return;  // workgroup-uniform
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* key = reinterpret_cast<double*>(smem);                            // [2 * kColChunk]
-  int64_t* ord = reinterpret_cast<int64_t*>(smem + 2 * kColChunk * 8);       // [2 * kColChunk]
+__device__ void collect_top_rows(const int32_t* __restrict__ list, int64_t r0, int64_t n, int k,
+                                 const int32_t (&qf)[DIM / 64], const uint16_t* __restrict__ rows,
+                                 const double* __restrict__ inv_norm,
+                                 const int64_t* __restrict__ norm2,
+                                 const uint64_t* __restrict__ row_mask, int64_t ordinal_base,
+                                 double* key, int64_t* ord) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = armi::wave_id();
-  const int cnt = col_cnt[qg];
-  const bool exhaustive = cnt > col_cap;
-  const int64_t n = exhaustive ? n_rows : cnt;
+  __syncthreads();  // the caller's previous use of key / ord is over
   for (int e = tid; e < 2 * kColChunk; e += kDenseMergeThreads) {
     key[e] = kNegInfD;
     ord[e] = kNoOrd;
   }
-  int32_t qf[DIM / 64];
-  load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
-  const int32_t* list = col_list + (size_t)qg * col_cap;
   const bool single = n <= kColChunk;
   constexpr int kPerWave = kColChunk / (kDenseMergeThreads / 64);  // 64 rows per wave and chunk
   for (int64_t c0 = 0; c0 < n; c0 += kColChunk) {
@@ -1786,8 +1782,8 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
         const int e = kPerWave * wave + b + j;
         int32_t o = -1;
         if (e < m) {
-          if (exhaustive) {
-            const int64_t row = c0 + e;
+          if (list == nullptr) {
+            const int64_t row = r0 + c0 + e;
             const bool on = norm2[row] >= 0 &&
                             (!row_mask || ((row_mask[row >> 6] >> (row & 63)) & 1ull));
             o = on ? (int32_t)row : -1;
@@ -1809,22 +1805,78 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
     armi::lds_sort_rank_desc(key, ord,
                              single ? armi::pow2_at_least(m > k ? m : k) : 2 * kColChunk);
   }
-  if (wave != 0) return;
-  int n_valid = 0;
-  for (int c = lane; c < k; c += 64) n_valid += ord[c] != kNoOrd;
+  __syncthreads();
+}
+
+template <int DIM>
+__global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel(
+    const int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list, int col_cap,
+    int32_t* __restrict__ help_done, int nq, const uint16_t* __restrict__ rows,
+    const double* __restrict__ inv_norm, const int64_t* __restrict__ norm2,
+    const uint64_t* __restrict__ row_mask, int64_t n_rows, const uint16_t* __restrict__ queries,
+    const double* __restrict__ inv_q, int k, int64_t ordinal_base, float* __restrict__ out_scores,
+    int64_t* __restrict__ out_ids, double* __restrict__ out_rank, int32_t* __restrict__ out_count,
+    uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* key = reinterpret_cast<double*>(smem);                            // [2 * kColChunk]
+  int64_t* ord = reinterpret_cast<int64_t*>(smem + 2 * kColChunk * 8);       // [2 * kColChunk]
+  int* s_last = reinterpret_cast<int*>(smem + 2 * kColChunk * 16);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = armi::wave_id();
+  auto write_out = [&](int qg) {
+    if (wave != 0) return;
+    int n_valid = 0;
+    for (int c = lane; c < k; c += 64) n_valid += ord[c] != kNoOrd;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
-  const double iq = inv_q[qg];
-  for (int c = lane; c < k; c += 64) {
-    const size_t o = (size_t)qg * k + c;
-    const bool v = ord[c] != kNoOrd;
-    out_scores[o] = v ? (float)(key[c] * iq) : kNegInf;
-    out_ids[o] = v ? ord[c] : -1;
-    out_rank[o] = v ? key[c] : kNegInfD;
+    for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
+    const double iq = inv_q[qg];
+    for (int c = lane; c < k; c += 64) {
+      const size_t o = (size_t)qg * k + c;
+      const bool v = ord[c] != kNoOrd;
+      out_scores[o] = v ? (float)(key[c] * iq) : kNegInf;
+      out_ids[o] = v ? ord[c] : -1;
+      out_rank[o] = v ? key[c] : kNegInfD;
+    }
+    if (lane == 0) {
+      out_count[qg] = n_valid;
+      flags[qg] = ARMI_FLAG_FALLBACK;
+    }
+  };
+  if ((int)blockIdx.x < nq) {  // the query's own workgroup
+    const int qg = blockIdx.x;
+    if (flags[qg] & ARMI_FLAG_CERTIFIED) return;  // workgroup-uniform
+    const int cnt = col_cnt[qg];
+    if (cnt > col_cap) return;  // overflowed: the helpers answer it
+    int32_t qf[DIM / 64];
+    load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
+    collect_top_rows<DIM>(col_list + (size_t)qg * col_cap, 0, cnt, k, qf, rows, inv_norm, norm2,
+                          row_mask, ordinal_base, key, ord);
+    write_out(qg);
+    return;
   }
-  if (lane == 0) {
-    out_count[qg] = n_valid;
-    flags[qg] = ARMI_FLAG_FALLBACK;
+  const int n_help = (int)gridDim.x - nq;
+  const int h = (int)blockIdx.x - nq;
+  const int64_t lo = n_rows * h / n_help, hi = n_rows * (h + 1) / n_help;
+  for (int qg = 0; qg < nq; ++qg) {
+    if ((flags[qg] & ARMI_FLAG_CERTIFIED) || col_cnt[qg] <= col_cap) continue;  // uniform
+    int32_t qf[DIM / 64];
+    load_fixed<DIM>(queries + (size_t)qg * DIM, lane, qf);
+    collect_top_rows<DIM>(nullptr, lo, hi - lo, k, qf, rows, inv_norm, norm2, row_mask,
+                          ordinal_base, key, ord);
+    int32_t* list = col_list + (size_t)qg * col_cap;
+    for (int c = tid; c < k; c += kDenseMergeThreads)
+      list[h * k + c] = ord[c] != kNoOrd ? (int32_t)(ord[c] - ordinal_base) : -1;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) *s_last = atomicAdd(help_done + qg, 1) == n_help - 1;
+    __syncthreads();
+    if (*s_last) {  // every helper's slice is in the list
+      __threadfence();
+      collect_top_rows<DIM>(list, 0, (int64_t)n_help * k, k, qf, rows, inv_norm, norm2, row_mask,
+                            ordinal_base, key, ord);
+      write_out(qg);
+    }
   }
 }
 
@@ -2128,7 +2180,8 @@ struct Workspace {
   int64_t* ex_ord;
   float* thr;          // [nq] collect threshold (+inf: certified)
   int32_t* col_cnt;    // [nq] rows appended by the collect pass
-  int32_t* col_list;   // [nq][kCollectCap] image positions
+  int32_t* col_list;   // [nq][kCollectCap] local rows
+  int32_t* help_done;  // [nq] helper workgroups done with an overflowed query
   uint64_t* mask_img;  // row filter in int8 image order
   size_t bytes;
 };
@@ -2144,6 +2197,7 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.thr = cv.take<float>(nq);
     w.col_cnt = cv.take<int32_t>(nq);
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
+    w.help_done = cv.take<int32_t>(nq);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
   }
   w.inv_q = cv.take<double>(nq);
@@ -2265,7 +2319,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
       idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt,
-      merge_two_stage(kc) ? 1 : 0);
+      w.help_done, merge_two_stage(kc) ? 1 : 0);
   ARMI_LAUNCHED("dense_merge_kernel");
   return dense_second_pass<DIM>(idx, queries, nq, k, row_mask, mask_i8, out_scores, out_ids,
                                 out_rank, out_count, out_flags, w, stream);
@@ -2291,8 +2345,11 @@ int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, in
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
-  dense_collect_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kColMergeLds, stream>>>(
-      w.col_cnt, w.col_list, kCollectCap, idx->rows, idx->inv_norm, idx->norm2,
+  // helpers for overflowed lists: each writes k rows into the list, so n_help * k <= the cap
+  const int n_help = std::max(1, std::min<int>(kMaxHelp, kCollectCap / k));
+  dense_collect_merge_kernel<DIM><<<dim3(nq + n_help), dim3(kDenseMergeThreads), kColMergeLds,
+                                    stream>>>(
+      w.col_cnt, w.col_list, kCollectCap, w.help_done, nq, idx->rows, idx->inv_norm, idx->norm2,
       row_mask, idx->n_rows, queries, w.inv_q, k, idx->ordinal_base, out_scores, out_ids,
       out_rank, out_count, out_flags);
   ARMI_LAUNCHED("dense_collect_merge_kernel");

@@ -102,6 +102,34 @@ def test_duplicate_pile_overflows_collect_list(gpu, oracle_mod):
     assert list(got["ids"][0]) == list(range(3000, 3010))
 
 
+@pytest.mark.parametrize("k", [1, 40, 240])
+def test_overflow_helpers_two_piles_filtered(gpu, oracle_mod, k):
+    """Two queries whose lists overflow in one call (two piles of 6500 identical rows, 4333 of them unfiltered), a row
+    filter that drops every third pile row, ordinal_base 7, k up to 240: the helper workgroups
+    (one 1/n_help slice of the shard each, n_help = min(64, 4096 / k)) find each pile's top-k,
+    and the last helper per query merges them; ties go by ordinal."""
+    from audio_rag_amd.retrieval.device import DenseIndex
+
+    base = oracle_mod.unit_fp16(9000, 1024, seed=97)
+    v1 = oracle_mod.unit_fp16(1, 1024, seed=98)
+    v2 = oracle_mod.unit_fp16(1, 1024, seed=99)
+    rows = np.concatenate([base[:2000], np.repeat(v1, 6500, axis=0), base[2000:5000],
+                           np.repeat(v2, 6500, axis=0), base[5000:]])
+    qs = np.concatenate([v1, oracle_mod.unit_fp16(5, 1024, seed=100), v2])
+    n = rows.shape[0]
+    keep = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in range(n):
+        if not (2000 <= r < 8500 or 11500 <= r < 18000) or r % 3:
+            keep[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    idx = DenseIndex(torch.from_numpy(rows.view(np.float16)).to(gpu), ordinal_base=7)
+    q = torch.from_numpy(qs.view(np.float16)).to(gpu)
+    mask = torch.from_numpy(keep.view(np.int64)).to(gpu)
+    got = _run(idx, q, k, mask)
+    ref = oracle_mod.dense_topk(rows, qs, k, ordinal_base=7, row_mask=keep)
+    _assert_same(got, ref)
+    assert got["flags"][0] == 2 and got["flags"][-1] == 2
+
+
 def test_fewer_valid_rows_than_k(gpu, oracle_mod):
     """A filter leaving 3 rows: the threshold is -inf and the collect pass returns them all."""
     from audio_rag_amd.retrieval.device import DenseIndex
