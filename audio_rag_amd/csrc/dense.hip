@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 
   if (t < t_end) {
     for (; t < t_end; t += kWaves) {
-      const int64_t tn = (t + kWaves < t_end) ? t + kWaves : t;
+      const int64_t tn = (t + kWaves < t_end) ? t + kWaves : 0;  // (tile 0: shared, L2-hot)
       const u32x4* nxt = row_ptr(tn);
       // The fragment image is loop-invariant; an opaque per-tile offset keeps the compiler from
       // hoisting all 2*KSTEPS fragment reads out of the tile loop (512 VGPRs -> scratch).
@@ -568,7 +568,10 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
             tn = t_begin + wnext < t_end ? t_begin + wnext : -1;
           }
           has_next = tn >= 0;
-          nxt = row_ptr(has_next ? tn : t);
+          // (no next tile: the loads go to image tile 0 instead, which every wave's last tile
+          // shares, so they hit L2 once it is there; re-reading the wave's own tile cost ~33 MB of
+          // HBM / Infinity-Cache fetches per launch, 1.33 x the algorithmic bytes at 100k rows)
+          nxt = row_ptr(has_next ? tn : 0);
           // the epilogue's row scales, issued before the next tile's loads: waiting for them
           // then leaves those in flight (issued after the prefetch, their wait was a vmcnt(0)
           // that drained it at every tile)
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(cur + 32 * (8 * (g + DEPTH) + i));
-        } else {  // (no next tile: the current one again, so every path issues the same loads)
+        } else {  // (no next tile: tile 0, so every path issues the same loads)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));

@@ -596,10 +596,13 @@ def main() -> None:
         alg = sum(pass_bytes[i % n_q_batches] for i in range(args.steps)) / max(args.steps, 1)
         if sp_n.value:
             sp_avg = sp_ms.value / sp_n.value
+            sp_traffic, sp_src = read_traffic(f"sparse_scan_{args.corpus}_n{n}_q{batch}")
             result["roofline_sparse"] = {
-                "bound": "hbm", "kernel": "sparse_scan_kernel", "achieved": alg / (sp_avg * 1e-3) / 1e9,
+                "bound": "hbm", "kernel": "sparse_scan_kernel<false>", "achieved": alg / (sp_avg * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg / (sp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                "frac": alg / (sp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": sp_traffic,
+                "traffic_source": sp_src,
+                "traffic_over_algorithmic": sp_traffic / alg if sp_traffic else None,
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": sp_avg,
                 "launches_timed": sp_n.value,
                 "note": "algorithmic bytes = sum over the distinct terms of the 64-query pass of "
