@@ -357,6 +357,14 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
 
   int64_t j = 0;   // tile of the stream
   int kt = 0;      // K-tile within the tile
+  // post: this K-tile follows a full tile's epilogue whose 32 stores per wave are still in flight.
+  // vmcnt retires loads, LDS-DMAs and stores in issue order, so a wait for a DMA issued after the
+  // stores waits for the stores too (the whole chip writing 128 KB per CU at once). The epilogue
+  // therefore issues K-tile s + 2's last two halves BEFORE its stores (buffer s & 1 is free
+  // after the K-tile's final barrier), this K-tile skips those two issues, and its closing wait
+  // leaves the stores (and the next K-tile's two halves) outstanding: the stores drain under two
+  // K-tiles of MFMAs instead of stalling the next one.
+  bool post = false;
   for (int64_t s = 0; s < total; ++s) {
     const int par = (int)(s & 1);
     // phase 0: quadrant (0, 0)
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
       write_half(pC, 0, 0);  // K-tile s + 1's feature half 0 (loaded in the previous phase 2)
       pA = load_half(s + 1, kt, 1, 0, 1);
     } else {
-      issue_half(s + 1, kt, 1, 0, 1);
+      if (!post) issue_half(s + 1, kt, 1, 0, 1);
     }
     if (kt == 1) issue_bias(j + 1, nxt.tp);  // slot (j+1)&1 was last read by epilogue(j-1)
     if constexpr (NBAR == 4) __builtin_amdgcn_s_barrier();
@@ -379,7 +387,7 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
       write_half(pD, 1, 1);
       pB = load_half(s + 1, kt, 1, 1, 0);
     } else {
-      issue_half(s + 1, kt, 1, 1, 0);
+      if (!post) issue_half(s + 1, kt, 1, 1, 0);
     }
     frags_ready();
     quadrant(0, 1);
@@ -406,14 +414,30 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
     frags_ready();
     quadrant(1, 0);
     if constexpr (!VG) {
-      if (s + 2 < total) {
+      if (post) {  // K-tile s + 1 complete; the 32 stores and s + 2's two halves may stay
+        if (s + 2 < total) {
+          asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        }
+      } else if (s + 2 < total) {
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
     __builtin_amdgcn_s_barrier();
+    post = false;
     if (++kt == nK) {
+      // a full tile stores exactly 32 instructions per wave (the counted waits above rely on
+      // it); a partial last tile keeps the plain schedule
+      if constexpr (!VG) {
+        if (cur.q0 + kT <= m && s + 2 < total) {
+          issue_half(s + 2, kt - 1, 2, 0, 1);
+          issue_half(s + 2, kt - 1, 2, 1, 0);
+          post = true;
+        }
+      }
       epilogue(j);
       kt = 0;
       ++j;
