@@ -55,6 +55,10 @@ if [[ $STEPS == *rerankprof* ]]; then
   echo "prof rerank done"; tail -1 "$R/gpurun_out/${TAG}_prof_rerank.log" | cut -c1-300
   cd "$R"
 fi
+if [[ $STEPS == *gemm* ]]; then
+  timeout -k 10 300 python tools/probes/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $?
+  grep '^{' gpurun_out/${TAG}_gemm.log
+fi
 if [[ $STEPS == *pipeline* ]]; then
   timeout -k 10 500 python bench.py --workload pipeline --queries 200 > gpurun_out/${TAG}_bench_pipeline.json 2>&1 || exit $?
   python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_bench_pipeline.json').read().strip().splitlines()[-1]);print('pipeline p50',d['p50_ms'],d['stage_p50_ms'])"
