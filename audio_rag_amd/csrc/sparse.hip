@@ -736,23 +736,41 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       y = or3(y, rv[0].y, rv[1].y);
       y = or3(y, rv[2].y, rv[3].y);
     };
+    // The next batch's entries (one scalar load) are requested right after this batch's LDS
+    // reads, so the two latencies overlap: the loop waits once per batch for both (scalar loads
+    // complete out of order, so any wait on one is a wait on every outstanding LDS read too).
+    // Round 3 loaded each batch's entries after the previous batch's math: a scalar-load and an
+    // LDS round trip in series per 4 terms (SQ counters r04d: the compute phase latency-bound).
+    // Prefetching past a list reads the zero padding or the next slot's entries (inside ql:
+    // kQStride = kMaxTerms + 2 kBatch), never used.
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
       const QTerm* L = ql + (wave * kQW + i) * kQStride;
       const int j1 = first_of(i, seg + 1);
       int j = first_of(i, seg);
+      if (j >= j1) continue;  // uniform
+      QTerm cur[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) cur[k] = L[j + k];  // uniform: one scalar load
       for (; j + kBatch <= j1; j += kBatch) {
-        QTerm tm[kBatch];
+        QTerm nxt[kBatch];  // requested first: in flight with this batch's LDS reads
 #pragma unroll
-        for (int k = 0; k < kBatch; ++k) tm[k] = L[j + k];  // uniform: one scalar load
-        batch(tm, kBatch, acc[i], hx[i], hy[i]);  // every entry inside the segment
-      }
-      if (j < j1) {
-        QTerm tm[kBatch];
+        for (int k = 0; k < kBatch; ++k) nxt[k] = L[j + kBatch + k];
+        uint2 rv[kBatch];
 #pragma unroll
-        for (int k = 0; k < kBatch; ++k) tm[k] = L[j + k];
-        batch(tm, j1 - j, acc[i], hx[i], hy[i]);
+        for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint2*>(buf + cur[k].off);
+        f2& a = acc[i];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+          a = a + f2{cur[k].w, cur[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
+        hx[i] = or3(hx[i], rv[0].x, rv[1].x);
+        hx[i] = or3(hx[i], rv[2].x, rv[3].x);
+        hy[i] = or3(hy[i], rv[0].y, rv[1].y);
+        hy[i] = or3(hy[i], rv[2].y, rv[3].y);
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) cur[k] = nxt[k];
       }
+      if (j < j1) batch(cur, j1 - j, acc[i], hx[i], hy[i]);  // cur = entries j .. j + 3
     }
   };
   auto candidates = [&](int tile, uint64_t m0, uint64_t m1) {
