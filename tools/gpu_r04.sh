@@ -55,6 +55,10 @@ if [[ $STEPS == *rerankprof* ]]; then
   echo "prof rerank done"; tail -1 "$R/gpurun_out/${TAG}_prof_rerank.log" | cut -c1-300
   cd "$R"
 fi
+if [[ $STEPS == *hybrid* ]]; then
+  timeout -k 10 300 python bench.py --workload hybrid --no-cpu-baseline --steps 40 --warmup 5 --latency-iters 5 > gpurun_out/${TAG}_bench_hybrid.json 2>&1 || exit $?
+  python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_bench_hybrid.json').read().strip().splitlines()[-1]);r=d['roofline_sparse'];print('hybrid',round(d['value']),'ms',round(d['ms_per_step'],4),'sparse scan ms',round(r['avg_launch_ms'],4),'frac',round(r['frac'],3))"
+fi
 if [[ $STEPS == *gemm* ]]; then
   timeout -k 10 300 python tools/probes/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $?
   grep '^{' gpurun_out/${TAG}_gemm.log
