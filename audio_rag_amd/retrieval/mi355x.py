@@ -117,15 +117,19 @@ class _QueryGraph:
             sc = out.rank if mode == "hybrid" else out.scores
             return torch.cat([out.count[:1].double(), out.ids[0].double(), sc[0].double()])
 
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                run()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.packed = run()
+        # captured under inference mode, as the reranker's graphs are (xlmr.py forward): the
+        # CUDA generator's graph-state tensors are created by the first capture in a process and
+        # updated in place by every later one, which torch refuses across the two modes
+        with torch.inference_mode():
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    run()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.packed = run()
 
     def search(self, dense, sparse: tuple[np.ndarray, np.ndarray] | None) -> np.ndarray:
         """The packed result row (count, ids[k], scores[k]) of one query."""
@@ -154,6 +158,7 @@ class MI355XRetriever(BaseRetriever):
         self.device = torch.device("cuda", config.device)
         self._collections: dict[str, ChunkCollection] = {}
         self._hybrid: ConcurrentHybrid | None = None
+        self._graphs_ok = True  # cleared when a capture is refused (search() then runs eagerly)
         # num_gpus > 1: the corpus is sharded by ordinal over the ranks of the default process
         # group (one process per GPU, launched by torchrun, torch.distributed initialised and
         # the process's GPU selected before the retriever is built): see _search_sharded
@@ -430,7 +435,7 @@ class MI355XRetriever(BaseRetriever):
                       search_type: str) -> tuple[np.ndarray, str] | None:
         """search() of one unfiltered query through the collection's captured graph for its
         branch (captured on first use); None when the path does not apply."""
-        if not self.config.query_graphs or coll.count == 0 or self._world > 1:
+        if not (self.config.query_graphs and self._graphs_ok) or coll.count == 0 or self._world > 1:
             return None
         mode = self._mode(coll, search_type, query.sparse is not None)
         sparse = query_sparse_arrays(query.sparse) if mode in ("hybrid", "sparse") else None
@@ -442,7 +447,12 @@ class MI355XRetriever(BaseRetriever):
         key = (mode, top_k, self.config.rrf_k)
         g = graphs.get(key)
         if g is None:
-            g = _QueryGraph(self, coll, mode, top_k)
+            try:
+                g = _QueryGraph(self, coll, mode, top_k)
+            except RuntimeError as e:  # capture refused: the same kernels through search_batch
+                logger.warning(f"query graph capture failed ({e}); searching without graphs")
+                self._graphs_ok = False
+                return None
             graphs[key] = g
         return g.search(dense, sparse), mode
 
