@@ -15,7 +15,11 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("m,n,k,epi", [(256, 256, 128, 0), (1000, 768, 768, 0),
                                        (2048, 3072, 768, 1), (517, 768, 3072, 0),
                                        (300, 2304, 768, 0), (4096, 768, 768, 1),
-                                       (77, 512, 192, 1)])
+                                       (77, 512, 192, 1),
+                                       # several tiles per workgroup: the K-tile stream crosses
+                                       # tile boundaries (next tile staged during an epilogue)
+                                       (70001, 2304, 768, 0), (20000, 3072, 768, 1),
+                                       (9000, 768, 3072, 0)])
 def test_linear_f16_matches_fp32(gpu, m, n, k, epi):
     from audio_rag_amd._armi import call, ptr, stream_handle
 
