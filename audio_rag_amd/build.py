@@ -19,7 +19,8 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 OUT_DIR = PKG / "_lib"
-LIB = OUT_DIR / "libarmi.so"
+# ARMI_LIB_OUT: write a probe build (ARMI_BUILD_FLAGS variants) elsewhere; load it with ARMI_LIB_PATH
+LIB = Path(os.environ["ARMI_LIB_OUT"]) if os.environ.get("ARMI_LIB_OUT") else OUT_DIR / "libarmi.so"
 OBJ_DIR = ROOT / "build" / "armi_obj"
 
 SOURCES = ["armi_common.cpp", "index.hip", "dense.hip", "sparse.hip", "rrf.hip", "encoder.hip",
@@ -63,7 +64,7 @@ def _compile(src: str, headers: list[Path], source_digest: str) -> Path:
 
 def build(verbose: bool = False) -> Path:
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
-    OUT_DIR.mkdir(parents=True, exist_ok=True)
+    LIB.parent.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h")) + [ROOT / "include" / "armi.h"]
     from audio_rag_amd._armi import source_digest
 
@@ -79,7 +80,7 @@ def build(verbose: bool = False) -> Path:
     os.replace(tmp, LIB)
     keep = {o.name for o in objs}
     for stale in OBJ_DIR.glob("*.o"):  # objects of superseded sources
-        if stale.name not in keep:
+        if stale.name not in keep and not os.environ.get("ARMI_LIB_OUT"):
             stale.unlink()
     if verbose:
         print(f"built {LIB}")
