@@ -1861,6 +1861,14 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
   const int n_help = (int)gridDim.x - nq;
   const int h = (int)blockIdx.x - nq;
   const int64_t lo = n_rows * h / n_help, hi = n_rows * (h + 1) / n_help;
+  // Nearly every call has no overflowed query: every thread checks its share of the queries at
+  // once (one load round trip, one barrier) before the per-query walk, whose dependent flag /
+  // count loads cost ~nq round trips (10 us at nq = 64, profiles/r04p: the helpers were the
+  // collect merge's whole time on certified calls).
+  bool any = false;
+  for (int q = tid; q < nq; q += kDenseMergeThreads)
+    any |= !(flags[q] & ARMI_FLAG_CERTIFIED) && col_cnt[q] > col_cap;
+  if (!__syncthreads_or(any)) return;  // workgroup-uniform
   for (int qg = 0; qg < nq; ++qg) {
     if ((flags[qg] & ARMI_FLAG_CERTIFIED) || col_cnt[qg] <= col_cap) continue;  // uniform
     int32_t qf[DIM / 64];
