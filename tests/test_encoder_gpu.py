@@ -282,6 +282,27 @@ def test_layernorm_f16_and_gelu_f16(gpu, width):
                                atol=2e-3)
 
 
+@pytest.mark.parametrize("width", [768, 1024])
+@pytest.mark.parametrize("rows", [1, 7, 300, 4097])  # odd counts: a half-wave with no row
+def test_add_layernorm_f16(gpu, width, rows):
+    """armi_enc_add_layernorm_f16: fp16 LayerNorm(x + res) of the all-fp16 residual stream (the
+    reranker's post-attention / post-FFN norm, XLMRobertaSelfOutput / XLMRobertaOutput) against
+    torch fp32 on the same fp16 inputs, within one fp16 rounding of the output."""
+    g = torch.Generator().manual_seed(rows + width)
+    x = torch.randn(rows, width, generator=g).half()
+    r = (torch.randn(rows, width, generator=g) * 2).half()
+    w, b = torch.randn(width, generator=g), torch.randn(width, generator=g)
+    ref = torch.nn.functional.layer_norm(x.float() + r.float(), (width,), w, b, 1e-5)
+    X, R, W, B = (t.to(gpu) for t in (x, r, w, b))
+    out16 = torch.full((rows + 1, width), float("nan"), dtype=torch.float16, device=gpu)
+    _call("armi_enc_add_layernorm_f16", X.data_ptr(), R.data_ptr(), W.data_ptr(), B.data_ptr(),
+          out16.data_ptr(), rows, width, 1e-5)
+    torch.cuda.synchronize()
+    got = out16.cpu().float()
+    torch.testing.assert_close(got[:rows], ref, rtol=2 ** -10, atol=1e-4)
+    assert torch.isnan(got[rows]).all()  # nothing written past the last row
+
+
 @pytest.mark.parametrize("L,residual", [(64, "fp16"), (256, "fp16"), (256, "fp32")])
 def test_cross_encoder_fp16_within_1e3(gpu, L, residual):
     """north_star: rerank scores within 1e-3 on the fp16 path (fp16 GEMMs + fused fp16
