@@ -38,6 +38,8 @@ using armi::TILE_ROWS;
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;
@@ -780,25 +782,40 @@ constexpr int kG2Rows = 256;  // rows per tile
 //     instruction over a scalar base.
 constexpr int kW4Threads = 256;
 constexpr int kW4Img = (kG2Rows + kGQB) * 64;  // one 32-wide k-step stage
-constexpr int kW4Norm = 4 * kW4Img;            // the two inverse-norm copies follow the ring
+constexpr int kW4Norm = 4 * kW4Img;            // the two row-scale copies follow the ring
 
 template <int DIM>
 constexpr size_t gemm_w4_lds_bytes() {
   constexpr size_t lists = (size_t)kGQB * 16 * 8 + kGQB * 4 * 4;
-  constexpr size_t ring = (size_t)kW4Norm + 2048;
+  constexpr size_t ring = (size_t)kW4Norm + 4096;
   return ring > lists ? ring : lists;
 }
 
+// I8 (round 4): the int8 x int8 form for k <= 64. Rows come from the index's int8 filter image
+// (rows8, tile-blocked, scattered row order; n_rows / ranges / row_mask in IMAGE positions) and
+// the queries from their per-call int8 quantisation (query_i8_kernel: q ~= s_q q8), both staged
+// by the same LDS-DMA pieces: a stage holds 64 components instead of 32 in the same 32 KB, and
+// v_mfma_i32_32x32x32_i8 (the fp16 MFMA's cycles at twice the K) takes the same fragment reads,
+// so a row tile costs half the k-loop. Each score is an UPPER BOUND of the fp16 row's cosine
+// (times |q|, the units of the int8 64-query scan): with D = x8.q8 (exact int32),
+//   x.q/|x| <= D s_q a32 + e32 (|q| + eq) + eq,   eq >= ||q - s_q q8||, e32 >= ||x - s_x x8||/|x|
+// (x.q = s_x s_q D + s_x x8.(q - s_q q8) + (x - s_x x8).q, Cauchy-Schwarz, s_x |x8| <= |x| +
+// ||x - s_x x8||), so dense_merge_kernel's exact rescore and certificate apply as for the int8
+// 64-query scan; the candidates' rows are converted to ordinals when the lists are written.
 // ABL (probe build only, results wrong): 1 no LDS-DMA pieces in the k-loop, 2 no tile
 // epilogue, 4 no MFMAs, 8 no mid-step barrier.
-template <int DIM, int ABL>
+template <int DIM, int ABL, bool I8>
 __global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void dense_gemm_scan_w4_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t rows_per_range, int n_ranges,
     int n_qb, const uint16_t* __restrict__ queries, int nq, float* __restrict__ cand_key,
-    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
-  constexpr int KT = DIM / 32;  // k-steps per row tile
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
+    const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
+    const int32_t* __restrict__ tile_ord, const int8_t* __restrict__ q8,
+    const float4* __restrict__ qsc) {
+  constexpr int KT = I8 ? DIM / 64 : DIM / 32;  // k-steps (stages) per row tile
+  typedef typename std::conditional<I8, i32x16, f32x16>::type acc_t;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int id = blockIdx.x;
@@ -817,10 +834,13 @@ void dense_gemm_scan_w4_kernel(
   const int n_here = (int)(hi - lo);
   const int last_row = (int)(n_rows - 1 - lo);                   // clamp target (row offset)
   const int last4 = (int)(((n_rows + 31) / 32) * 32 - 4 - lo);  // last 16-B group of the norms
-  const unsigned char* __restrict__ rsrc = reinterpret_cast<const unsigned char*>(rows + lo * DIM);
+  const unsigned char* __restrict__ rsrc =
+      I8 ? reinterpret_cast<const unsigned char*>(rows8 + lo * DIM)
+         : reinterpret_cast<const unsigned char*>(rows + lo * DIM);
   const unsigned char* __restrict__ qsrc =
-      reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
-  const float* __restrict__ inv_r = inv_norm32 + lo;
+      I8 ? reinterpret_cast<const unsigned char*>(q8 + (size_t)q_base * DIM)
+         : reinterpret_cast<const unsigned char*>(queries + (size_t)q_base * DIM);
+  const float* __restrict__ inv_r = (I8 ? a32 : inv_norm32) + lo;
 
   const int tid = threadIdx.x;
   const int wave = armi::wave_id();
@@ -852,7 +872,7 @@ void dense_gemm_scan_w4_kernel(
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int q = min(q_base + p * 64 + prow, nq - 1);
-    b_off[p] = (uint32_t)((q - q_base) * DIM * 2) + c16;
+    b_off[p] = (uint32_t)((q - q_base) * DIM * (I8 ? 1 : 2)) + c16;
   }
   auto issue_piece = [&](int st, int p) {
     const int tn = st / KT;
@@ -860,19 +880,32 @@ void dense_gemm_scan_w4_kernel(
     lds_ptr_t dst = (lds_ptr_t)(smem + (st & 3) * kW4Img + (p * 4 + wave) * 1024);
     if (p < 4) {
       const uint32_t row = (uint32_t)min(tn * kG2Rows + p * 64 + prow, last_row);
-      __builtin_amdgcn_global_load_lds(rsrc + t * 64 + (row * (uint32_t)(DIM * 2) + c16), dst, 16,
-                                       0, 0);
+      if constexpr (I8) {
+        // tile-blocked image: 16-B chunk cc of the 32-row tile's row rr at cc * 512 + rr * 16;
+        // stage t = chunks 4t .. 4t + 3
+        __builtin_amdgcn_global_load_lds(
+            rsrc + t * 2048 + ((row >> 5) * (uint32_t)(32 * DIM) + (row & 31) * 16 + c * 512), dst,
+            16, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds(rsrc + t * 64 + (row * (uint32_t)(DIM * 2) + c16), dst,
+                                         16, 0, 0);
+      }
     } else {
       __builtin_amdgcn_global_load_lds(qsrc + t * 64 + b_off[p - 4], dst, 16, 0, 0);
     }
   };
-  // inverse norms of row tile tn -> LDS [kW4Norm + (tn & 1) KB] (wave 0, 4 rows per lane;
-  // clamped to the padded norm array, rows past the range are masked anyway)
+  // row scales of row tile tn -> LDS [kW4Norm + (tn & 1) 2 KB] (wave 0, 4 rows per lane;
+  // clamped to the padded arrays, rows past the range are masked anyway): the inverse norms, or
+  // for I8 a32 then e32
   auto issue_norms = [&](int tn) {
     if (wave == 0) {
       const int rr = min(tn * kG2Rows + 4 * lane, last4);
-      __builtin_amdgcn_global_load_lds(inv_r + rr, (lds_ptr_t)(smem + kW4Norm + (tn & 1) * 1024),
+      __builtin_amdgcn_global_load_lds(inv_r + rr, (lds_ptr_t)(smem + kW4Norm + (tn & 1) * 2048),
                                        16, 0, 0);
+      if constexpr (I8)
+        __builtin_amdgcn_global_load_lds(e32 + lo + rr,
+                                         (lds_ptr_t)(smem + kW4Norm + (tn & 1) * 2048 + 1024), 16,
+                                         0, 0);
     }
   };
 
@@ -909,11 +942,32 @@ void dense_gemm_scan_w4_kernel(
     int zero = 0;
     asm volatile("; agpr-form hint %0" ::"a"(zero));
   }
-  f32x16 acc[4][4];
+  acc_t acc[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
+    for (int n = 0; n < 4; ++n) acc[m][n] = acc_t{};
+  auto mma = [&](u32x4 a, u32x4 b, acc_t c) -> acc_t {
+    if constexpr (I8)
+      return __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a),
+                                                   __builtin_bit_cast(i32x4, b), c, 0, 0, 0);
+    else
+      return mfma16(a, b, c);
+  };
+  // I8: the lane's queries' scales (q = q_base + wq 128 + n 32 + r): s_q, eq, |q| + eq
+  float qs_s[4] = {0.f, 0.f, 0.f, 0.f}, qs_e[4] = {0.f, 0.f, 0.f, 0.f}, qs_n[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (I8) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int q = q_base + wq * 128 + n * 32 + r;
+      if (q < nq) {
+        const float4 v = qsc[q];
+        qs_s[n] = v.x;
+        qs_e[n] = v.y;
+        qs_n[n] = v.z;
+      }
+    }
+  }
 
   // Tile epilogue without compares (one wave per SIMD: nothing overlaps it, so no wave-divergent
   // insertion per score and no lane masks): each score carries its row code m*16 + j in its 6 low
@@ -934,33 +988,45 @@ void dense_gemm_scan_w4_kernel(
       __builtin_amdgcn_sched_barrier(0);
       const int ro = tile * kG2Rows + wr * 128 + m * 32;  // row offset of the 32-row block
       const int64_t rb = lo + ro;
-      uint32_t linv = lds0 + (uint32_t)(kW4Norm + (tile & 1) * 1024 +
+      uint32_t linv = lds0 + (uint32_t)(kW4Norm + (tile & 1) * 2048 +
                                         (wr * 128 + m * 32 + 4 * h) * 4);
       // block m's norms are read after block m-1's scores are folded (else hipcc hoists the
       // four blocks' norms and masks together)
       asm volatile("" : "+v"(linv) : "v"(b3[0]), "v"(b3[1]), "v"(b3[2]), "v"(b3[3]));
-      u32x4 invw[4];
+      u32x4 invw[4], errw[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(invw[g]) : "v"(linv), "i"(32 * g));
+      if constexpr (I8) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(errw[g]) : "v"(linv), "i"(1024 + 32 * g));
+      }
       uint32_t valid = ro + 32 <= n_here ? 0xffffffffu
                                          : (ro >= n_here ? 0u : (1u << (n_here - ro)) - 1u);
       if (row_mask && valid) valid &= (uint32_t)(row_mask[rb >> 6] >> (rb & 63));
       asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(invw[0]), "+v"(invw[1]), "+v"(invw[2]), "+v"(invw[3]) :: "memory");
-      // score = fma(acc, inv, bias): (inv, 0) for a live row, (0, -FLT_MAX) otherwise
+                   : "+v"(invw[0]), "+v"(invw[1]), "+v"(invw[2]), "+v"(invw[3]), "+v"(errw[0]),
+                     "+v"(errw[1]), "+v"(errw[2]), "+v"(errw[3])::"memory");
+      // score = fma(acc, inv, bias): (inv, 0) for a live row, (0, -FLT_MAX) otherwise; I8:
+      // inv = a32, bias = e32 (dead: e32 = -FLT_MAX, folded per query below)
       float inv[16], bias[16];
       const uint32_t vb = valid >> (4 * h);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const uint32_t w4v[4] = {invw[g].x, invw[g].y, invw[g].z, invw[g].w};
+        const uint32_t e4v[4] = {errw[g].x, errw[g].y, errw[g].z, errw[g].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int j = 4 * g + e;
           const float iv = __uint_as_float(w4v[e]);
           const bool live = ((vb >> ((j & 3) + 8 * (j >> 2))) & 1u) && iv == iv;
           inv[j] = live ? iv : 0.0f;
-          bias[j] = live ? 0.0f : -3.4028234663852886e38f;
+          if constexpr (I8)
+            bias[j] = live ? __uint_as_float(e4v[e]) : -3.4028234663852886e38f;
+          else
+            bias[j] = live ? 0.0f : -3.4028234663852886e38f;
         }
       }
 #pragma unroll
@@ -971,7 +1037,16 @@ void dense_gemm_scan_w4_kernel(
         asm volatile("" : "+a"(acc[m][n]) : "v"(b3[(n + 3) & 3]));
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
+          float y;
+          if constexpr (I8) {
+            // D s_q a32 + (e32 (|q| + eq) + eq); a dead row's -FLT_MAX times a positive
+            // |q| + eq stays hugely negative (|q| + eq >= |q| > 0 for a query, 0 past nq)
+            const float sl = __builtin_fmaf(bias[j], qs_n[n], qs_e[n]);
+            y = __builtin_fmaf((float)acc[m][n][j], inv[j] * qs_s[n], sl);
+            y = bias[j] < -1.0e38f ? -3.4028234663852886e38f : y;
+          } else {
+            y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
+          }
           // code m*16 + j (an inline constant) in the low 6 mantissa bits
           const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
           const float t = fminf(b1[n], e);
@@ -1021,7 +1096,7 @@ void dense_gemm_scan_w4_kernel(
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
+        for (int n = 0; n < 4; ++n) acc[m][n] = acc_t{};
       for (int kt = 0; kt < KT; ++kt) {
         const int s = tile * KT + kt;
         // Stages past the last k-step are issued too (rows clamped into the store, never read),
@@ -1033,7 +1108,7 @@ void dense_gemm_scan_w4_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           if constexpr (!(ABL & 4))
-            acc[i >> 2][i & 3] = mfma16(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
+            acc[i >> 2][i & 3] = mma(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
           if (i < 8) read_item(s, 1, i);
           if (!(ABL & 1) && i >= 8 && (i & 1)) issue_piece(s3, (i - 8) >> 1);
           __builtin_amdgcn_sched_barrier(0);
@@ -1048,7 +1123,7 @@ void dense_gemm_scan_w4_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           if constexpr (!(ABL & 4))
-            acc[i >> 2][i & 3] = mfma16(fa[1][i >> 2], fb[1][i & 3], acc[i >> 2][i & 3]);
+            acc[i >> 2][i & 3] = mma(fa[1][i >> 2], fb[1][i & 3], acc[i >> 2][i & 3]);
           if (i < 8) read_item(s + 1, 0, i);
           if (!(ABL & 1) && i >= 8 && (i & 1)) issue_piece(s3, 4 + ((i - 8) >> 1));
           __builtin_amdgcn_sched_barrier(0);
@@ -1105,6 +1180,12 @@ void dense_gemm_scan_w4_kernel(
     }
     const int rank = (lane & 16) ? 15 - (lane & 15) : (lane & 15);
     const int qg = q_base + ql;
+    if constexpr (I8) {
+      // image position -> ordinal (armi_index.h: row rr of image tile tau is ordinal
+      // rr * T + tile_ord[tau])
+      const int64_t T = n_rows / 32;
+      if (row >= 0) row = (int32_t)((int64_t)(row & 31) * T + tile_ord[row >> 5]);
+    }
     if (qg < nq) {
       const size_t base = (size_t)rp * nq + qg;
       cand_key[base * kKW + rank] = key;
@@ -1114,6 +1195,89 @@ void dense_gemm_scan_w4_kernel(
         cand_bound[base] = fmaxf(fmaxf(dd[0], dd[1]), fmaxf(dd[2], dd[3]));
       }
     }
+  }
+}
+
+// Per-call int8 quantisation of the queries for the int8 tiled scan (one wave per query):
+// s_q = f max|q_i| / 127 with the f of {1, 0.8, 0.65, 0.5} whose clamped rounding
+// q8 = clamp(round(q / s_q), +-127) leaves the smallest residual (clipping a few large components
+// buys a finer step for the rest: the residual is in the bound whatever it is), and the scales
+// qsc[q] = (s_q, eq, |q| + eq, 0) with eq >= ||q - s_q q8||_2 and |q| rounded up. Rounding: the
+// computed residual r_i = fl(q_i - fl(s_q q8_i)) is within 2^-23 (|q_i| + |rho_i|) of the true
+// one, and the fp32 sum of DIM squares within DIM 2^-24 relative, so
+// eq = sqrt(sum r^2) (1 + 2^-10) + |q| 2^-20 bounds ||rho|| (DIM <= 1024).
+template <int DIM>
+__global__ __launch_bounds__(256) void query_i8_kernel(const uint16_t* __restrict__ queries,
+                                                       int nq, int8_t* __restrict__ q8,
+                                                       float4* __restrict__ qsc) {
+  const int q = blockIdx.x * 4 + armi::wave_id();
+  if (q >= nq) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  constexpr int CH = DIM / 8;               // 16-B chunks of 8 components
+  constexpr int PER = (CH + 63) / 64;
+  float v[PER][8];
+  float amax = 0.0f, ss = 0.0f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    u32x4 w = {0u, 0u, 0u, 0u};
+    if (c < CH) w = *reinterpret_cast<const u32x4*>(queries + (size_t)q * DIM + 8 * c);
+    const half8 hv = __builtin_bit_cast(half8, w);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[i][e] = (float)hv[e];
+      amax = fmaxf(amax, fabsf(v[i][e]));
+      ss += v[i][e] * v[i][e];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    amax = fmaxf(amax, __shfl_xor(amax, off));
+    ss += __shfl_xor(ss, off);
+  }
+  constexpr float kF[4] = {1.0f, 0.8f, 0.65f, 0.5f};
+  float err[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float sf = amax * kF[f] / 127.0f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = sf > 0.0f ? rintf(v[i][e] / sf) : 0.0f;
+        t = fminf(fmaxf(t, -127.0f), 127.0f);
+        const float res = v[i][e] - sf * t;
+        err[f] += res * res;
+      }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) err[f] += __shfl_xor(err[f], off);
+  }
+  int best = 0;
+#pragma unroll
+  for (int f = 1; f < 4; ++f) best = err[f] < err[best] ? f : best;
+  const float sq = amax * kF[best] / 127.0f;
+  float er = 0.0f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = sq > 0.0f ? rintf(v[i][e] / sq) : 0.0f;
+      t = fminf(fmaxf(t, -127.0f), 127.0f);
+      const float res = v[i][e] - sq * t;
+      er += res * res;
+      packed[e >> 2] |= ((uint32_t)(int32_t)t & 0xffu) << (8 * (e & 3));
+    }
+    if (c < CH)
+      *reinterpret_cast<u32x2*>(q8 + (size_t)q * DIM + 8 * c) = u32x2{packed[0], packed[1]};
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) er += __shfl_xor(er, off);
+  if (lane == 0) {
+    const float qn = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
+    const float eq = sqrtf(er) * (1.0f + 1.0f / 1024.0f) + qn * (1.0f / 1048576.0f);
+    qsc[q] = make_float4(sq, eq, qn + eq, 0.0f);
   }
 }
 
@@ -1429,7 +1593,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #pragma unroll
   for (int j = 0; j < kFilterBatch; ++j) {
     const int e = tid + j * kDenseMergeThreads;
-    if (e < pool && e % kKW == sel_col - 1) umax[e / kKW] = ord_key(kk[j]);
+    if (sel_col > 0 && e < pool && e % kKW == sel_col - 1) umax[e / kKW] = ord_key(kk[j]);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
@@ -1448,7 +1612,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
       u[i] = g < n_wg ? umax[g] : ord_key(kNegInf);
     }
     float t0 = kNegInf;
-    if (n_wg >= sel_rank) {
+    if (sel_col > 0 && n_wg >= sel_rank) {
       uint32_t prefix = 0;  // largest v with #{u >= v} >= r, i.e. the r-th largest key
       for (int bit = 31; bit >= 0; --bit) {
         const uint32_t cand = prefix | (1u << bit);
@@ -1465,7 +1629,33 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     }
   }
   __syncthreads(); MERGE_STAMP(2);
-  const float t0 = red[9];
+  float t0 = red[9];
+  if (sel_col == 0) {
+    // exact selection (the int8 tiled scan): t0 = the kc-th largest key of the whole pool, by a
+    // workgroup radix select over the keys held in registers (one barrier per bit; the per-wave
+    // counts alternate between two LDS slots). Its looser upper bounds make many list entries
+    // clear a list-statistics threshold, which overflowed kSelCap at 256 lists (r04w: every
+    // query of a 1M x 256 call uncertified); the exact threshold keeps ~kc entries.
+    int* wcnt = reinterpret_cast<int*>(rkey) + 320;  // [2][kMW], past umax / bpart
+    uint32_t kq[kFilterBatch];
+#pragma unroll
+    for (int j = 0; j < kFilterBatch; ++j) kq[j] = ord_key(kk[j]);
+    uint32_t prefix = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = prefix | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < kFilterBatch; ++j) c += __popcll(__ballot(kq[j] >= cand));
+      if (lane == 0) wcnt[(bit & 1) * 8 + wave] = c;
+      __syncthreads();
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < kDenseMergeThreads / 64; ++w) tot += wcnt[(bit & 1) * 8 + w];
+      if (tot >= kc) prefix = cand;
+    }
+    const uint32_t lowest = ord_key(kNegInf);
+    t0 = from_ord_key(prefix > lowest ? prefix : lowest);
+  }
 
   // filter the pool held in registers
   float dmax = kNegInf;
@@ -2110,6 +2300,20 @@ bool use_i8_filter(const armi_index* idx, int k) { return idx->rows8 != nullptr 
 // k = 40 at 1M random unit rows: ~110 rows reach the 40th cosine (bound slack 0.26 sigma at
 // 3.94 sigma), so 256; the collect pass catches whatever a smaller pool misses.
 int kc_i8(int k) { return k <= 10 ? 64 : (k <= 20 ? 128 : 256); }
+// The int8 x int8 tiled scan's bound adds the query's quantisation term (eq ~ ||q|| 0.006-0.009 at
+// dim 1024): about twice the slack of the 64-query int8 scan, so the merge rescores 256 rows. Its
+// certificate rate (r04s-u, random unit rows, 512 queries, top-5 with 128 rescored rows): 99.9 %
+// at 1.25M rows, 99.2 % at 125k, 94.5 % at 20k; one uncertified query costs the call a collect
+// pass over the shard. At k = 40 too many rows reach the 40th cosine through the slack (10 % of
+// 1.25M-row calls certified with 256). So it runs for k <= 5 (the metric's top-5) on shards of
+// >= 512k rows, where the halved k-loop (0.92 vs 1.41-1.49 ms at 1.25M x 512) outweighs the
+// larger rescore; otherwise the fp16 tiled scan.
+constexpr int kTiledI8MaxK = 5;
+constexpr int64_t kTiledI8MinRows = int64_t(1) << 19;
+int kc_tiled_i8(int) { return 256; }
+bool use_tiled_i8(const armi_index* idx, int k) {
+  return idx->rows8 != nullptr && k <= kTiledI8MaxK && idx->n_rows >= kTiledI8MinRows;
+}
 
 // dense_merge_kernel's rescore: fp32 keys of the kc best, exact keys only for the rows within the
 // fp32 error of the k-th, when kc > 64 (k > 10: hybrid's prefetch of 40 rescores 256); else every
@@ -2125,7 +2329,8 @@ bool merge_two_stage(int kc) {
 }
 
 // Threshold column of the merge's pool selection (dense_merge_kernel): the smallest J (power of
-// two, <= kKW) with r = ceil(kc / J) <= n_wg.
+// two, <= kKW) with r = ceil(kc / J) <= n_wg. (sel_col = 0 instead selects the pool's exact kc-th
+// key: the int8 tiled scan.)
 void merge_select(int kc, int n_wg, int& col, int& rank) {
   int j = 1;
   while (j < kKW && (kc + j - 1) / j > n_wg) j <<= 1;
@@ -2144,11 +2349,16 @@ struct GemmPlan {
   int grid = 0;
 };
 
-GemmPlan plan_gemm(const armi_index* idx, int nq) {
+// rows scanned by the tiled form: image positions (T * 32) for the int8 form, else the rows
+int64_t gemm_rows(const armi_index* idx, int k) {
+  return use_tiled_i8(idx, k) ? std::max<int64_t>(idx->n_tiles, 1) * 32 : idx->n_rows;
+}
+
+GemmPlan plan_gemm(const armi_index* idx, int nq, int64_t n_scan) {
   GemmPlan p;
   p.n_qb = (nq + kGQB - 1) / kGQB;
   const int cus = std::min(std::max(idx->num_cus, 1), 256);
-  const int64_t rows = std::max<int64_t>(idx->n_rows, 1);
+  const int64_t rows = std::max<int64_t>(n_scan, 1);
   int want = std::max(1, (cus + p.n_qb - 1) / p.n_qb);
   want = (int)std::min<int64_t>(want, (rows + kGRT - 1) / kGRT);  // >= one row tile per range
   // dense_gemm_scan_w4_kernel addresses a range's rows (plus one tile of clamped reads) with
@@ -2194,6 +2404,8 @@ struct Workspace {
   int32_t* col_list;   // [nq][kCollectCap] local rows
   int32_t* help_done;  // [nq] helper workgroups done with an overflowed query
   uint64_t* mask_img;  // row filter in int8 image order
+  int8_t* q8;          // [nq][dim] int8 queries of the int8 tiled scan
+  float4* qsc;         // [nq] their scales (query_i8_kernel)
   size_t bytes;
 };
 
@@ -2201,7 +2413,8 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
   armi::Carver cv(base);
   Workspace w{};
   if (fast) {
-    const int n_wg = use_gemm_scan(nq) ? plan_gemm(idx, nq).n_ranges : plan_scan(idx, k, nq).n_wg;
+    const int n_wg = use_gemm_scan(nq) ? plan_gemm(idx, nq, gemm_rows(idx, k)).n_ranges
+                                       : plan_scan(idx, k, nq).n_wg;
     w.cand_key = cv.take<float>((size_t)n_wg * nq * kKW);
     w.cand_row = cv.take<int32_t>((size_t)n_wg * nq * kKW);
     w.cand_bound = cv.take<float>((size_t)n_wg * nq);
@@ -2210,6 +2423,10 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
     w.help_done = cv.take<int32_t>(nq);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
+    if (use_gemm_scan(nq) && use_tiled_i8(idx, k)) {
+      w.q8 = cv.take<int8_t>((size_t)nq * idx->dim);
+      w.qsc = cv.take<float4>(nq);
+    }
   }
   w.inv_q = cv.take<double>(nq);
   w.qnorm = cv.take<double>(nq);
@@ -2285,17 +2502,26 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     mask_i8 = w.mask_img;
   }
   if (use_gemm_scan(nq)) {
-    const GemmPlan gp = plan_gemm(idx, nq);
+    const bool i8 = use_tiled_i8(idx, k);
+    const int64_t n_scan = gemm_rows(idx, k);
+    const GemmPlan gp = plan_gemm(idx, nq, n_scan);
     n_wg = gp.n_ranges;
     ARMI_REQUIRE((gp.rows_per_range + kG2Rows) * (int64_t)DIM * 2 < (int64_t(1) << 32),
                  "armi_dense_topk: row range too large for the tiled scan");
-    auto kern = dense_gemm_scan_w4_kernel<DIM, 0>;
+    if (i8) {
+      kc = kc_tiled_i8(k);
+      query_i8_kernel<DIM><<<dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream>>>(queries, nq,
+                                                                                     w.q8, w.qsc);
+      ARMI_LAUNCHED("query_i8_kernel");
+    }
+    auto kern = i8 ? dense_gemm_scan_w4_kernel<DIM, 0, true> : dense_gemm_scan_w4_kernel<DIM, 0, false>;
     if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     kern<<<dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(), stream>>>(
-        idx->rows, idx->inv_norm32, row_mask, idx->n_rows, gp.rows_per_range, gp.n_ranges,
-        gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
+        idx->rows, idx->inv_norm32, i8 ? mask_i8 : row_mask, n_scan, gp.rows_per_range,
+        gp.n_ranges, gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, idx->rows8,
+        idx->a32, idx->e32, idx->tile_ord, w.q8, w.qsc);
     ARMI_LAUNCHED("dense_gemm_scan_w4_kernel");
     if (int rc = tl.end()) return rc;
   } else if (use_i8_filter(idx, k)) {
@@ -2326,6 +2552,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                "dense merge: the candidate pool must fit one filter round (<= 256 lists)");
   int sel_col = 1, sel_rank = kc;
   merge_select(kc, n_wg, sel_col, sel_rank);
+  if (use_gemm_scan(nq) && use_tiled_i8(idx, k)) sel_col = 0;  // exact pool selection
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
@@ -2386,7 +2613,8 @@ extern "C" {
 int armi_dense_scan_form(const armi_index* idx, int n_queries, int k) {
   if (!idx || n_queries <= 0 || k <= 0) return -1;
   k = std::min(k, kMaxK);
-  if (use_gemm_scan(n_queries)) return ARMI_SCAN_TILED_FP16;
+  if (use_gemm_scan(n_queries))
+    return use_tiled_i8(idx, k) ? ARMI_SCAN_TILED_INT8 : ARMI_SCAN_TILED_FP16;
   return use_i8_filter(idx, k) ? ARMI_SCAN_INT8_FILTER : ARMI_SCAN_FP16;
 }
 

@@ -40,7 +40,7 @@ METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # dense (non-sparse) matrix peaks, MI355X_MICROARCH.md: bf16/f16 ~2.5 PF; fp32-input MFMA runs at
 # 1/16 of the bf16 rate (cdna_hip_programming.md §3 'FP32-input MFMA')
-MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.0}
+MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.0, "i8": 5000.0}  # dense, no sparsity
 
 # measured fp16 MFMA ceiling under the chip's clock management (back-to-back MFMAs on random
 # operands hold ~1.63 GHz, not 2.4): profiles/r02o_mfma_ceiling.txt; reported beside the spec peak
@@ -220,7 +220,7 @@ TRAFFIC_DIR = ROOT / "profiles" / "traffic"
 
 def traffic_key(form: int, n_rows: int, dim: int, n_queries: int, corpus: str) -> str:
     """Name of the committed PMC measurement of one scan shape (tools/pmc_dense_traffic.sh)."""
-    name = {0: "fp16", 1: "i8", 2: "tiled"}.get(form, f"form{form}")
+    name = {0: "fp16", 1: "i8", 2: "tiled", 3: "tiled_i8"}.get(form, f"form{form}")
     return f"dense_{name}_{corpus}_n{n_rows}_d{dim}_q{n_queries}"
 
 
@@ -486,14 +486,20 @@ def main() -> None:
         # int8 filter image (1 B / component) + a32, e32 (8 B / row) + the fp16 queries
         alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim * 2
         scan_kernel = f"dense_scan_i8_kernel<{dim}, false>"
+    elif form == _armi.SCAN_TILED_INT8:
+        # int8 image + a32, e32 per row; the call's int8 queries (1 B / component)
+        alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim
+        scan_kernel = f"dense_gemm_scan_w4_kernel<{dim}, 0, true>"
     else:
         alg_bytes = shard_rows * dim * 2 + shard_rows * 4 + nq_scan * dim * 2
         scan_kernel = (f"dense_scan_kernel<{dim}>" if form == _armi.SCAN_FP16
-                       else f"dense_gemm_scan_w4_kernel<{dim}, 0>")
+                       else f"dense_gemm_scan_w4_kernel<{dim}, 0, false>")
     alg_flops = 2.0 * shard_rows * dim * nq_scan
     # the scan's bound: HBM while the batch is small (arithmetic intensity ~ queries/pass flop/B),
-    # the fp16 MFMA once the all-gathered batch of a multi-GPU step passes the ridge
-    mfma_bound = alg_flops / (MFMA_PEAK_TFLOPS["fp16"] * 1e12) > alg_bytes / (HBM_PEAK_GBS * 1e9)
+    # the MFMA (fp16, or int8 for the int8 tiled form: 2x the fp16 rate) once the all-gathered
+    # batch of a multi-GPU step passes the ridge
+    mfma_dtype = "i8" if form == _armi.SCAN_TILED_INT8 else "fp16"
+    mfma_bound = alg_flops / (MFMA_PEAK_TFLOPS[mfma_dtype] * 1e12) > alg_bytes / (HBM_PEAK_GBS * 1e9)
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = (read_traffic(traffic_key(form, shard_rows, dim, nq_scan, args.corpus))
                             if world == 1 else (None, None))
@@ -551,11 +557,12 @@ def main() -> None:
             "bound": "mfma",
             "kernel": scan_kernel,
             "achieved": alg_flops / (scan_avg_ms * 1e-3) / 1e12,
-            "peak": MFMA_PEAK_TFLOPS["fp16"],
-            "unit": "TFLOP/s",
-            "frac": alg_flops / (scan_avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["fp16"],
+            "peak": MFMA_PEAK_TFLOPS[mfma_dtype],
+            "unit": "TFLOP/s" if mfma_dtype == "fp16" else "TOPS (int8)",
+            "frac": alg_flops / (scan_avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS[mfma_dtype],
             "frac_of_measured_ceiling": (alg_flops / (scan_avg_ms * 1e-3) / 1e12
-                                         / MFMA_PRACTICAL_TFLOPS["fp16"]),
+                                         / MFMA_PRACTICAL_TFLOPS["fp16"]
+                                         if mfma_dtype == "fp16" else None),
             "traffic": None,
             "algorithmic_flops_per_launch": alg_flops,
             "algorithmic_bytes_per_launch": alg_bytes,

@@ -87,7 +87,7 @@ int64_t armi_index_invalid_rows(const armi_index* index);
  *   inv_norm32[r]= (float)(inv_norm[r] * 2^24)          (scale factor of the fast scan)
  * The index also keeps an int8 filter image of the rows (1 B per component, built at create
  * time: s_r = max_i |x_ri| / 127, round(x_ri / s_r)) with s_r / |x_r| and a Cauchy-Schwarz bound
- * of the quantisation error per row; the 64-query scan reads it for k <= 16 (armi_dense_scan_form). */
+ * of the quantisation error per row; the scans read it for k <= 64 (armi_dense_scan_form). */
 int armi_index_norms(const armi_index* index, const int64_t** norm2, const double** inv_norm,
                      const float** inv_norm32);
 
@@ -95,12 +95,17 @@ int armi_index_norms(const armi_index* index, const int64_t** norm2, const doubl
  *   ARMI_SCAN_FP16         64-query scan over the fp16 rows (2 B per component)
  *   ARMI_SCAN_INT8_FILTER  64-query scan over the index's int8 filter image (1 B per component
  *                          + 8 B per row), then an exact fp16 rescore of the best upper bounds
- *                          (k <= 16; the default for those k)
- *   ARMI_SCAN_TILED_FP16   > 128 queries: the LDS-tiled MFMA scan over the fp16 rows
+ *                          (k <= 64; the default for those k)
+ *   ARMI_SCAN_TILED_FP16   > 128 queries otherwise: the LDS-tiled MFMA scan over the fp16 rows
+ *   ARMI_SCAN_TILED_INT8   > 128 queries, k <= 5, >= 512k rows: the LDS-tiled int8 x int8 MFMA
+ *                          scan over the int8 image and per-call int8 queries (upper bounds),
+ *                          then the exact fp16 rescore (the all-gathered batch of a multi-GPU
+ *                          step over a large shard)
  * Results are the same exact ranking on every form. -1 for invalid arguments. */
 #define ARMI_SCAN_FP16 0
 #define ARMI_SCAN_INT8_FILTER 1
 #define ARMI_SCAN_TILED_FP16 2
+#define ARMI_SCAN_TILED_INT8 3
 int armi_dense_scan_form(const armi_index* index, int n_queries, int k);
 
 /* Workspace bytes needed by armi_dense_topk for n_queries queries and top-k. */
