@@ -2301,15 +2301,16 @@ bool use_i8_filter(const armi_index* idx, int k) { return idx->rows8 != nullptr 
 // 3.94 sigma), so 256; the collect pass catches whatever a smaller pool misses.
 int kc_i8(int k) { return k <= 10 ? 64 : (k <= 20 ? 128 : 256); }
 // The int8 x int8 tiled scan's bound adds the query's quantisation term (eq ~ ||q|| 0.006-0.009 at
-// dim 1024): about twice the slack of the 64-query int8 scan, so the merge rescores 256 rows. Its
-// certificate rate (r04s-u, random unit rows, 512 queries, top-5 with 128 rescored rows): 99.9 %
-// at 1.25M rows, 99.2 % at 125k, 94.5 % at 20k; one uncertified query costs the call a collect
-// pass over the shard. At k = 40 too many rows reach the 40th cosine through the slack (10 % of
-// 1.25M-row calls certified with 256). So it runs for k <= 5 (the metric's top-5) on shards of
-// >= 512k rows, where the halved k-loop (0.92 vs 1.41-1.49 ms at 1.25M x 512) outweighs the
-// larger rescore; otherwise the fp16 tiled scan.
+// dim 1024): about twice the slack of the 64-query int8 scan, so the merge rescores 256 rows,
+// selected exactly from the pool. One uncertified query costs the call a collect pass over the
+// shard, so the form runs where its certificate holds and its halved k-loop pays
+// (tools/probes/tiled_i8_cert.py, random unit rows, top-5; profiles/r04y_tiled_i8_threshold.txt):
+// 100 % certified from 250k rows up (250k x 256: 201 vs 229 us per call on the fp16 form; 1.25M x
+// 512: 1.10 vs ~1.45 ms), 98.6-99.2 % at 65k-125k rows (then slower than the fp16 form). At k = 40
+// too many rows reach the 40th cosine through the slack (10 % of 1.25M-row calls certified, r04s).
+// So: k <= 5 (the metric's top-5) on shards of >= 200k rows; otherwise the fp16 tiled scan.
 constexpr int kTiledI8MaxK = 5;
-constexpr int64_t kTiledI8MinRows = int64_t(1) << 19;
+constexpr int64_t kTiledI8MinRows = 200000;
 int kc_tiled_i8(int) { return 256; }
 bool use_tiled_i8(const armi_index* idx, int k) {
   return idx->rows8 != nullptr && k <= kTiledI8MaxK && idx->n_rows >= kTiledI8MinRows;

@@ -97,7 +97,7 @@ int armi_index_norms(const armi_index* index, const int64_t** norm2, const doubl
  *                          + 8 B per row), then an exact fp16 rescore of the best upper bounds
  *                          (k <= 64; the default for those k)
  *   ARMI_SCAN_TILED_FP16   > 128 queries otherwise: the LDS-tiled MFMA scan over the fp16 rows
- *   ARMI_SCAN_TILED_INT8   > 128 queries, k <= 5, >= 512k rows: the LDS-tiled int8 x int8 MFMA
+ *   ARMI_SCAN_TILED_INT8   > 128 queries, k <= 5, >= 200k rows: the LDS-tiled int8 x int8 MFMA
  *                          scan over the int8 image and per-call int8 queries (upper bounds),
  *                          then the exact fp16 rescore (the all-gathered batch of a multi-GPU
  *                          step over a large shard)

@@ -71,7 +71,7 @@ def test_scan_form_by_k(gpu, oracle_mod):
     assert idx.scan_form(64, 40) == _armi.SCAN_INT8_FILTER  # the reference's hybrid prefetch
     assert idx.scan_form(64, 64) == _armi.SCAN_INT8_FILTER
     assert idx.scan_form(64, 65) == _armi.SCAN_FP16
-    assert idx.scan_form(300, 5) == _armi.SCAN_TILED_FP16  # < 512k rows: the fp16 tiled scan
+    assert idx.scan_form(300, 5) == _armi.SCAN_TILED_FP16  # < 200k rows: the fp16 tiled scan
 
 
 @pytest.mark.parametrize("k", [1, 5, 6, 7, 10, 16, 17, 40, 65])

@@ -1,4 +1,4 @@
-"""The int8 x int8 tiled scan (ARMI_SCAN_TILED_INT8: > 128 queries, k <= 5, shards of >= 512k
+"""The int8 x int8 tiled scan (ARMI_SCAN_TILED_INT8: > 128 queries, k <= 5, shards of >= 200k
 rows): dense_gemm_scan_w4_kernel<dim, 0, true> over the index's int8 image and the call's int8
 queries, keys = certified upper bounds, exact fp16 rescore and certificate in dense_merge_kernel,
 collect pass for whatever is not certified. Results must equal the exhaustive exact scan bit for
