@@ -954,17 +954,24 @@ void dense_gemm_scan_w4_kernel(
     else
       return mfma16(a, b, c);
   };
-  // I8: the lane's queries' scales (q = q_base + wq 128 + n 32 + r): s_q, eq, |q| + eq
-  float qs_s[4] = {0.f, 0.f, 0.f, 0.f}, qs_e[4] = {0.f, 0.f, 0.f, 0.f}, qs_n[4] = {0.f, 0.f, 0.f, 0.f};
+  // I8: the lane's queries (q = q_base + wq 128 + n 32 + r). Scores are kept divided by s_q
+  // (one query per (lane, n), so the lane's and the workgroup's comparisons see one scale):
+  // u = D a32 + e32 c1 + c2 with c1 = (|q| + eq) / s_q, c2 = eq / s_q, and s_q u is written to
+  // the candidate lists. A zero query (s_q = 0: D = eq = |q| = 0) keeps scale 1, c1 = 1, c2 = 0
+  // (e32 >= 0 still bounds its 0 cosine; c1 >= 1 keeps a dead row's key at -inf / -FLT_MAX).
+  float qs_s[4] = {1.f, 1.f, 1.f, 1.f}, qs_c1[4] = {1.f, 1.f, 1.f, 1.f},
+        qs_c2[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (I8) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int q = q_base + wq * 128 + n * 32 + r;
       if (q < nq) {
         const float4 v = qsc[q];
-        qs_s[n] = v.x;
-        qs_e[n] = v.y;
-        qs_n[n] = v.z;
+        if (v.x > 0.0f) {
+          qs_s[n] = v.x;
+          qs_c1[n] = v.z / v.x;
+          qs_c2[n] = v.y / v.x;
+        }
       }
     }
   }
@@ -1039,21 +1046,24 @@ void dense_gemm_scan_w4_kernel(
         for (int j = 0; j < 16; ++j) {
           float y;
           if constexpr (I8) {
-            // D s_q a32 + (e32 (|q| + eq) + eq); a dead row's -FLT_MAX times a positive
-            // |q| + eq stays hugely negative (|q| + eq >= |q| > 0 for a query, 0 past nq)
-            const float sl = __builtin_fmaf(bias[j], qs_n[n], qs_e[n]);
-            y = __builtin_fmaf((float)acc[m][n][j], inv[j] * qs_s[n], sl);
-            y = bias[j] < -1.0e38f ? -3.4028234663852886e38f : y;
+            // D a32 + e32 c1 + c2 (divided by s_q). A dead row (inv 0, bias -FLT_MAX) gives -inf
+            // (c1 >= 1), clamped to -FLT_MAX: the row code would turn -inf into a NaN, which the
+            // chain below is not transparent to (a NaN moves b1 into b2)
+            y = __builtin_elementwise_maximumnum(
+                __builtin_fmaf((float)acc[m][n][j], inv[j],
+                               __builtin_fmaf(bias[j], qs_c1[n], qs_c2[n])),
+                -3.4028234663852886e38f);
           } else {
             y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
           }
           // code m*16 + j (an inline constant) in the low 6 mantissa bits
           const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
-          const float t = fminf(b1[n], e);
-          b1[n] = fmaxf(b1[n], e);
-          const float t2 = fminf(b2[n], t);
-          b2[n] = fmaxf(b2[n], t);
-          b3[n] = fmaxf(b3[n], t2);
+          // (no NaN reaches the chain)
+          const float t = __builtin_elementwise_minimumnum(b1[n], e);
+          b1[n] = __builtin_elementwise_maximumnum(b1[n], e);
+          const float t2 = __builtin_elementwise_minimumnum(b2[n], t);
+          b2[n] = __builtin_elementwise_maximumnum(b2[n], t);
+          b3[n] = __builtin_elementwise_maximumnum(b3[n], t2);
         }
       }
     }
@@ -1154,10 +1164,10 @@ void dense_gemm_scan_w4_kernel(
       const int q = wq * 128 + n * 32 + r;
 #pragma unroll
       for (int j = 0; j < kLaneList; ++j) {
-        lkey[q * 16 + slot + j] = sl[n][j];
+        lkey[q * 16 + slot + j] = sl[n][j] * qs_s[n];  // I8: back to key units (else * 1)
         lrow[q * 16 + slot + j] = il[n][j];
       }
-      ldisc[q * 4 + wr * 2 + h] = dl[n];
+      ldisc[q * 4 + wr * 2 + h] = dl[n] * qs_s[n];
     }
   }
   __syncthreads();
