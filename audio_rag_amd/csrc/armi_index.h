@@ -66,6 +66,13 @@ struct armi_sparse_index {
   int32_t* post = nullptr;       // [n_postings + 128][2]: (row, value bits) per posting
   int32_t* long_of = nullptr;    // [vocab] index into start_tab, -1 for short terms
   int32_t* start_tab = nullptr;  // [n_long][n_ranges]
+  // Dense columns (round 4): a term in at least 1/8 of the rows also keeps its value bits per row
+  // (0 = no posting, a zero value as -0.0, like the postings), so the scan stages its tile by one
+  // coalesced load instead of cursor, ballot and scatter work.
+  int32_t n_dense = 0;
+  int64_t dense_stride = 0;      // words per column (rows rounded up, + one tile of zeros)
+  int32_t* dense_of = nullptr;   // [vocab] column of the term, -1
+  uint32_t* dense_val = nullptr; // [n_dense][dense_stride]
 };
 
 namespace armi {

@@ -135,6 +135,40 @@ __global__ void sentinels_kernel(const int32_t* __restrict__ term_ptr, int32_t v
   if (t < kPad) post[n_postings + t] = make_int2(kEndRow, 0);
 }
 
+// dense columns: flag[t] = 1 for a term in >= 1/8 of the rows (df = postings - its sentinel)
+__global__ void dense_flag_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
+                                  int64_t n_rows, int32_t* __restrict__ flag) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < vocab) {
+    const int64_t df = term_ptr[t + 1] - 1 - term_ptr[t];
+    flag[t] = (df > 0 && df * 8 >= n_rows) ? 1 : 0;
+  } else if (t == vocab) {
+    flag[t] = 0;
+  }
+}
+
+__global__ void dense_of_kernel(const int32_t* __restrict__ flag, const int32_t* __restrict__ scan,
+                                int32_t vocab, int32_t* __restrict__ dense_of) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < vocab) dense_of[t] = flag[t] ? scan[t] : -1;
+}
+
+// value bits of every posting of a dense term into its column (the postings' encoding)
+__global__ void dense_fill_kernel(const int32_t* __restrict__ term_ptr,
+                                  const int32_t* __restrict__ dense_of,
+                                  const int2* __restrict__ post, int64_t n_postings,
+                                  const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
+                                  int64_t stride, uint32_t* __restrict__ dense_val) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const uint32_t t = skeys[i];
+  if (t >= (uint32_t)vocab) return;
+  const int32_t d = dense_of[t];
+  if (d < 0) return;
+  const int2 pv = post[i + t];  // the posting postings_kernel wrote for sorted entry i
+  dense_val[(size_t)d * stride + pv.x] = (uint32_t)pv.y;
+}
+
 __global__ void long_of_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
                                const int32_t* __restrict__ scan, int32_t* __restrict__ long_of) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -551,7 +585,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const int32_t* __restrict__ qof, int2* __restrict__ cursors,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
-    int32_t* __restrict__ coll_row, int dbg) {
+    int32_t* __restrict__ coll_row, int dbg, const int32_t* __restrict__ dense_of,
+    const uint32_t* __restrict__ dense_val, int64_t dense_stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][kTile]
   const int g = blockIdx.x;
   const int wave = armi::wave_id();
@@ -582,13 +617,21 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   int2 creg = make_int2(0, kEndRow);
   {
     const int s = lane / kHold, u = s * kU + (lane % kHold) * kWaves + wave;
-    if (s < nSeg && u < nU)
-      creg = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, post);
+    if (s < nSeg && u < nU) {
+      const int32_t t = uterm[u];
+      const int32_t d = dense_of[t];
+      creg = d >= 0 ? make_int2(-(d + 1), 0)
+                    : range_cursor(t, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
+    }
   }
   for (int s = kRegSegs; s < nSeg; ++s) {
     const int u = s * kU + lane * kWaves + wave;
-    if (lane < kHold && u < nU)
-      gcur[u] = range_cursor(uterm[u], g, lo, n_ranges, term_ptr, long_of, start_tab, post);
+    if (lane < kHold && u < nU) {
+      const int32_t t = uterm[u];
+      const int32_t d = dense_of[t];
+      gcur[u] = d >= 0 ? make_int2(-(d + 1), 0)
+                       : range_cursor(t, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
+    }
   }
 
   // per lane (= row pair within the tile) and query: the two best rows seen in this lane, plus
@@ -617,6 +660,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   typedef int32_t p4 __attribute__((ext_vector_type(4), aligned(8)));
   p4 sp[kHold];
   uint32_t amask = 0;
+  uint32_t dmask = 0;  // held terms of the staged step that are dense columns (cursor.x < 0)
   int2 scv = make_int2(0, kEndRow);
   const int rev2 = 2 * (63 - lane);
   // scatter target of a lane whose posting is outside the tile: a 64-entry scratch row
@@ -631,13 +675,23 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const bool mine = l >= 0 && l < kHold && u < nU;
     if (seg >= kRegSegs) cv = mine ? gcur[u] : make_int2(0, kEndRow);
     amask = (uint32_t)(__ballot(mine && cv.y < thi) >> base) & ((1u << kHold) - 1u);
+    dmask = (uint32_t)(__ballot(mine && cv.x < 0) >> base) & ((1u << kHold) - 1u);
     if (dbg & 2) amask = 0;
     scv = cv;
+    const int64_t tlo = lo + (int64_t)tile * kTile;
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       if ((amask >> k) & 1u) {
-        const int2* pc = post + rl_i(cv.x, base + k);  // uniform
-        sp[k] = *reinterpret_cast<const p4*>(pc + rev2);
+        const int cx = rl_i(cv.x, base + k);  // uniform
+        if (cx < 0) {
+          // dense column: the tile's value bits, rows tlo + 2 lane and + 1 in .x / .y (zero past
+          // the store). A 16-B load straight into sp[k] (.z / .w unused): an 8-B load into part
+          // of it would need a copy, i.e. a wait for the load here instead of in finish
+          sp[k] = *reinterpret_cast<const p4*>(dense_val + (size_t)(-cx - 1) * dense_stride + tlo +
+                                               2 * lane);
+        } else {
+          sp[k] = *reinterpret_cast<const p4*>(post + cx + rev2);
+        }
       }
     }
   };
@@ -661,6 +715,10 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
     for (int k = 0; k < kHold; ++k) {
       uint32_t* row = buf + (k * kWaves + wave) * kTile;
+      if ((amask & dmask) >> k & 1u) {  // dense column: the whole row image, no clear, no cursor
+        reinterpret_cast<uint2*>(row)[lane] = make_uint2((uint32_t)sp[k].x, (uint32_t)sp[k].y);
+        continue;
+      }
       if ((dm >> k) & 1u) reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
       if ((amask >> k) & 1u) {
         const uint64_t be = __ballot(sp[k].x < thi), bo = __ballot(sp[k].z < thi);
@@ -1248,6 +1306,35 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
                                                              idx->start_tab);
     ARMI_LAUNCHED("start_tab_kernel");
   }
+  // dense columns (at most 4x the bytes of their postings: df >= rows / 8, 4 B per row)
+  int32_t *dflag, *dscan;
+  ARMI_HIP(tmp.alloc(&dflag, (size_t)vocab + 1));
+  ARMI_HIP(tmp.alloc(&dscan, (size_t)vocab + 1));
+  dense_flag_kernel<<<grid_for((int64_t)vocab + 1, 256), 256, 0, stream>>>(idx->term_ptr, vocab,
+                                                                          idx->n_rows, dflag);
+  ARMI_LAUNCHED("dense_flag_kernel");
+  size_t dscan_bytes = 0;
+  ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, dscan_bytes, dflag, dscan, vocab + 1, stream));
+  unsigned char* dscan_tmp;
+  ARMI_HIP(tmp.alloc(&dscan_tmp, dscan_bytes));
+  ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(dscan_tmp, dscan_bytes, dflag, dscan, vocab + 1, stream));
+  int32_t n_dense = 0;
+  ARMI_HIP(hipMemcpyAsync(&n_dense, dscan + vocab, 4, hipMemcpyDeviceToHost, stream));
+  ARMI_HIP(hipStreamSynchronize(stream));
+  idx->n_dense = n_dense;
+  idx->dense_stride = (idx->n_rows + kTile - 1) / kTile * kTile + kTile;  // + the 16-B over-read
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->dense_of), std::max<size_t>(vocab, 1) * 4));
+  dense_of_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(dflag, dscan, vocab, idx->dense_of);
+  ARMI_LAUNCHED("dense_of_kernel");
+  const size_t dense_words = std::max<size_t>((size_t)n_dense * idx->dense_stride, 1);
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->dense_val), dense_words * 4));
+  ARMI_HIP(hipMemsetAsync(idx->dense_val, 0, dense_words * 4, stream));
+  if (nnz > 0 && n_dense > 0) {
+    dense_fill_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(
+        idx->term_ptr, idx->dense_of, reinterpret_cast<const int2*>(idx->post), idx->n_postings,
+        skeys, nnz, vocab, idx->dense_stride, idx->dense_val);
+    ARMI_LAUNCHED("dense_fill_kernel");
+  }
   ARMI_HIP(hipStreamSynchronize(stream));
   return ARMI_OK;
 }
@@ -1257,6 +1344,8 @@ void free_index(armi_sparse_index* idx) {
   (void)hipFree(idx->post);
   (void)hipFree(idx->long_of);
   (void)hipFree(idx->start_tab);
+  (void)hipFree(idx->dense_of);
+  (void)hipFree(idx->dense_val);
   delete idx;
 }
 
@@ -1446,7 +1535,8 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
-        w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg);
+        w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg,
+        idx->dense_of, idx->dense_val, idx->dense_stride);
     ARMI_LAUNCHED("sparse_scan_kernel");
     if (int rc = tl.end()) return rc;
 #ifdef ARMI_SPARSE_PROFILE
@@ -1478,7 +1568,8 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     sparse_scan_kernel<true><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
-        w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg);
+        w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg,
+        idx->dense_of, idx->dense_val, idx->dense_stride);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp), dim3(256), lds_collect, stream>>>(
         w.coll_count, w.coll_key, w.coll_row, q0, k, idx->ordinal_base, out_scores, out_ids,
