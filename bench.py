@@ -594,12 +594,17 @@ def main() -> None:
         result["rerank_share_of_step"] = (rr_ms * 1e-3) / elapsed
     if sindex is not None and world == 1:
         # sparse scan roofline: algorithmic bytes of a 64-query pass = sum over the pass's
-        # distinct terms of 8 B (row int32 + value fp32) per posting
+        # distinct terms of what the scan must read for them: 8 B (row int32 + value fp32) per
+        # posting, or 4 B per row for a term in >= 1/8 of the rows (the index's dense columns)
         sp_ms, sp_n = _armi.ctypes.c_double(), _armi.ctypes.c_int64()
         _armi.call("armi_kernel_timing_read", _armi.TIMING_SPARSE_SCAN, _armi.ctypes.byref(sp_ms),
                    _armi.ctypes.byref(sp_n))
         post = torch.bincount(csr[1].long(), minlength=VOCAB)
-        pass_bytes = [8.0 * float(post[torch.unique(qs[1].long())].sum()) for qs in q_sparse]
+        def term_bytes(df: torch.Tensor) -> float:
+            dense = df * 8 >= n
+            return float(torch.where(dense, torch.full_like(df, 4 * n), 8 * df).sum())
+
+        pass_bytes = [term_bytes(post[torch.unique(qs[1].long())]) for qs in q_sparse]
         alg = sum(pass_bytes[i % n_q_batches] for i in range(args.steps)) / max(args.steps, 1)
         if sp_n.value:
             sp_avg = sp_ms.value / sp_n.value
@@ -613,7 +618,8 @@ def main() -> None:
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": sp_avg,
                 "launches_timed": sp_n.value,
                 "note": "algorithmic bytes = sum over the distinct terms of the 64-query pass of "
-                        "8 B per posting; the kernel is instruction/latency-bound (DESIGN §3)"}
+                        "8 B per posting (4 B per row for dense-column terms, df >= rows/8); the "
+                        "kernel is instruction/latency-bound (DESIGN §3)"}
     result["cpu_baseline"] = None
     if world == 1 and not args.no_cpu_baseline:
         ref = CpuReference(rows, csr)
