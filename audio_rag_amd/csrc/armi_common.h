@@ -168,6 +168,67 @@ __device__ __forceinline__ void wave_sort_rank_desc(double& key, int64_t& ord) {
   }
 }
 
+// Lane l reads lane l ^ S, without the LDS pipe (ds_bpermute): S = 1, 2 one DPP quad
+// permutation, 4 a half-row mirror then a quad reversal ((l ^ 7) ^ 3), 8 a row rotation by 8,
+// 16 / 32 one v_permlane16/32_swap of the value with itself (the swapped row of the other half)
+// and a select.
+#ifndef ARMI_SORT_DPP
+#define ARMI_SORT_DPP 1  // 0: ds_bpermute (__shfl_xor) as before round 4 (r04ai: 100k step -2 %)
+#endif
+template <int S>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  static_assert(S == 1 || S == 2 || S == 4 || S == 8 || S == 16 || S == 32, "lane xor");
+  if constexpr (S == 1) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (S == 2) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (S == 4) {
+    const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x1B, 0xF, 0xF, false);
+  } else if constexpr (S == 8) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (S == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? (uint32_t)p[0] : (uint32_t)p[1];
+  } else {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? (uint32_t)p[0] : (uint32_t)p[1];
+  }
+}
+
+template <int S, int N>
+__device__ __forceinline__ void xor_exchange_n(const float (&key)[N], const int32_t (&row)[N],
+                                               float (&ok)[N], int32_t (&orow)[N]) {
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+#if ARMI_SORT_DPP
+    ok[n] = __uint_as_float(xor_lane<S>(__float_as_uint(key[n])));
+    orow[n] = (int32_t)xor_lane<S>((uint32_t)row[n]);
+#else
+    ok[n] = __shfl_xor(key[n], S);
+    orow[n] = __shfl_xor(row[n], S);
+#endif
+  }
+}
+
+// b[n] = max over the wave of b[n], for N values at once (all lanes get it).
+template <int N>
+__device__ __forceinline__ void wave_max_all_n(float (&b)[N]) {
+#if ARMI_SORT_DPP
+#define ARMI_MAX_STEP(S)                                                                    \
+  _Pragma("unroll") for (int n = 0; n < N; ++n)                                            \
+      b[n] = fmaxf(b[n], __uint_as_float(xor_lane<S>(__float_as_uint(b[n]))));
+  ARMI_MAX_STEP(32) ARMI_MAX_STEP(16) ARMI_MAX_STEP(8) ARMI_MAX_STEP(4) ARMI_MAX_STEP(2)
+  ARMI_MAX_STEP(1)
+#undef ARMI_MAX_STEP
+#else
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int n = 0; n < N; ++n) b[n] = fmaxf(b[n], __shfl_xor(b[n], off));
+#endif
+}
+
 // N independent wave sorts at once: every stage issues all N lists' shuffles before using any,
 // so the N dependent shuffle chains overlap instead of running back to back.
 template <int N>
@@ -179,10 +240,13 @@ __device__ __forceinline__ void wave_sort_approx_desc_n(float (&key)[N], int32_t
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       float ok[N];
       int32_t orow[N];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        ok[n] = __shfl_xor(key[n], stride);
-        orow[n] = __shfl_xor(row[n], stride);
+      switch (stride) {  // (unrolled: one case per stage)
+        case 1: xor_exchange_n<1>(key, row, ok, orow); break;
+        case 2: xor_exchange_n<2>(key, row, ok, orow); break;
+        case 4: xor_exchange_n<4>(key, row, ok, orow); break;
+        case 8: xor_exchange_n<8>(key, row, ok, orow); break;
+        case 16: xor_exchange_n<16>(key, row, ok, orow); break;
+        default: xor_exchange_n<32>(key, row, ok, orow); break;
       }
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;

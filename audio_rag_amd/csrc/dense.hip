@@ -302,10 +302,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq)
     if (lane == kKW) b[qq] = fmaxf(b[qq], key[qq]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-    for (int qq = 0; qq < QW; ++qq) b[qq] = fmaxf(b[qq], __shfl_xor(b[qq], off));
+  armi::wave_max_all_n<QW>(b);
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
@@ -334,7 +331,16 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& 
   hi = __builtin_bit_cast(uint32_t, h - bias);
 }
 
-__device__ __forceinline__ u32x4 i8_load(const u32x4* p) { return *p; }
+#ifndef ARMI_I8_NT
+#define ARMI_I8_NT 0
+#endif
+__device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
+#if ARMI_I8_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 
 // Int8-filter form of dense_scan_kernel: the default 64-query scan (round 2). Each row's first
 // pass reads its 1-byte int8 image (rows8, one 1 KB row at dim 1024) instead of its 2-byte fp16
@@ -373,7 +379,7 @@ template <int DIM, bool COLLECT>
 __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
-    int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
+    int tiles_odd, int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr, int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list,
@@ -395,8 +401,8 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
   u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
   float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
   float* qscale = qnorm + kQB;  // (unused slot, keeps the layout of scan_i8_lds_bytes)
-  float* qerr = qscale + kQB;   // [8][kQB] norm partials
-  int32_t* qsel = reinterpret_cast<int32_t*>(qerr + kQB * (kThreads / kQB));  // [kQB] COLLECT
+  // (qscale + kQB: [8][kQB] unused slots, keep the layout of scan_i8_lds_bytes)
+  int32_t* qsel = reinterpret_cast<int32_t*>(qscale + kQB + kQB * (kThreads / kQB));  // [kQB] COLLECT
   float* qthr = reinterpret_cast<float*>(qsel + kQB);                        // [kQB] COLLECT
   int32_t* wcnt = reinterpret_cast<int32_t*>(qthr + kQB);                    // [kWaves]
 
@@ -450,12 +456,14 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
     return queries + (size_t)q * DIM;
   };
-  // Tile schedule: workgroup rp owns tiles [rp * tiles_per_wg, ...); wave w starts on tile
-  // t_begin + w, then takes the next tile of the range from the workgroup's LDS counter (first
-  // pass) or every kWaves-th (collect pass). A dynamic cross-workgroup dequeue (round 3) was
-  // slower (profiles/r03d_*, r03e_*) and was removed in round 4.
-  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
-  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
+  // Tile schedule: workgroup rp owns tiles_per_wg tiles (even rp) or tiles_odd (odd rp: the odd
+  // XCDs, plan_scan's skew) of consecutive ranges; wave w starts on tile t_begin + w, then takes
+  // the next tile of the range from the workgroup's LDS counter (first pass) or every kWaves-th
+  // (collect pass). A dynamic cross-workgroup dequeue (round 3: profiles/r03d_*, r03e_*; round 4
+  // tail form: profiles/r04ah_dense_tail_ab.txt) was slower.
+  const int64_t t_begin =
+      (int64_t)(rp >> 1) * (tiles_per_wg + tiles_odd) + ((rp & 1) ? tiles_per_wg : 0);
+  const int64_t t_end = min(t_begin + (int64_t)((rp & 1) ? tiles_odd : tiles_per_wg), n_tiles);
   int64_t t = t_begin + wave < t_end ? t_begin + wave : -1;
   // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
   // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
@@ -478,41 +486,38 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
   // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13), and the
   //    fp16 fragment image (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7, the
-  //    corpus chunks' order). Thread (q = tid % 64, sh0 = tid / 64) copies entries sh = sh0 + 8 i
-  //    of query q, all 2*KSTEPS/8 loads in flight at once (a dependent load per entry would cost
-  //    one L2 round trip each), and sums its components' squares on the way.
+  //    corpus chunks' order; 16-B chunk j = 16(s>>3) + 8h + (s&7) of the query row). Wave w
+  //    copies queries 8w .. 8w + 7: lane l takes query 8w + (l&7), chunk 8i + (l>>3) at step i,
+  //    so one load instruction reads 8 whole 128-B lines (8 chunks of each of 8 rows) and the
+  //    8-lane store groups write 8 adjacent 16-B slots (no bank conflict). Round 4 (r04ag stamps:
+  //    10.8 us of every launch) had lane = query, 64 lines per load instruction, each line
+  //    re-fetched by 8 instructions through a thrashed L1. All loads are in flight at once.
   {
-    constexpr int PER = KSTEPS * 2 / (kThreads / kQB);  // entries per thread (16 at dim 1024)
-    const int q = threadIdx.x & (kQB - 1);
-    const int sh0 = threadIdx.x >> 6;
+    constexpr int PER = DIM / 64;  // load instructions per wave
+    const int q = 8 * wave + (lane & 7);
+    const int jl = lane >> 3;
     u32x4 v[PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int sh = sh0 + (kThreads / kQB) * i;
-      const int s = sh >> 1, hh = sh & 1;
-      const int off = 128 * (s >> 3) + 64 * hh + 8 * (s & 7);
-      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(qrow(q) + off) : u32x4{0u, 0u, 0u, 0u};
-    }
+    for (int i = 0; i < PER; ++i)
+      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(qrow(q) + 8 * (8 * i + jl))
+                    : u32x4{0u, 0u, 0u, 0u};
     __builtin_amdgcn_sched_barrier(0);
     prefetch_first();
     __builtin_amdgcn_sched_barrier(0);
     float ss = 0.0f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int sh = sh0 + (kThreads / kQB) * i;
+      const int j = 8 * i + jl;
+      const int sh = 2 * (8 * (j >> 4) + (j & 7)) + ((j >> 3) & 1);
       qimg[sh * kQB + q] = v[i];
       const half8 hv = __builtin_bit_cast(half8, v[i]);
 #pragma unroll
       for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
     }
-    qerr[sh0 * kQB + q] = ss;  // partial sums, [8][kQB]
-    __syncthreads();
-    if (threadIdx.x < kQB) {
-      float tq = 0.0f;
-#pragma unroll
-      for (int j = 0; j < kThreads / kQB; ++j) tq += qerr[j * kQB + threadIdx.x];
-      qnorm[threadIdx.x] = sqrtf(tq) * (1.0f + 1.0f / 4096.0f);
-    }
+    ss += __shfl_xor(ss, 8);
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    if (lane < 8) qnorm[q] = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
   }
   __syncthreads();
   I8_STAMP(1);
@@ -733,10 +738,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq)
     if (lane == kKW) b[qq] = fmaxf(b[qq], key[qq]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-    for (int qq = 0; qq < QW; ++qq) b[qq] = fmaxf(b[qq], __shfl_xor(b[qq], off));
+  armi::wave_max_all_n<QW>(b);
 #pragma unroll
   for (int qq = 0; qq < QW; ++qq) {
     const int q = wave * QW + qq;
@@ -2264,11 +2266,17 @@ __global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
 
 size_t merge_lds_bytes(int pool2) { return (size_t)pool2 * 24 + 16; }
 
+#ifndef ARMI_I8_ODD_SKEW
+#define ARMI_I8_ODD_SKEW 0
+#endif
+bool use_i8_filter(const armi_index* idx, int k);
+
 struct ScanPlan {
   int n_qb = 1;   // 64-query blocks of the call
   int grid = 0;   // workgroups launched
   int n_wg = 0;   // tile ranges (candidate lists per query)
   int tiles_per_wg = 0;
+  int tiles_odd = 0;  // tiles of an odd workgroup (= tiles_per_wg without the skew)
   int pool2 = 0;
   int kc = 0;
 };
@@ -2283,6 +2291,23 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
   const int64_t wgs = std::min<int64_t>(want, tiles);
   p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
   p.n_wg = (int)((tiles + p.tiles_per_wg - 1) / p.tiles_per_wg);
+  p.tiles_odd = p.tiles_per_wg;
+  // int8 passes: odd workgroups (blockIdx % 8 odd: the odd XCDs) take ARMI_I8_ODD_SKEW per mille
+  // fewer tiles. Phase stamps on two boxes (profiles/r04ag_i8_stamps_*, r04ah_dense_tail_ab.txt):
+  // the odd XCDs' waves stream ~7 % slower, so with an even split their workgroups end ~10 us
+  // after the even ones at 1M rows.
+  if (ARMI_I8_ODD_SKEW > 0 && use_i8_filter(idx, k) && wgs % 16 == 0 && tiles >= 16 * wgs) {
+    const double f = 1.0 - ARMI_I8_ODD_SKEW / 1000.0;
+    const int le = (int)std::ceil((double)tiles / ((double)(wgs / 2) * (1.0 + f)));
+    const int lo = std::max(kWaves, (int)((double)le * f));
+    const int64_t pair = le + lo, full = tiles / pair, rem = tiles % pair;
+    const int n = (int)(2 * full + (rem == 0 ? 0 : (rem > le ? 2 : 1)));
+    if (n <= wgs) {
+      p.tiles_per_wg = le;
+      p.tiles_odd = lo;
+      p.n_wg = n;
+    }
+  }
   p.grid = p.n_qb == 1 ? p.n_wg : p.n_qb * 8 * ((p.n_wg + 7) / 8);
   p.pool2 = armi::pow2_at_least(p.n_wg * kKW);
   p.kc = std::max(4, std::min(armi::pow2_at_least(k + 8), 256));
@@ -2543,8 +2568,8 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, idx->tile_ord,
-        nullptr, nullptr, nullptr, nullptr, 0);
+        sp.tiles_odd, sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -2589,8 +2614,8 @@ int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, in
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
-        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord, out_flags, w.thr,
-        w.col_cnt, w.col_list, kCollectCap);
+        cp.tiles_odd, cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord,
+        out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;

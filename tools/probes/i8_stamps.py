@@ -63,7 +63,18 @@ def main() -> None:
         wl = live.all(axis=1)
         wg_spread = (st[wl][:, :, 2].max(axis=1) - st[wl][:, :, 2].min(axis=1)) / 100.0
         wg_merge = (st[wl][:, :, 3].max(axis=1) - st[wl][:, :, 2].max(axis=1)) / 100.0
-        spans.append(dict(wg_wave_end_spread_mean=float(wg_spread.mean()),
+        wg_end = np.where(live.any(axis=1), np.where(live, rel[..., 2], -1e9).max(axis=1), np.nan)
+        wg_loop = np.where(live.any(axis=1), np.where(live, rel[..., 2] - rel[..., 1], np.nan).mean(axis=1), np.nan)
+        per_xcd = {}
+        for x in range(8):
+            ex, lx = wg_end[x::8], wg_loop[x::8]
+            ex, lx = ex[~np.isnan(ex)], lx[~np.isnan(lx)]
+            if len(ex) > 2:
+                ex, lx = np.sort(ex)[1:], lx  # drop the short remainder workgroup
+                per_xcd[f"xcd{x}_end_mean"] = float(ex.mean())
+                per_xcd[f"xcd{x}_end_max"] = float(ex.max())
+                per_xcd[f"xcd{x}_wave_loop_mean"] = float(np.median(lx))
+        spans.append(dict(**per_xcd, wg_wave_end_spread_mean=float(wg_spread.mean()),
                           wg_wave_end_spread_max=float(wg_spread.max()),
                           wg_pure_merge_mean=float(wg_merge.mean()),
                           wg_pure_merge_max=float(wg_merge.max()),
