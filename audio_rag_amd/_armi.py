@@ -39,6 +39,7 @@ SIGNATURES: dict[str, tuple] = {
     "armi_source_digest": (ctypes.c_char_p, []),
     "armi_index_create": (c_int, [c_int, c_void_p, c_int64, c_int, c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_dense_scan_form": (c_int, [c_void_p, c_int, c_int]),
+    "armi_dense_scan_nontemporal": (c_int, [c_void_p, c_int, c_int]),
     "armi_index_destroy": (c_int, [c_void_p]),
     "armi_index_rows": (c_int64, [c_void_p]),
     "armi_index_dim": (c_int, [c_void_p]),

@@ -331,15 +331,11 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t d, uint32_t& lo, uint32_t& 
   hi = __builtin_bit_cast(uint32_t, h - bias);
 }
 
-#ifndef ARMI_I8_NT
-#define ARMI_I8_NT 0
-#endif
+// NT: nontemporal loads (images larger than the Infinity Cache, use_nt_stream)
+template <bool NT>
 __device__ __forceinline__ u32x4 i8_load(const u32x4* p) {
-#if ARMI_I8_NT
-  return __builtin_nontemporal_load(p);
-#else
+  if constexpr (NT) return __builtin_nontemporal_load(p);
   return *p;
-#endif
 }
 
 // Int8-filter form of dense_scan_kernel: the default 64-query scan (round 2). Each row's first
@@ -375,11 +371,11 @@ __device__ uint64_t g_i8_stamps[256 * kWaves * 4];
 // reaches it is appended to the query's list: a row of the true top-k has exact >= k-th found,
 // hence key >= thr, so the list holds the whole top-k whatever the corpus looks like (runs of
 // near-duplicates, one-ulp neighbours, exact duplicates). dense_collect_merge_kernel rescores it.
-template <int DIM, bool COLLECT>
+template <int DIM, bool COLLECT, bool NT>
 __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
     const uint64_t* __restrict__ row_mask, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
-    int tiles_odd, int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
+    int n_ranges, int n_qb, const uint16_t* __restrict__ queries_all, int q_stride,
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr, int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list,
@@ -456,14 +452,14 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     if constexpr (COLLECT) return queries_all + (size_t)qsel[q] * DIM;
     return queries + (size_t)q * DIM;
   };
-  // Tile schedule: workgroup rp owns tiles_per_wg tiles (even rp) or tiles_odd (odd rp: the odd
-  // XCDs, plan_scan's skew) of consecutive ranges; wave w starts on tile t_begin + w, then takes
-  // the next tile of the range from the workgroup's LDS counter (first pass) or every kWaves-th
-  // (collect pass). A dynamic cross-workgroup dequeue (round 3: profiles/r03d_*, r03e_*; round 4
-  // tail form: profiles/r04ah_dense_tail_ab.txt) was slower.
-  const int64_t t_begin =
-      (int64_t)(rp >> 1) * (tiles_per_wg + tiles_odd) + ((rp & 1) ? tiles_per_wg : 0);
-  const int64_t t_end = min(t_begin + (int64_t)((rp & 1) ? tiles_odd : tiles_per_wg), n_tiles);
+  // Tile schedule: workgroup rp owns tiles [rp * tiles_per_wg, ...); wave w starts on tile
+  // t_begin + w, then takes the next tile of the range from the workgroup's LDS counter (first
+  // pass) or every kWaves-th (collect pass). Measured and not adopted: a dynamic cross-workgroup
+  // dequeue (round 3: profiles/r03d_*, r03e_*; round 4 tail form: r04ah_dense_tail_ab.txt) and
+  // fewer tiles for the odd XCDs, whose waves stream ~5 % slower (r04aj / r04ak: +1.3 % without
+  // the nontemporal stream, none with it).
+  const int64_t t_begin = (int64_t)rp * tiles_per_wg;
+  const int64_t t_end = min(t_begin + (int64_t)tiles_per_wg, n_tiles);
   int64_t t = t_begin + wave < t_end ? t_begin + wave : -1;
   // tile-blocked int8 image (armi_index.h): chunk c of the tile's row r at c * 512 + r * 16, so
   // chunk c of the lane's row is cur[32 c]; the padded tail tile is allocated (zero rows, NaN a32)
@@ -480,7 +476,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
       for (int g = 0; g < DEPTH; ++g)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) buf[g][i] = i8_load(cur + 32 * (8 * g + i));
+        for (int i = 0; i < 4; ++i) buf[g][i] = i8_load<NT>(cur + 32 * (8 * g + i));
     }
   };
 
@@ -595,11 +591,11 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
         if (g + DEPTH < GROUPS) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            buf[g % DEPTH][i] = i8_load(cur + 32 * (8 * (g + DEPTH) + i));
+            buf[g % DEPTH][i] = i8_load<NT>(cur + 32 * (8 * (g + DEPTH) + i));
         } else {  // (no next tile: tile 0, so every path issues the same loads)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            buf[g % DEPTH][i] = i8_load(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
+            buf[g % DEPTH][i] = i8_load<NT>(nxt + 32 * (8 * (g + DEPTH - GROUPS) + i));
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -2266,17 +2262,11 @@ __global__ __launch_bounds__(kMergeThreads) void merge_lists_kernel(
 
 size_t merge_lds_bytes(int pool2) { return (size_t)pool2 * 24 + 16; }
 
-#ifndef ARMI_I8_ODD_SKEW
-#define ARMI_I8_ODD_SKEW 0
-#endif
-bool use_i8_filter(const armi_index* idx, int k);
-
 struct ScanPlan {
   int n_qb = 1;   // 64-query blocks of the call
   int grid = 0;   // workgroups launched
   int n_wg = 0;   // tile ranges (candidate lists per query)
   int tiles_per_wg = 0;
-  int tiles_odd = 0;  // tiles of an odd workgroup (= tiles_per_wg without the skew)
   int pool2 = 0;
   int kc = 0;
 };
@@ -2291,23 +2281,6 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
   const int64_t wgs = std::min<int64_t>(want, tiles);
   p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
   p.n_wg = (int)((tiles + p.tiles_per_wg - 1) / p.tiles_per_wg);
-  p.tiles_odd = p.tiles_per_wg;
-  // int8 passes: odd workgroups (blockIdx % 8 odd: the odd XCDs) take ARMI_I8_ODD_SKEW per mille
-  // fewer tiles. Phase stamps on two boxes (profiles/r04ag_i8_stamps_*, r04ah_dense_tail_ab.txt):
-  // the odd XCDs' waves stream ~7 % slower, so with an even split their workgroups end ~10 us
-  // after the even ones at 1M rows.
-  if (ARMI_I8_ODD_SKEW > 0 && use_i8_filter(idx, k) && wgs % 16 == 0 && tiles >= 16 * wgs) {
-    const double f = 1.0 - ARMI_I8_ODD_SKEW / 1000.0;
-    const int le = (int)std::ceil((double)tiles / ((double)(wgs / 2) * (1.0 + f)));
-    const int lo = std::max(kWaves, (int)((double)le * f));
-    const int64_t pair = le + lo, full = tiles / pair, rem = tiles % pair;
-    const int n = (int)(2 * full + (rem == 0 ? 0 : (rem > le ? 2 : 1)));
-    if (n <= wgs) {
-      p.tiles_per_wg = le;
-      p.tiles_odd = lo;
-      p.n_wg = n;
-    }
-  }
   p.grid = p.n_qb == 1 ? p.n_wg : p.n_qb * 8 * ((p.n_wg + 7) / 8);
   p.pool2 = armi::pow2_at_least(p.n_wg * kKW);
   p.kc = std::max(4, std::min(armi::pow2_at_least(k + 8), 256));
@@ -2327,6 +2300,16 @@ bool use_gemm_scan(int nq) { return nq > 2 * kQB; }
 // dense prefetch limit 2 * 20, src/audio_rag/retrieval/qdrant.py:281-293).
 constexpr int kI8MaxK = 64;
 bool use_i8_filter(const armi_index* idx, int k) { return idx->rows8 != nullptr && k <= kI8MaxK; }
+// The int8 passes stream the image with nontemporal loads when it exceeds ARMI_I8_NT_MIN_MB: an
+// image that the Infinity Cache (256 MB) cannot hold is re-read from HBM every call anyway, and
+// the nontemporal form ran 4 % faster at 1M rows (1 GB image); at 100k rows (100 MB, cache
+// resident across calls) it ran 2-5 % slower (profiles/r04aj_dense_nt_skew_ab.txt).
+#ifndef ARMI_I8_NT_MIN_MB
+#define ARMI_I8_NT_MIN_MB 192
+#endif
+bool use_nt_stream(const armi_index* idx) {
+  return (double)idx->n_tiles * TILE_ROWS * idx->dim > ARMI_I8_NT_MIN_MB * 1048576.0;
+}
 // Rows rescored per query after the int8 pass: the rows whose key (an upper bound) reaches the
 // k-th exact cosine are about 15-35 for k = 5 at 1M random unit rows (bound slack ~0.008). k <= 10
 // rescores 64 (hybrid's dense prefetch of 10: 6 400 of 6 400 queries certified at 1M rows, step
@@ -2562,13 +2545,14 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     if (int rc = tl.end()) return rc;
   } else if (use_i8_filter(idx, k)) {
     kc = kc_i8(k);
-    auto kern = dense_scan_i8_kernel<DIM, false>;
+    auto kern = use_nt_stream(idx) ? dense_scan_i8_kernel<DIM, false, true>
+                                   : dense_scan_i8_kernel<DIM, false, false>;
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.tiles_odd, sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
+        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
         idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
@@ -2610,11 +2594,12 @@ int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, in
     const ScanPlan cp = plan_scan(idx, k, 1);  // one block's ranges; blocks of one range share an XCD
     const int n_qb = (nq + kQB - 1) / kQB;
     const int grid = n_qb == 1 ? cp.n_wg : n_qb * 8 * ((cp.n_wg + 7) / 8);
-    auto kern = dense_scan_i8_kernel<DIM, true>;
+    auto kern = use_nt_stream(idx) ? dense_scan_i8_kernel<DIM, true, true>
+                                   : dense_scan_i8_kernel<DIM, true, false>;
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
-        cp.tiles_odd, cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord,
+        cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord,
         out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
@@ -2652,6 +2637,12 @@ int armi_dense_scan_form(const armi_index* idx, int n_queries, int k) {
   if (use_gemm_scan(n_queries))
     return use_tiled_i8(idx, k) ? ARMI_SCAN_TILED_INT8 : ARMI_SCAN_TILED_FP16;
   return use_i8_filter(idx, k) ? ARMI_SCAN_INT8_FILTER : ARMI_SCAN_FP16;
+}
+
+int armi_dense_scan_nontemporal(const armi_index* idx, int n_queries, int k) {
+  const int form = armi_dense_scan_form(idx, n_queries, k);
+  if (form < 0) return -1;
+  return form == ARMI_SCAN_INT8_FILTER && use_nt_stream(idx) ? 1 : 0;
 }
 
 size_t armi_dense_workspace_bytes(const armi_index* idx, int n_queries, int k) {

@@ -49,7 +49,7 @@ constexpr int kCollectCap = 4096;       // rows per query collected by the fallb
 constexpr int kMaxTerms = 256;          // query terms per query (BGE-M3 queries are short)
 constexpr int kLongTerm = 256;          // postings from which a term gets a range-start table
 constexpr int kPad = 128;               // sentinel slots past the last list (two 64-posting loads)
-constexpr int kBatch = 4;               // terms whose LDS reads are in flight together
+constexpr int kBatch = 4;  // terms whose LDS reads are in flight together (8: no gain, r04ak)
 constexpr int kTile = 128;              // rows per scan step: two adjacent rows per lane
 constexpr int kQStride = kMaxTerms + 2 * kBatch;  // list entries per query slot (+ padding)
 constexpr int kMaxRanges = 256;
@@ -789,10 +789,11 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
       for (int k = 0; k < kBatch; ++k)
         a = a + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
-      x = or3(x, rv[0].x, rv[1].x);
-      x = or3(x, rv[2].x, rv[3].x);
-      y = or3(y, rv[0].y, rv[1].y);
-      y = or3(y, rv[2].y, rv[3].y);
+#pragma unroll
+      for (int k = 0; k < kBatch; k += 2) {
+        x = or3(x, rv[k].x, rv[k + 1].x);
+        y = or3(y, rv[k].y, rv[k + 1].y);
+      }
     };
     // The next batch's entries (one scalar load) are requested right after this batch's LDS
     // reads, so the two latencies overlap: the loop waits once per batch for both (scalar loads
@@ -821,10 +822,11 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
           a = a + f2{cur[k].w, cur[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
-        hx[i] = or3(hx[i], rv[0].x, rv[1].x);
-        hx[i] = or3(hx[i], rv[2].x, rv[3].x);
-        hy[i] = or3(hy[i], rv[0].y, rv[1].y);
-        hy[i] = or3(hy[i], rv[2].y, rv[3].y);
+#pragma unroll
+        for (int k = 0; k < kBatch; k += 2) {
+          hx[i] = or3(hx[i], rv[k].x, rv[k + 1].x);
+          hy[i] = or3(hy[i], rv[k].y, rv[k + 1].y);
+        }
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) cur[k] = nxt[k];
       }

@@ -127,6 +127,10 @@ class DenseIndex:
         """Which scan armi_dense_topk runs for this call shape (_armi.SCAN_*)."""
         return int(query("armi_dense_scan_form", self._handle, n_queries, k))
 
+    def scan_nontemporal(self, n_queries: int, k: int) -> bool:
+        """Whether the int8 first pass of this call shape streams with nontemporal loads."""
+        return int(query("armi_dense_scan_nontemporal", self._handle, n_queries, k)) == 1
+
     def workspace_bytes(self, n_queries: int, k: int, exact: bool = False) -> int:
         fn = "armi_dense_exact_workspace_bytes" if exact else "armi_dense_workspace_bytes"
         return int(query(fn, self._handle, n_queries, k))

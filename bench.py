@@ -485,7 +485,8 @@ def main() -> None:
     if form == _armi.SCAN_INT8_FILTER:
         # int8 filter image (1 B / component) + a32, e32 (8 B / row) + the fp16 queries
         alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim * 2
-        scan_kernel = f"dense_scan_i8_kernel<{dim}, false>"
+        nt = "true" if index.scan_nontemporal(nq_scan, pre_k) else "false"
+        scan_kernel = f"dense_scan_i8_kernel<{dim}, false, {nt}>"
     elif form == _armi.SCAN_TILED_INT8:
         # int8 image + a32, e32 per row; the call's int8 queries (1 B / component)
         alg_bytes = shard_rows * dim + shard_rows * 8 + nq_scan * dim

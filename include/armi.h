@@ -108,6 +108,11 @@ int armi_index_norms(const armi_index* index, const int64_t** norm2, const doubl
 #define ARMI_SCAN_TILED_INT8 3
 int armi_dense_scan_form(const armi_index* index, int n_queries, int k);
 
+/* 1 when the call's ARMI_SCAN_INT8_FILTER passes stream the int8 image with nontemporal loads
+ * (images larger than the Infinity Cache), else 0; -1 for invalid arguments. Introspection for
+ * profiling (the kernel instance that runs); results do not depend on it. */
+int armi_dense_scan_nontemporal(const armi_index* index, int n_queries, int k);
+
 /* Workspace bytes needed by armi_dense_topk for n_queries queries and top-k. */
 size_t armi_dense_workspace_bytes(const armi_index* index, int n_queries, int k);
 

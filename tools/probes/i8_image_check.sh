@@ -25,3 +25,13 @@ for s in ${STAMPS:-stamps}; do
     tail -1 gpurun_out/${TAG}_${s}_$n.log | python -c "import json,sys;d=json.loads(sys.stdin.read());m=d['median_us'];print(sys.argv[1],{k:round(v,1) for k,v in m.items() if not k.startswith('xcd')})" $s
   done
 done
+# hybrid (configs[2] retrieval) lines: default vs HYB_VARIANTS
+if [ -n "$HYB_VARIANTS" ]; then
+  for rep in 1 2; do
+    for v in default $HYB_VARIANTS; do
+      L=""; [ $v != default ] && L=$PWD/ablibs/$v/libarmi.so
+      ARMI_LIB_PATH=$L timeout -k 10 180 python bench.py --workload hybrid --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/${TAG}_hyb_${v}_$rep.json 2> gpurun_out/${TAG}_hyb_${v}_$rep.err || exit 1
+      python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline_sparse') or {};print('hybrid',sys.argv[2],round(d['value']),round(d['ms_per_step'],4),round(r.get('avg_launch_ms',0),4))" gpurun_out/${TAG}_hyb_${v}_$rep.json $v
+    done
+  done
+fi
