@@ -224,16 +224,17 @@ def traffic_key(form: int, n_rows: int, dim: int, n_queries: int, corpus: str) -
     return f"dense_{name}_{corpus}_n{n_rows}_d{dim}_q{n_queries}"
 
 
-def read_traffic(key: str) -> tuple[float | None, str | None]:
+def read_traffic(key: str, kernel: str) -> tuple[float | None, str | None]:
     """HBM bytes per launch of the scan measured by rocprofv3 PMC passes (FETCH_SIZE and
-    WRITE_SIZE in separate runs, gfx950-corrected) for exactly this shape, or (None, None) when no
-    such measurement is committed: a traffic figure of another shape says nothing here."""
+    WRITE_SIZE in separate runs, gfx950-corrected) for exactly this shape and kernel instance, or
+    (None, None) when no such measurement is committed: a traffic figure of another shape or
+    kernel says nothing here."""
     p = TRAFFIC_DIR / f"{key}.json"
     if not p.exists():
         return None, None
     try:
         d = json.loads(p.read_text())
-        if d.get("key") != key:
+        if d.get("key") != key or d.get("kernel") != kernel:
             return None, None
         return float(d["hbm_bytes_per_launch"]), str(p.relative_to(ROOT))
     except Exception:
@@ -502,8 +503,8 @@ def main() -> None:
     mfma_dtype = "i8" if form == _armi.SCAN_TILED_INT8 else "fp16"
     mfma_bound = alg_flops / (MFMA_PEAK_TFLOPS[mfma_dtype] * 1e12) > alg_bytes / (HBM_PEAK_GBS * 1e9)
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = (read_traffic(traffic_key(form, shard_rows, dim, nq_scan, args.corpus))
-                            if world == 1 else (None, None))
+    traffic, traffic_src = (read_traffic(traffic_key(form, shard_rows, dim, nq_scan, args.corpus),
+                                         scan_kernel) if world == 1 else (None, None))
     result = {
         "metric": METRIC,
         "value": total_queries / elapsed,
@@ -609,7 +610,8 @@ def main() -> None:
         alg = sum(pass_bytes[i % n_q_batches] for i in range(args.steps)) / max(args.steps, 1)
         if sp_n.value:
             sp_avg = sp_ms.value / sp_n.value
-            sp_traffic, sp_src = read_traffic(f"sparse_scan_{args.corpus}_n{n}_q{batch}")
+            sp_traffic, sp_src = read_traffic(f"sparse_scan_{args.corpus}_n{n}_q{batch}",
+                                              "sparse_scan_kernel<false>")
             result["roofline_sparse"] = {
                 "bound": "hbm", "kernel": "sparse_scan_kernel<false>", "achieved": alg / (sp_avg * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
