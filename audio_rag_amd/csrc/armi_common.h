@@ -83,6 +83,62 @@ __device__ __forceinline__ bool approx_better(float ka, int32_t ia, float kb, in
   return (ka > kb) | ((ka == kb) & (ia < ib));
 }
 
+// Lane l reads lane l ^ S, without the LDS pipe (ds_bpermute): S = 1, 2 one DPP quad
+// permutation, 4 a half-row mirror then a quad reversal ((l ^ 7) ^ 3), 8 a row rotation by 8,
+// 16 / 32 one v_permlane16/32_swap of the value with itself (the swapped row of the other half)
+// and a select.
+#ifndef ARMI_SORT_DPP
+#define ARMI_SORT_DPP 1  // 0: ds_bpermute (__shfl_xor) as before round 4 (r04ai: 100k step -2 %)
+#endif
+template <int S>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  static_assert(S == 1 || S == 2 || S == 4 || S == 8 || S == 16 || S == 32, "lane xor");
+  if constexpr (S == 1) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (S == 2) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (S == 4) {
+    const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x1B, 0xF, 0xF, false);
+  } else if constexpr (S == 8) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (S == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? (uint32_t)p[0] : (uint32_t)p[1];
+  } else {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? (uint32_t)p[0] : (uint32_t)p[1];
+  }
+}
+
+// v of lane l ^ stride for any 4- or 8-byte type (stride: a compile-time constant after the
+// sorts' full unrolling, so the switch folds)
+template <typename T>
+__device__ __forceinline__ T xor_stride(T v, int stride) {
+#if ARMI_SORT_DPP
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte lane values");
+  auto one = [&](uint32_t u) -> uint32_t {
+    switch (stride) {
+      case 1: return xor_lane<1>(u);
+      case 2: return xor_lane<2>(u);
+      case 4: return xor_lane<4>(u);
+      case 8: return xor_lane<8>(u);
+      case 16: return xor_lane<16>(u);
+      default: return xor_lane<32>(u);
+    }
+  };
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, one(__builtin_bit_cast(uint32_t, v)));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t lo = one((uint32_t)u), hi = one((uint32_t)(u >> 32));
+    return __builtin_bit_cast(T, lo | (hi << 32));
+  }
+#else
+  return __shfl_xor(v, stride);
+#endif
+}
+
 // In-LDS bitonic sort of n (power of two) entries into descending rank order, executed by the
 // whole workgroup. Entries: (double key, int64 ordinal).
 __device__ inline void lds_sort_rank_desc(double* key, int64_t* ord, int n) {
@@ -135,8 +191,8 @@ __device__ __forceinline__ void wave_sort_approx_desc(float& key, int32_t& row) 
   for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const float ok = __shfl_xor(key, stride);
-      const int32_t orow = __shfl_xor(row, stride);
+      const float ok = xor_stride(key, stride);
+      const int32_t orow = xor_stride(row, stride);
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;
       const bool other_better = approx_better(ok, orow, key, row);
@@ -156,8 +212,8 @@ __device__ __forceinline__ void wave_sort_rank_desc(double& key, int64_t& ord) {
   for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const double ok = __shfl_xor(key, stride);
-      const int64_t oo = __shfl_xor(ord, stride);
+      const double ok = xor_stride(key, stride);
+      const int64_t oo = xor_stride(ord, stride);
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;
       const bool other_better = rank_better(ok, oo, key, ord);
@@ -165,34 +221,6 @@ __device__ __forceinline__ void wave_sort_rank_desc(double& key, int64_t& ord) {
       key = take_other ? ok : key;
       ord = take_other ? oo : ord;
     }
-  }
-}
-
-// Lane l reads lane l ^ S, without the LDS pipe (ds_bpermute): S = 1, 2 one DPP quad
-// permutation, 4 a half-row mirror then a quad reversal ((l ^ 7) ^ 3), 8 a row rotation by 8,
-// 16 / 32 one v_permlane16/32_swap of the value with itself (the swapped row of the other half)
-// and a select.
-#ifndef ARMI_SORT_DPP
-#define ARMI_SORT_DPP 1  // 0: ds_bpermute (__shfl_xor) as before round 4 (r04ai: 100k step -2 %)
-#endif
-template <int S>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
-  static_assert(S == 1 || S == 2 || S == 4 || S == 8 || S == 16 || S == 32, "lane xor");
-  if constexpr (S == 1) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-  } else if constexpr (S == 2) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
-  } else if constexpr (S == 4) {
-    const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x1B, 0xF, 0xF, false);
-  } else if constexpr (S == 8) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
-  } else if constexpr (S == 16) {
-    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (threadIdx.x & 16) ? (uint32_t)p[0] : (uint32_t)p[1];
-  } else {
-    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (threadIdx.x & 32) ? (uint32_t)p[0] : (uint32_t)p[1];
   }
 }
 

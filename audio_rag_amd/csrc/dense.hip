@@ -510,9 +510,9 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 #pragma unroll
       for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
     }
-    ss += __shfl_xor(ss, 8);
-    ss += __shfl_xor(ss, 16);
-    ss += __shfl_xor(ss, 32);
+    ss += armi::xor_stride(ss, 8);
+    ss += armi::xor_stride(ss, 16);
+    ss += armi::xor_stride(ss, 32);
     if (lane < 8) qnorm[q] = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
   }
   __syncthreads();
@@ -1177,8 +1177,8 @@ void dense_gemm_scan_w4_kernel(
     for (int size = 2; size <= 16; size <<= 1) {
 #pragma unroll
       for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const float ok = __shfl_xor(key, stride);
-        const int32_t orow = __shfl_xor(row, stride);
+        const float ok = armi::xor_stride(key, stride);
+        const int32_t orow = armi::xor_stride(row, stride);
         const bool lower = (lane & stride) == 0;
         const bool desc = (lane & size) == 0;
         const bool other_better = armi::approx_better(ok, orow, key, row);
@@ -1240,8 +1240,8 @@ __global__ __launch_bounds__(256) void query_i8_kernel(const uint16_t* __restric
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    amax = fmaxf(amax, __shfl_xor(amax, off));
-    ss += __shfl_xor(ss, off);
+    amax = fmaxf(amax, armi::xor_stride(amax, off));
+    ss += armi::xor_stride(ss, off);
   }
   constexpr float kF[4] = {1.0f, 0.8f, 0.65f, 0.5f};
   float err[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1258,7 +1258,7 @@ __global__ __launch_bounds__(256) void query_i8_kernel(const uint16_t* __restric
         err[f] += res * res;
       }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) err[f] += __shfl_xor(err[f], off);
+    for (int off = 32; off > 0; off >>= 1) err[f] += armi::xor_stride(err[f], off);
   }
   int best = 0;
 #pragma unroll
@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(256) void query_i8_kernel(const uint16_t* __restric
       *reinterpret_cast<u32x2*>(q8 + (size_t)q * DIM + 8 * c) = u32x2{packed[0], packed[1]};
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) er += __shfl_xor(er, off);
+  for (int off = 32; off > 0; off >>= 1) er += armi::xor_stride(er, off);
   if (lane == 0) {
     const float qn = sqrtf(ss) * (1.0f + 1.0f / 4096.0f);
     const float eq = sqrtf(er) * (1.0f + 1.0f / 1024.0f) + qn * (1.0f / 1048576.0f);
@@ -1330,7 +1330,7 @@ __device__ __forceinline__ int64_t dot_fixed(const int32_t (&qf)[DIM / 64],
 #pragma unroll
   for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)xf[i];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  for (int off = 32; off > 0; off >>= 1) acc += armi::xor_stride(acc, off);
   return acc;
 }
 
@@ -1356,7 +1356,7 @@ __global__ __launch_bounds__(64) void query_norms_kernel(const uint16_t* __restr
 #pragma unroll
   for (int i = 0; i < DIM / 64; ++i) acc += (int64_t)qf[i] * (int64_t)qf[i];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  for (int off = 32; off > 0; off >>= 1) acc += armi::xor_stride(acc, off);
   if (lane == 0) {
     inv_q[q] = acc > 0 ? 1.0 / sqrt((double)acc) : 0.0;
     qnorm_real[q] = sqrt((double)acc) * (1.0 / 16777216.0);
@@ -1416,18 +1416,18 @@ __device__ __forceinline__ void exact_keys8(const int32_t (&qf)[DIM / 64],
   for (int m = 0; m < 4; ++m) {  // lanes with bit 5 keep rows 4..7, the others rows 0..3
     const int64_t mine = b5 ? v[4 + m] : v[m];
     const int64_t give = b5 ? v[m] : v[4 + m];
-    v[m] = mine + __shfl_xor(give, 32);
+    v[m] = mine + armi::xor_stride(give, 32);
   }
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int64_t mine = b4 ? v[2 + m] : v[m];
     const int64_t give = b4 ? v[m] : v[2 + m];
-    v[m] = mine + __shfl_xor(give, 16);
+    v[m] = mine + armi::xor_stride(give, 16);
   }
-  int64_t dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
-  dot += __shfl_xor(dot, 4);
-  dot += __shfl_xor(dot, 2);
-  dot += __shfl_xor(dot, 1);
+  int64_t dot = (b3 ? v[1] : v[0]) + armi::xor_stride(b3 ? v[0] : v[1], 8);
+  dot += armi::xor_stride(dot, 4);
+  dot += armi::xor_stride(dot, 2);
+  dot += armi::xor_stride(dot, 1);
   const int r = (lane >> 3) & 7;  // = 4 b5 + 2 b4 + b3
   row = -1;
   double myinv = 0.0;
@@ -1484,18 +1484,18 @@ __device__ __forceinline__ void approx_keys8(const float (&qh)[DIM / 64],
   for (int m = 0; m < 4; ++m) {
     const float mine = b5 ? v[4 + m] : v[m];
     const float give = b5 ? v[m] : v[4 + m];
-    v[m] = mine + __shfl_xor(give, 32);
+    v[m] = mine + armi::xor_stride(give, 32);
   }
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const float mine = b4 ? v[2 + m] : v[m];
     const float give = b4 ? v[m] : v[2 + m];
-    v[m] = mine + __shfl_xor(give, 16);
+    v[m] = mine + armi::xor_stride(give, 16);
   }
-  float dot = (b3 ? v[1] : v[0]) + __shfl_xor(b3 ? v[0] : v[1], 8);
-  dot += __shfl_xor(dot, 4);
-  dot += __shfl_xor(dot, 2);
-  dot += __shfl_xor(dot, 1);
+  float dot = (b3 ? v[1] : v[0]) + armi::xor_stride(b3 ? v[0] : v[1], 8);
+  dot += armi::xor_stride(dot, 4);
+  dot += armi::xor_stride(dot, 2);
+  dot += armi::xor_stride(dot, 1);
   const int r = (lane >> 3) & 7;
   row = -1;
   double myinv = 0.0;
@@ -1583,7 +1583,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
 #pragma unroll
   for (int i = 0; i < DIM / 64; ++i) n2q += (int64_t)qf[i] * (int64_t)qf[i];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n2q += __shfl_xor(n2q, off);
+  for (int off = 32; off > 0; off >>= 1) n2q += armi::xor_stride(n2q, off);
   const double inv_q = n2q > 0 ? 1.0 / sqrt((double)n2q) : 0.0;
   const double qnorm_real = sqrt((double)n2q) * (1.0 / 16777216.0);
   if (tid == 0) {
@@ -1604,7 +1604,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     if (sel_col > 0 && e < pool && e % kKW == sel_col - 1) umax[e / kKW] = ord_key(kk[j]);
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) bpart[wave] = b;
   __syncthreads(); MERGE_STAMP(1);
 
@@ -1681,7 +1681,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
     }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
+  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
   if (lane == 0) red[wave] = dmax;
   __syncthreads(); MERGE_STAMP(3);
   const int n_sel = ctr[0];
@@ -1723,15 +1723,15 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
         if (other) { key = okey; row = orow; }
 #pragma unroll
         for (int stride = 32; stride > 0; stride >>= 1) {
-          const float k2 = __shfl_xor(key, stride);
-          const int32_t r2 = __shfl_xor(row, stride);
+          const float k2 = armi::xor_stride(key, stride);
+          const int32_t r2 = armi::xor_stride(row, stride);
           const bool lower = (lane & stride) == 0;
           const bool better = armi::approx_better(k2, r2, key, row);
           if (lower == better) { key = k2; row = r2; }
         }
       }
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) lost = fmaxf(lost, __shfl_xor(lost, off));
+      for (int off = 32; off > 0; off >>= 1) lost = fmaxf(lost, armi::xor_stride(lost, off));
       skey[lane] = key;
       srow[lane] = row;
       if (lane == 0) red[10] = lost;
@@ -1810,7 +1810,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
         live += c < kc && skey[c] != kNegInf;
       }
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off);
+      for (int off = 32; off > 0; off >>= 1) live += armi::xor_stride(live, off);
       double cut = kNegInfD;
       if (live >= k) {
         uint32_t prefix = 0;
@@ -1894,7 +1894,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_merge_kernel(
   int n_valid = 0;
   for (int c = lane; c < n_s; c += 64) n_valid += rord[c] != kNoOrd;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
+  for (int off = 32; off > 0; off >>= 1) n_valid += armi::xor_stride(n_valid, off);
   bool certified;
   int n_out;
   const double delta =
@@ -2030,7 +2030,7 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
     int n_valid = 0;
     for (int c = lane; c < k; c += 64) n_valid += ord[c] != kNoOrd;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) n_valid += __shfl_xor(n_valid, off);
+    for (int off = 32; off > 0; off >>= 1) n_valid += armi::xor_stride(n_valid, off);
     const double iq = inv_q[qg];
     for (int c = lane; c < k; c += 64) {
       const size_t o = (size_t)qg * k + c;

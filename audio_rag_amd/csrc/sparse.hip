@@ -241,7 +241,7 @@ __device__ __forceinline__ void deal_queries(const int32_t* __restrict__ q_indpt
   for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int o = __shfl_xor(sk, stride);
+      const int o = armi::xor_stride(sk, stride);
       const bool lower = (lane & stride) == 0;
       const bool desc = (lane & size) == 0;
       if ((lower == desc) ? (o > sk) : (o < sk)) sk = o;
@@ -974,7 +974,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-        for (int i = 0; i < kQW; ++i) bq[i] = fmaxf(bq[i], __shfl_xor(bq[i], o));
+        for (int i = 0; i < kQW; ++i) bq[i] = fmaxf(bq[i], armi::xor_stride(bq[i], o));
       armi::wave_sort_approx_desc_n<kQW>(ck, cr);
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   }
   if (tid == 0) ctr[0] = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, __shfl_xor(b, off));
+  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) red[wave] = b;
   __syncthreads();
   if (wave == 0) {  // t0 = k-th largest list maximum (radix select over <= 256 keys)
@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
     }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
+  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
   if (lane == 0) red[4 + wave] = dmax;
   __syncthreads();
   const int n_sel = ctr[0];
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   int nv = 0;
   for (int c = lane; c < min(n2, k); c += 64) nv += skey[c] != kNegInf;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
+  for (int off = 32; off > 0; off >>= 1) nv += armi::xor_stride(nv, off);
   bool certified;
   if (nv >= k)
     certified = skey[k - 1] > bound;

@@ -122,3 +122,33 @@ def test_certified_at_100k(gpu, oracle_mod, k):
     got = _run(idx, qs, k, gpu)
     assert (got["flags"] == 1).all(), got["flags"]
     _assert_same(got, oracle_mod.dense_topk(rows, qs, k))
+
+
+def test_nontemporal_stream_first_and_collect_pass(gpu, oracle_mod):
+    """A shard whose int8 image (> 192 MB) streams with nontemporal loads: the first pass and the
+    collect pass (forced: 60 near-duplicates of query 0 overflow its workgroup list, so it is not
+    certified) run the <dim, *, true> kernel instances; every query equals the exhaustive exact
+    scan, a sample the oracle."""
+    n, dim = 262_144 + 96, 1024
+    rows = oracle_mod.unit_fp16(n, dim, seed=901)
+    v = rows[5].copy()
+    for i in range(60):  # one-ulp variants of v in consecutive rows (one workgroup's range)
+        w = v.copy()
+        w[i % dim] = w[i % dim] + (1 + i // dim)
+        rows[1000 + i] = w
+    qs = oracle_mod.unit_fp16(64, dim, seed=902)
+    qs[0] = v
+    idx = _index(rows, gpu, base=7)
+    assert idx.scan_nontemporal(64, 5)
+    got = _run(idx, qs, 5, gpu)
+    assert got["flags"][0] != 1  # query 0 went through the collect pass
+    exact = idx.topk(_dev(qs.view(np.float16), gpu), 5, exact=True)
+    torch.cuda.synchronize()
+    for f in ("ids", "scores", "rank", "count"):
+        np.testing.assert_array_equal(got[f], getattr(exact, f).cpu().numpy(), err_msg=f)
+    sample = [0, 1, 63]
+    ref = oracle_mod.dense_topk(rows, qs[sample], 5, ordinal_base=7)
+    np.testing.assert_array_equal(got["ids"][sample], ref.ids)
+    np.testing.assert_array_equal(got["scores"][sample], ref.scores)
+    small = _index(rows[:100_000], gpu)
+    assert not small.scan_nontemporal(64, 5)  # 100 MB image: plain loads
