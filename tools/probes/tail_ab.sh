@@ -1,5 +1,6 @@
 #!/bin/bash
 # Dense int8 first pass: static ranges vs a dynamic tail (ARMI_I8_TAIL_STATIC builds under ablibs/).
+# Record of the r04ah A/B (profiles/r04ah_dense_tail_ab.txt): the tail form and its build flag were removed after it.
 # Parity of each variant under -m gpu, then interleaved 1M / 100k bench lines and the stamps.
 TAG=${1:-tab}
 cd "$GRAFT_REPO_ROOT" || exit 1; mkdir -p gpurun_out
