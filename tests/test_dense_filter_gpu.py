@@ -126,15 +126,17 @@ def test_certified_at_100k(gpu, oracle_mod, k):
 
 def test_nontemporal_stream_first_and_collect_pass(gpu, oracle_mod):
     """A shard whose int8 image (> 192 MB) streams with nontemporal loads: the first pass and the
-    collect pass (forced: 60 near-duplicates of query 0 overflow its workgroup list, so it is not
-    certified) run the <dim, *, true> kernel instances; every query equals the exhaustive exact
-    scan, a sample the oracle."""
+    collect pass run the <dim, *, true> kernel instances. The collect pass is forced: 300 one-ulp
+    variants of query 0 (the scattered image order spreads them over the workgroups, so every
+    list keeps them) are more than the merge rescores (kc = 64), and the rest of them, with
+    upper bounds above the 5th exact key, leave query 0 uncertified. Every query equals the
+    exhaustive exact scan, a sample the oracle."""
     n, dim = 262_144 + 96, 1024
     rows = oracle_mod.unit_fp16(n, dim, seed=901)
     v = rows[5].copy()
-    for i in range(60):  # one-ulp variants of v in consecutive rows (one workgroup's range)
+    for i in range(300):  # one-ulp variants of v (one component each)
         w = v.copy()
-        w[i % dim] = w[i % dim] + (1 + i // dim)
+        w[i] = w[i] + 1
         rows[1000 + i] = w
     qs = oracle_mod.unit_fp16(64, dim, seed=902)
     qs[0] = v
