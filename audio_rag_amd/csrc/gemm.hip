@@ -357,6 +357,60 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
   if (wp == 0) __builtin_amdgcn_s_barrier();
 }
 
+
+// out[m][n] = epi(x . w^T + bias) for a few token rows (m <= 32: the batch-1 query encode of
+// BGE-M3, embeddings/xlmr_f16.py), where the GEMM is a weight stream: workgroup j owns output
+// columns 16j .. 16j + 15 and its 8 waves split K in eighths; each wave runs
+// v_mfma_f32_16x16x32_f16 over its slice with the weight rows read straight from HBM (lane l:
+// column l & 15, k 8 (l >> 4) .. + 7 of each 32-step, i.e. 16 contiguous bytes of the [n][k]
+// row), the token rows from L2; the 8 partial tiles are summed in LDS in wave order (the same
+// result every run), then bias (+ exact GELU) and the fp16 store.
+template <int EPI>
+__global__ __launch_bounds__(512) void linear_small_m_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
+    uint16_t* __restrict__ out, int m, int n, int k) {
+  __shared__ float part[8][2][16][17];  // [wave][row tile][row][col] (+1: bank spread)
+  const int wave = armi::wave_id();
+  const int lane = threadIdx.x & 63;
+  const int n0 = blockIdx.x * 16;
+  const int kw = k / 8;
+  const int kb = wave * kw;
+  const int c = lane & 15, kq = 8 * (lane >> 4);
+  const uint16_t* wp = w + (size_t)(n0 + c) * k + kb + kq;
+  const uint16_t* xp0 = x + (size_t)c * k + kb + kq;
+  const uint16_t* xp1 = x + (size_t)(c + 16) * k + kb + kq;
+  const bool r0 = c < m, r1 = c + 16 < m, two = m > 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < kw; s += 32) {
+    const u32x4 b = *reinterpret_cast<const u32x4*>(wp + s);
+    const u32x4 a0 = r0 ? *reinterpret_cast<const u32x4*>(xp0 + s) : u32x4{0u, 0u, 0u, 0u};
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a0),
+                                                  __builtin_bit_cast(half8, b), acc0, 0, 0, 0);
+    if (two) {
+      const u32x4 a1 = r1 ? *reinterpret_cast<const u32x4*>(xp1 + s) : u32x4{0u, 0u, 0u, 0u};
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a1),
+                                                    __builtin_bit_cast(half8, b), acc1, 0, 0, 0);
+    }
+  }
+  // D layout of the 16x16 tile: lane l holds column l & 15, rows 4 (l >> 4) + j
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    part[wave][0][4 * (lane >> 4) + j][c] = acc0[j];
+    part[wave][1][4 * (lane >> 4) + j][c] = acc1[j];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;  // output (tile, row, col) = (t >> 8, (t >> 4) & 15, t & 15)
+  const int tile = t >> 8, row = 16 * tile + ((t >> 4) & 15), col = t & 15;
+  if (row < m) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += part[q][tile][(t >> 4) & 15][col];
+    v += bias[n0 + col];
+    if (EPI == ARMI_EPI_BIAS_GELU) v = gelu_erf(v);
+    out[(size_t)row * n + n0 + col] = __builtin_bit_cast(uint16_t, (_Float16)v);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -397,6 +451,24 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
   kern<<<dim3(grid), dim3(kThreads), kLds, stream>>>(x, w, bias, out, m, n, k, n_tp, n_tiles);
   ARMI_LAUNCHED("linear_f16_kernel");
   return tl.end();
+}
+
+
+int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float* bias,
+                              uint16_t* out, int m, int n, int k, int epilogue,
+                              hipStream_t stream) {
+  ARMI_REQUIRE(m >= 0 && m <= 32, "enc_linear_small_f16: m must be in [0, 32]");
+  ARMI_REQUIRE(n >= 16 && n % 16 == 0, "enc_linear_small_f16: n must be a multiple of 16");
+  ARMI_REQUIRE(k >= 256 && k % 256 == 0 && (int64_t)n * k < (int64_t(1) << 31),
+               "enc_linear_small_f16: k must be a multiple of 256 (n * k < 2^31)");
+  ARMI_REQUIRE(epilogue == ARMI_EPI_BIAS || epilogue == ARMI_EPI_BIAS_GELU,
+               "enc_linear_small_f16: unknown epilogue");
+  if (m == 0) return ARMI_OK;
+  ARMI_REQUIRE(x && w && bias && out, "enc_linear_small_f16: null pointer argument");
+  auto kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_small_m_kernel<1> : linear_small_m_kernel<0>;
+  kern<<<dim3(n / 16), dim3(512), 0, stream>>>(x, w, bias, out, m, n, k);
+  ARMI_LAUNCHED("linear_small_m_kernel");
+  return ARMI_OK;
 }
 
 }  // extern "C"

@@ -11,7 +11,8 @@ the sparse head's token weights relu(Linear(d -> 1)(h)).
 
 Seven kernels per layer instead of the ~16 of the transformers forward: a captured query encode
 is launch-bound (a 16-token query reads 0.6 GB of weights, 0.1 ms at HBM rate), so the kernel
-count sets its latency.
+count sets its latency. Up to 32 token rows the four linears run on armi_enc_linear_small_f16
+(the intermediate dense with its GELU fused: six kernels per layer).
 """
 
 from __future__ import annotations
@@ -48,6 +49,11 @@ class XLMREncoderF16:
             self.layers.append(dict(
                 wqkv=f16(torch.cat([sd[a + "query.weight"], sd[a + "key.weight"],
                                     sd[a + "value.weight"]])),
+                bqkv32=f32(torch.cat([sd[a + "query.bias"], sd[a + "key.bias"],
+                                      sd[a + "value.bias"]])),
+                bo32=f32(sd[p + "attention.output.dense.bias"]),
+                bi32=f32(sd[p + "intermediate.dense.bias"]),
+                bo232=f32(sd[p + "output.dense.bias"]),
                 bqkv=f16(torch.cat([sd[a + "query.bias"], sd[a + "key.bias"],
                                     sd[a + "value.bias"]])),
                 wo=f16(sd[p + "attention.output.dense.weight"]),
@@ -65,6 +71,23 @@ class XLMREncoderF16:
             self.sparse = (f16(sparse_linear.weight.detach().to(device)),
                            f16(sparse_linear.bias.detach().to(device)))
 
+    # token rows up to which the linears run on armi_enc_linear_small_f16 (a weight stream with
+    # the GELU fused) instead of hipBLASLt
+    SMALL_M = 32
+
+    def _lin(self, x: torch.Tensor, ly: dict, w: str, b: str, gelu: bool = False) -> torch.Tensor:
+        m = x.shape[0]
+        if m <= self.SMALL_M:
+            n = ly[w].shape[0]
+            out = torch.empty((m, n), dtype=torch.float16, device=self.device)
+            call("armi_enc_linear_small_f16", ptr(x), ptr(ly[w]), ptr(ly[b + "32"]), ptr(out), m,
+                 n, ly[w].shape[1], 1 if gelu else 0, stream_handle())
+            return out
+        y = torch.nn.functional.linear(x, ly[w], ly[b])
+        if gelu:
+            call("armi_enc_gelu_f16", ptr(y), None, y.shape[0], y.shape[1], stream_handle())
+        return y
+
     def forward(self, ids: torch.Tensor, mask: torch.Tensor):
         """ids, mask: int32 [n, L] on the device -> (dense fp16 [n, d] L2-normalised <s> rows,
         sparse token weights fp32 [n, L] or None)."""
@@ -80,16 +103,15 @@ class XLMREncoderF16:
         h16 = h.half()
         scale = 1.0 / math.sqrt(dh)
         for ly in self.layers:
-            qkv = lin(h16, ly["wqkv"], ly["bqkv"])                           # [n*L, 3d]
+            qkv = self._lin(h16, ly, "wqkv", "bqkv")                         # [n*L, 3d]
             ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)
             call("armi_enc_attention_f16", ptr(qkv), ptr(mask), ptr(ctx), n, L, H, dh, scale, s)
-            attn = lin(ctx, ly["wo"], ly["bo"])
+            attn = self._lin(ctx, ly, "wo", "bo")
             h1 = torch.empty_like(h16)
             call("armi_enc_add_layernorm_f16", ptr(attn), ptr(h16), ptr(ly["ln1"][0]),
                  ptr(ly["ln1"][1]), ptr(h1), rows, d, self.eps, s)
-            inter = lin(h1, ly["wi"], ly["bi"])                              # [n*L, 4d]
-            call("armi_enc_gelu_f16", ptr(inter), None, rows, inter.shape[1], s)
-            out = lin(inter, ly["wo2"], ly["bo2"])
+            inter = self._lin(h1, ly, "wi", "bi", gelu=True)                 # [n*L, 4d]
+            out = self._lin(inter, ly, "wo2", "bo2")
             h16 = torch.empty_like(h1)
             call("armi_enc_add_layernorm_f16", ptr(out), ptr(h1), ptr(ly["ln2"][0]),
                  ptr(ly["ln2"][1]), ptr(h16), rows, d, self.eps, s)

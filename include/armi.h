@@ -375,6 +375,13 @@ int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
 #define ARMI_EPI_BIAS_GELU 1
 int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out,
                         int64_t m, int n, int k, int epilogue, hipStream_t stream);
+/* The same layer for m <= 32 token rows (the batch-1 query encode of BGE-M3,
+ * embeddings/bge.py:137-157 through embeddings/xlmr_f16.py): a weight stream, 16 output columns
+ * per workgroup, K split over its 8 waves and summed in a fixed order. n % 16 == 0,
+ * k % 256 == 0; bias fp32 [n]. */
+int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float* bias,
+                              uint16_t* out, int m, int n, int k, int epilogue,
+                              hipStream_t stream);
 
 #ifdef __cplusplus
 }

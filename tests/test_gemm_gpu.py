@@ -45,3 +45,28 @@ def test_linear_f16_rejects_bad_shapes(gpu):
         call("armi_enc_linear_f16", None, None, None, None, 10, 100, 768, 0, stream_handle())
     with pytest.raises(ArmiError):
         call("armi_enc_linear_f16", None, None, None, None, 10, 256, 100, 0, stream_handle())
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(1, 3072, 1024, 0), (7, 1024, 1024, 0), (16, 4096, 1024, 1),
+                                       (17, 1024, 4096, 0), (32, 3072, 1024, 1),
+                                       (12, 16, 256, 0)])
+def test_linear_small_m_matches_fp32(gpu, m, n, k, epi):
+    """armi_enc_linear_small_f16 (the batch-1 query encode's weight-stream GEMM, m <= 32) against
+    the same torch fp32 reference; rows of the output buffer past m stay untouched."""
+    from audio_rag_amd._armi import call, ptr, stream_handle
+
+    g = torch.Generator(device=gpu).manual_seed(7 * m + n + k)
+    x = torch.randn((m, k), generator=g, device=gpu).half()
+    w = (torch.randn((n, k), generator=g, device=gpu) / k ** 0.5).half()
+    w[:, 0] += torch.arange(n, device=gpu).half() * 1e-3
+    b = torch.randn(n, generator=g, device=gpu) * 0.1
+    out = torch.full((m + 2, n), float("nan"), dtype=torch.float16, device=gpu)
+    call("armi_enc_linear_small_f16", ptr(x), ptr(w), ptr(b), ptr(out), m, n, k, epi,
+         stream_handle())
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t() + b
+    if epi:
+        ref = torch.nn.functional.gelu(ref)
+    assert not torch.isnan(out[:m]).any()
+    assert torch.isnan(out[m:]).all()
+    torch.testing.assert_close(out[:m].float(), ref, rtol=2 ** -10, atol=1e-3)
