@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
 // column l & 15, k 8 (l >> 4) .. + 7 of each 32-step, i.e. 16 contiguous bytes of the [n][k]
 // row), the token rows from L2; the 8 partial tiles are summed in LDS in wave order (the same
 // result every run), then bias (+ exact GELU) and the fp16 store.
-template <int EPI>
+template <int EPI, int STEPS>
 __global__ __launch_bounds__(512) void linear_small_m_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
     uint16_t* __restrict__ out, int m, int n, int k) {
@@ -381,8 +381,7 @@ __global__ __launch_bounds__(512) void linear_small_m_kernel(
   const uint16_t* xp1 = x + (size_t)(c + 16) * k + kb + kq;
   const bool r0 = c < m, r1 = c + 16 < m, two = m > 16;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < kw; s += 32) {
-    const u32x4 b = *reinterpret_cast<const u32x4*>(wp + s);
+  auto step = [&](const u32x4& b, int s) {
     const u32x4 a0 = r0 ? *reinterpret_cast<const u32x4*>(xp0 + s) : u32x4{0u, 0u, 0u, 0u};
     acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a0),
                                                   __builtin_bit_cast(half8, b), acc0, 0, 0, 0);
@@ -391,6 +390,17 @@ __global__ __launch_bounds__(512) void linear_small_m_kernel(
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a1),
                                                     __builtin_bit_cast(half8, b), acc1, 0, 0, 0);
     }
+  };
+  if constexpr (STEPS > 0) {
+    // the slice's weight pieces (the HBM stream) all in flight before the first MFMA; the token
+    // rows are L2 hits
+    u32x4 b[STEPS];
+#pragma unroll
+    for (int i = 0; i < STEPS; ++i) b[i] = *reinterpret_cast<const u32x4*>(wp + 32 * i);
+#pragma unroll
+    for (int i = 0; i < STEPS; ++i) step(b[i], 32 * i);
+  } else {
+    for (int s = 0; s < kw; s += 32) step(*reinterpret_cast<const u32x4*>(wp + s), s);
   }
   // D layout of the 16x16 tile: lane l holds column l & 15, rows 4 (l >> 4) + j
 #pragma unroll
@@ -465,7 +475,12 @@ int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float*
                "enc_linear_small_f16: unknown epilogue");
   if (m == 0) return ARMI_OK;
   ARMI_REQUIRE(x && w && bias && out, "enc_linear_small_f16: null pointer argument");
-  auto kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_small_m_kernel<1> : linear_small_m_kernel<0>;
+  const bool g = epilogue == ARMI_EPI_BIAS_GELU;
+  auto kern = k == 1024 ? (g ? linear_small_m_kernel<1, 4> : linear_small_m_kernel<0, 4>)
+              : k == 4096 ? (g ? linear_small_m_kernel<1, 16> : linear_small_m_kernel<0, 16>)
+              : k == 768  ? (g ? linear_small_m_kernel<1, 3> : linear_small_m_kernel<0, 3>)
+              : k == 3072 ? (g ? linear_small_m_kernel<1, 12> : linear_small_m_kernel<0, 12>)
+                          : (g ? linear_small_m_kernel<1, 0> : linear_small_m_kernel<0, 0>);
   kern<<<dim3(n / 16), dim3(512), 0, stream>>>(x, w, bias, out, m, n, k);
   ARMI_LAUNCHED("linear_small_m_kernel");
   return ARMI_OK;
