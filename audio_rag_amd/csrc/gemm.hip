@@ -360,20 +360,20 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
 
 // out[m][n] = epi(x . w^T + bias) for a few token rows (m <= 32: the batch-1 query encode of
 // BGE-M3, embeddings/xlmr_f16.py), where the GEMM is a weight stream: workgroup j owns output
-// columns 16j .. 16j + 15 and its 8 waves split K in eighths; each wave runs
+// columns 16j .. 16j + 15 and its WAVES waves split K evenly; each wave runs
 // v_mfma_f32_16x16x32_f16 over its slice with the weight rows read straight from HBM (lane l:
 // column l & 15, k 8 (l >> 4) .. + 7 of each 32-step, i.e. 16 contiguous bytes of the [n][k]
-// row), the token rows from L2; the 8 partial tiles are summed in LDS in wave order (the same
+// row), the token rows from L2; the partial tiles are summed in LDS in wave order (the same
 // result every run), then bias (+ exact GELU) and the fp16 store.
-template <int EPI, int STEPS>
-__global__ __launch_bounds__(512) void linear_small_m_kernel(
+template <int EPI, int STEPS, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void linear_small_m_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
     uint16_t* __restrict__ out, int m, int n, int k) {
-  __shared__ float part[8][2][16][17];  // [wave][row tile][row][col] (+1: bank spread)
+  __shared__ float part[WAVES][2][16][17];  // [wave][row tile][row][col] (+1: bank spread)
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
   const int n0 = blockIdx.x * 16;
-  const int kw = k / 8;
+  const int kw = k / WAVES;
   const int kb = wave * kw;
   const int c = lane & 15, kq = 8 * (lane >> 4);
   const uint16_t* wp = w + (size_t)(n0 + c) * k + kb + kq;
@@ -411,10 +411,10 @@ __global__ __launch_bounds__(512) void linear_small_m_kernel(
   __syncthreads();
   const int t = threadIdx.x;  // output (tile, row, col) = (t >> 8, (t >> 4) & 15, t & 15)
   const int tile = t >> 8, row = 16 * tile + ((t >> 4) & 15), col = t & 15;
-  if (row < m) {
+  if (t < 512 && row < m) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v += part[q][tile][(t >> 4) & 15][col];
+    for (int q = 0; q < WAVES; ++q) v += part[q][tile][(t >> 4) & 15][col];
     v += bias[n0 + col];
     if (EPI == ARMI_EPI_BIAS_GELU) v = gelu_erf(v);
     out[(size_t)row * n + n0 + col] = __builtin_bit_cast(uint16_t, (_Float16)v);
@@ -476,11 +476,18 @@ int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float*
   if (m == 0) return ARMI_OK;
   ARMI_REQUIRE(x && w && bias && out, "enc_linear_small_f16: null pointer argument");
   const bool g = epilogue == ARMI_EPI_BIAS_GELU;
-  auto kern = k == 1024 ? (g ? linear_small_m_kernel<1, 4> : linear_small_m_kernel<0, 4>)
-              : k == 4096 ? (g ? linear_small_m_kernel<1, 16> : linear_small_m_kernel<0, 16>)
-              : k == 768  ? (g ? linear_small_m_kernel<1, 3> : linear_small_m_kernel<0, 3>)
-              : k == 3072 ? (g ? linear_small_m_kernel<1, 12> : linear_small_m_kernel<0, 12>)
-                          : (g ? linear_small_m_kernel<1, 0> : linear_small_m_kernel<0, 0>);
+  // K = 4096 / 3072 (the output dense: 64 or 48 workgroups for 8 or 6 MB of weights): 16 waves
+  // per workgroup, twice the loads in flight per CU
+  if (k == 4096 || k == 3072) {
+    auto kern = k == 4096 ? (g ? linear_small_m_kernel<1, 8, 16> : linear_small_m_kernel<0, 8, 16>)
+                          : (g ? linear_small_m_kernel<1, 6, 16> : linear_small_m_kernel<0, 6, 16>);
+    kern<<<dim3(n / 16), dim3(1024), 0, stream>>>(x, w, bias, out, m, n, k);
+    ARMI_LAUNCHED("linear_small_m_kernel");
+    return ARMI_OK;
+  }
+  auto kern = k == 1024 ? (g ? linear_small_m_kernel<1, 4, 8> : linear_small_m_kernel<0, 4, 8>)
+              : k == 768  ? (g ? linear_small_m_kernel<1, 3, 8> : linear_small_m_kernel<0, 3, 8>)
+                          : (g ? linear_small_m_kernel<1, 0, 8> : linear_small_m_kernel<0, 0, 8>);
   kern<<<dim3(n / 16), dim3(512), 0, stream>>>(x, w, bias, out, m, n, k);
   ARMI_LAUNCHED("linear_small_m_kernel");
   return ARMI_OK;
