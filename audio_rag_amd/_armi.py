@@ -23,7 +23,7 @@ ARMI_FLAG_CERTIFIED = 1
 ARMI_FLAG_FALLBACK = 2
 TIMING_DENSE_SCAN, TIMING_SPARSE_SCAN, TIMING_ENCODER_GEMM = 0, 1, 2
 SCAN_FP16, SCAN_INT8_FILTER, SCAN_TILED_FP16, SCAN_TILED_INT8 = 0, 1, 2, 3  # armi_dense_scan_form
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

@@ -1,5 +1,6 @@
 // Error plumbing of the C ABI (thread-local last error).
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -22,6 +23,20 @@ int hip_fail(hipError_t e, const char* what) {
   std::string m = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
   set_error(m);
   return ARMI_ERR_HIP;
+}
+
+int allow_lds_raw(const void* kernel, size_t bytes) {
+  if (bytes <= 65536) return ARMI_OK;
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, size_t> raised;
+  int dev = 0;
+  ARMI_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  size_t& have = raised[{dev, kernel}];
+  if (have >= bytes) return ARMI_OK;
+  ARMI_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  have = bytes;
+  return ARMI_OK;
 }
 
 struct Timing {

@@ -44,6 +44,15 @@ struct TimedLaunch {
   int end();
 };
 
+// Raises a kernel's dynamic-LDS limit to `bytes` (> 64 KiB needs it) on the current device, once
+// per (device, kernel): later searches issue stream work only (no runtime call per search, so the
+// calls stay graph-capturable). The attribute is per device, hence the device in the key.
+int allow_lds_raw(const void* kernel, size_t bytes);
+template <typename K>
+inline int allow_lds(K kernel, size_t bytes) {
+  return allow_lds_raw(reinterpret_cast<const void*>(kernel), bytes);
+}
+
 // Carves consecutive 256-B aligned sub-buffers out of one caller workspace.
 struct Carver {
   char* base;

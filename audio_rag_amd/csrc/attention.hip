@@ -621,12 +621,9 @@ int armi_enc_attention_f16(const uint16_t* qkv, const int32_t* mask, uint16_t* c
   ARMI_REQUIRE(n_seq <= 65535, "attention_f16: n_seq must be <= 65535 per call");
   ARMI_REQUIRE(qkv && mask && ctx, "attention_f16: null pointer argument");
   const size_t lds = attention_lds_bytes(L);
-  // raise the dynamic-LDS limit once, to the largest L (not per call: keeps the launch path free
-  // of non-stream runtime calls, so it can be captured in a HIP graph)
-  static const hipError_t raised = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(attention_f16_kernel),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_lds_bytes(kMaxL));
-  ARMI_HIP(raised);
+  // raise the dynamic-LDS limit once per device, to the largest L (not per call: keeps the
+  // launch path free of non-stream runtime calls, so it can be captured in a HIP graph)
+  if (int rc = armi::allow_lds(attention_f16_kernel, attention_lds_bytes(kMaxL))) return rc;
   const float scale_log2 = scale * 1.4426950408889634f;
   attention_f16_kernel<<<dim3((L + kQPerWg - 1) / kQPerWg, heads, n_seq), dim3(kThreads), lds,
                          stream>>>(qkv, mask, ctx, L, heads, scale_log2);

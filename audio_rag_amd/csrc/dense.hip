@@ -2458,21 +2458,7 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
   return w;
 }
 
-// Enables > 64 KiB of dynamic LDS for a kernel, once per (kernel, size) in the process: the
-// search calls then issue stream work only (no runtime call per search, graph-capturable).
-template <typename K>
-int allow_lds(K kernel, size_t bytes) {
-  if (bytes <= 65536) return ARMI_OK;
-  static std::mutex mu;
-  static std::map<const void*, size_t> raised;
-  const void* f = reinterpret_cast<const void*>(kernel);
-  std::lock_guard<std::mutex> g(mu);
-  auto it = raised.find(f);
-  if (it != raised.end() && it->second >= bytes) return ARMI_OK;
-  ARMI_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  raised[f] = bytes;
-  return ARMI_OK;
-}
+using armi::allow_lds;
 
 // out_rank must be non-null (callers substitute workspace scratch).
 template <int DIM>

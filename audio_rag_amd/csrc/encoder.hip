@@ -300,10 +300,9 @@ int armi_enc_cls_head_sigmoid(const float* hidden, const float* dense_wt, const 
                "cls_head: null pointer argument");
   const int threads = (width + 63) / 64 * 64;
   const size_t lds = ((size_t)kHeadSeq * width + (size_t)kHeadSeq * (threads / 64)) * sizeof(float);
-  static const hipError_t raised = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(cls_head_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)(((size_t)kHeadSeq * 1024 + kHeadSeq * 16) * sizeof(float)));
-  ARMI_HIP(raised);
+  if (int rc = armi::allow_lds(cls_head_kernel,
+                               ((size_t)kHeadSeq * 1024 + kHeadSeq * 16) * sizeof(float)))
+    return rc;
   cls_head_kernel<<<dim3((n_seq + kHeadSeq - 1) / kHeadSeq), dim3(threads), lds, stream>>>(
       hidden, dense_wt, dense_b, out_w, out_b, out, n_seq, L, width);
   ARMI_LAUNCHED("cls_head_kernel");

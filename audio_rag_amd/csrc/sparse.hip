@@ -65,7 +65,6 @@ constexpr int kBmWords = kBitmapVocab / 32;
 constexpr size_t kPrepBmLds = (size_t)kBmWords * 8;    // term bitmap + per-word prefix, 64 KB
 constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
-constexpr uint32_t kFlagOverflow = 4u;
 static_assert(kQW * kKW == 64, "one 16-lane list segment per query of the wave");
 
 // ------------------------------------------------------------------------- index build
@@ -1143,34 +1142,232 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   }
 }
 
+// Second-pass merge, one workgroup per query of the pass (certified queries exit at once): sort
+// the rows the collect pass appended (every row scoring >= the k-th candidate) and keep k.
+// A list that overflowed (more than kCollectCap rows reach the threshold: a pile of re-uploaded
+// identical chunks, or a threshold of -inf when the merge held fewer than k candidates) is
+// answered by the grid's n_help helper workgroups instead, exactly: helper h scores its 1/n_help
+// of the shard's rows for that query, term at a time in ascending term order (fl32(w * v) added
+// to an fp32 sum that starts at 0: the scan's sum, whose absent terms add +-0), keeps its slice's
+// top k by (score desc, row asc) and writes them into the query's collect list at slot h * k;
+// the last helper to finish (a per-query counter, zeroed with the collect counts) sorts those
+// n_help * k <= kCollectCap rows and emits the top k. On calls without an overflowed list the
+// helpers check every query's count at once and exit.
+constexpr int kHelpRows = 4096;                // rows a helper scores per chunk
+constexpr int kHelpPer = kHelpRows / 256;      // ... per thread (thread t owns rows t + 256 i)
+constexpr int kMaxHelp = 64;
+constexpr int kBestPad = 256;                  // the running best list (>= kMaxK entries)
+constexpr int kHelpSort = 8192;                // >= kBestPad + kHelpRows, a power of 2
+static_assert(kBestPad >= kMaxK && kHelpSort >= kBestPad + kHelpRows, "helper sort buffer");
+static_assert(kHelpSort >= kCollectCap, "the collect list sorts in the same buffer");
+// sort buffer (key f32, row i32), chunk accumulators, chunk row flags, per-term weight / dense
+// column / cursor / list end, small shared words
+constexpr size_t kCollectLds =
+    (size_t)kHelpSort * 8 + kHelpRows * 4 + kHelpRows + (size_t)kMaxTerms * 16 + 64;
+
 __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
-    const int* __restrict__ coll_count, const float* __restrict__ coll_key,
-    const int32_t* __restrict__ coll_row, int q_first, int k, int64_t ordinal_base,
-    float* __restrict__ out_scores, int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count,
-    uint32_t* __restrict__ flags) {
-  const int ql = blockIdx.x;
-  const int qg = q_first + ql;
-  if (flags[ql] & ARMI_FLAG_CERTIFIED) return;
+    const int* __restrict__ coll_count, float* __restrict__ coll_key,
+    int32_t* __restrict__ coll_row, int* __restrict__ help_done, int nq, int q_first, int k,
+    int64_t ordinal_base, int64_t n_rows, const uint64_t* __restrict__ row_mask,
+    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
+    const int32_t* __restrict__ dense_of, const uint32_t* __restrict__ dense_val,
+    int64_t dense_stride, const int32_t* __restrict__ uterm, const QTerm* __restrict__ qlist,
+    const int32_t* __restrict__ qu, const int32_t* __restrict__ qcount,
+    const int32_t* __restrict__ qof, float* __restrict__ out_scores,
+    int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* key = reinterpret_cast<float*>(smem);
-  int32_t* row = reinterpret_cast<int32_t*>(smem + kCollectCap * 4);
-  const int total = coll_count[ql];
-  const int n = min(total, kCollectCap);
-  const int n2 = armi::pow2_at_least(max(n, 2));
-  for (int e = threadIdx.x; e < n2; e += 256) {
-    key[e] = e < n ? coll_key[(size_t)ql * kCollectCap + e] : kNegInf;
-    row[e] = e < n ? coll_row[(size_t)ql * kCollectCap + e] : 0x7fffffff;
+  float* skey = reinterpret_cast<float*>(smem);                      // [kHelpSort]
+  int32_t* srow = reinterpret_cast<int32_t*>(smem + kHelpSort * 4);  // [kHelpSort]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = armi::wave_id();
+  // emit the sorted [0, k) of skey / srow for query ql (valid entries form a prefix)
+  auto write_out = [&](int ql) {
+    if (wave != 0) return;
+    int nv = 0;
+    for (int c = lane; c < k; c += 64) nv += srow[c] != kEndRow;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nv += armi::xor_stride(nv, off);
+    const int qg = q_first + ql;
+    for (int c = lane; c < k; c += 64) {
+      const size_t o = (size_t)qg * k + c;
+      out_scores[o] = c < nv ? skey[c] : kNegInf;
+      out_ids[o] = c < nv ? ordinal_base + srow[c] : -1;
+    }
+    if (lane == 0) {
+      out_count[qg] = nv;
+      flags[ql] |= ARMI_FLAG_FALLBACK;
+    }
+  };
+  if ((int)blockIdx.x < nq) {  // the query's own workgroup
+    const int ql = blockIdx.x;
+    if (flags[ql] & ARMI_FLAG_CERTIFIED) return;  // workgroup-uniform
+    const int total = coll_count[ql];
+    if (total > kCollectCap) return;  // overflowed: the helpers answer it
+    const int n2 = armi::pow2_at_least(max(max(total, k), 2));
+    for (int e = tid; e < n2; e += 256) {
+      skey[e] = e < total ? coll_key[(size_t)ql * kCollectCap + e] : kNegInf;
+      srow[e] = e < total ? coll_row[(size_t)ql * kCollectCap + e] : kEndRow;
+    }
+    armi::lds_sort_approx_desc(skey, srow, n2);
+    __syncthreads();
+    write_out(ql);
+    return;
   }
-  armi::lds_sort_approx_desc(key, row, n2);
-  const int nv = min(n, k);
-  for (int c = threadIdx.x; c < k; c += 256) {
-    const size_t o = (size_t)qg * k + c;
-    out_scores[o] = c < nv ? key[c] : kNegInf;
-    out_ids[o] = c < nv ? ordinal_base + row[c] : -1;
-  }
-  if (threadIdx.x == 0) {
-    out_count[qg] = nv;
-    flags[ql] |= ARMI_FLAG_FALLBACK | (total > kCollectCap ? kFlagOverflow : 0u);
+  const int n_help = (int)gridDim.x - nq;
+  const int h = (int)blockIdx.x - nq;
+  bool any = false;
+  for (int q = tid; q < nq; q += 256)
+    any |= !(flags[q] & ARMI_FLAG_CERTIFIED) && coll_count[q] > kCollectCap;
+  if (!__syncthreads_or(any)) return;  // workgroup-uniform
+  float* acc = reinterpret_cast<float*>(smem + kHelpSort * 8);                  // [kHelpRows]
+  uint8_t* has = smem + kHelpSort * 8 + kHelpRows * 4;                          // [kHelpRows]
+  float* tw = reinterpret_cast<float*>(has + kHelpRows);                        // [kMaxTerms]
+  int32_t* tcol = reinterpret_cast<int32_t*>(tw + kMaxTerms);                   // [kMaxTerms]
+  int32_t* tcur = tcol + kMaxTerms;                                             // [kMaxTerms]
+  int32_t* tend = tcur + kMaxTerms;                                             // [kMaxTerms]
+  int* sh = reinterpret_cast<int*>(tend + kMaxTerms);  // [0] slot, [1] survivors, [2] last helper
+  const int64_t lo = n_rows * h / n_help, hi = n_rows * (h + 1) / n_help;
+  for (int ql = 0; ql < nq; ++ql) {
+    if ((flags[ql] & ARMI_FLAG_CERTIFIED) || coll_count[ql] <= kCollectCap) continue;  // uniform
+    __syncthreads();  // the previous query is done with the shared arrays
+    if (tid < kQB && qof[tid] == ql) sh[0] = tid;
+    for (int e = tid; e < kBestPad; e += 256) {
+      skey[e] = kNegInf;
+      srow[e] = kEndRow;
+    }
+    __syncthreads();
+    const int slot = sh[0];
+    const int nt = qcount[slot];
+    for (int j = tid; j < nt; j += 256) {  // the query's terms, ascending
+      const int32_t t = uterm[qu[slot * kQStride + j]];
+      tw[j] = qlist[slot * kQStride + j].w;
+      const int32_t d = dense_of[t];
+      tcol[j] = d;
+      // non-dense term: its first posting at or after row lo, and its list's sentinel
+      const int32_t b = term_ptr[t], e = term_ptr[t + 1] - 1;
+      int32_t a = b, n = d >= 0 ? 0 : e - b;
+      while (n > 0) {
+        const int32_t hh = n >> 1;
+        if (post[a + hh].x < lo) {
+          a += hh + 1;
+          n -= hh + 1;
+        } else {
+          n = hh;
+        }
+      }
+      tcur[j] = a;
+      tend[j] = e;
+    }
+    __syncthreads();
+    for (int64_t c0 = lo; c0 < hi; c0 += kHelpRows) {
+      const int32_t chi = (int32_t)min<int64_t>(c0 + kHelpRows, hi);
+      const int32_t r0 = (int32_t)c0;
+#pragma unroll
+      for (int i = 0; i < kHelpPer; ++i) {  // owner-local clear
+        acc[tid + 256 * i] = 0.f;
+        has[tid + 256 * i] = 0;
+      }
+      bool scattered = false;  // a posting term wrote other threads' rows since the last barrier
+      for (int j = 0; j < nt; ++j) {
+        const int32_t d = tcol[j];
+        const float w = tw[j];
+        if (d >= 0) {  // dense column: each thread adds to its own rows, no barrier between terms
+          if (scattered) {
+            __syncthreads();
+            scattered = false;
+          }
+          const uint32_t* col = dense_val + (size_t)d * dense_stride;
+          uint32_t v[kHelpPer];
+#pragma unroll
+          for (int i = 0; i < kHelpPer; ++i) {
+            const int32_t r = r0 + tid + 256 * i;
+            v[i] = r < chi ? col[r] : 0u;
+          }
+#pragma unroll
+          for (int i = 0; i < kHelpPer; ++i) {
+            if (v[i] != 0u) {  // 0 = no posting (a zero value is stored as -0.0)
+              const int e = tid + 256 * i;
+              acc[e] = acc[e] + w * __uint_as_float(v[i]);
+              has[e] = 1;
+            }
+          }
+        } else {  // postings: the chunk's ones are a prefix from the cursor (rows ascend)
+          __syncthreads();
+          int32_t cur = tcur[j];
+          const int32_t end = tend[j];
+          for (;;) {
+            const int32_t e = cur + tid;
+            const int2 p = e < end ? post[e] : make_int2(kEndRow, 0);
+            const bool in = p.x < chi;
+            if (in) {
+              const int r = p.x - r0;
+              acc[r] = acc[r] + w * __int_as_float(p.y);
+              has[r] = 1;
+            }
+            const int n_in = __syncthreads_count(in);
+            cur += n_in;
+            if (n_in < 256) break;
+          }
+          if (tid == 0) tcur[j] = cur;  // read again after the next chunk's barriers
+          scattered = true;
+        }
+      }
+      if (tid == 0) sh[1] = 0;
+      __syncthreads();
+      // rows better than the running k-th (key desc, row asc) join the best list
+      const float kk = skey[k - 1];
+      const int32_t kr = srow[k - 1];
+#pragma unroll
+      for (int i = 0; i < kHelpPer; ++i) {
+        const int e = tid + 256 * i;
+        const int32_t r = r0 + e;
+        const bool on = r < chi && has[e] &&
+                        (!row_mask || ((row_mask[r >> 6] >> (r & 63)) & 1ull));
+        if (on && armi::approx_better(acc[e], r, kk, kr)) {
+          const int s2 = atomicAdd(&sh[1], 1);
+          skey[kBestPad + s2] = acc[e];
+          srow[kBestPad + s2] = r;
+        }
+      }
+      __syncthreads();
+      const int ns = sh[1];
+      if (ns > 0) {  // uniform
+        const int n2 = armi::pow2_at_least(kBestPad + ns);
+        for (int e = kBestPad + ns + tid; e < n2; e += 256) {
+          skey[e] = kNegInf;
+          srow[e] = kEndRow;
+        }
+        armi::lds_sort_approx_desc(skey, srow, n2);
+        __syncthreads();
+        for (int e = k + tid; e < kBestPad; e += 256) {
+          skey[e] = kNegInf;
+          srow[e] = kEndRow;
+        }
+        __syncthreads();
+      }
+    }
+    // this slice's top k into the query's list, then the last helper merges the slices
+    for (int c = tid; c < k; c += 256) {
+      coll_key[(size_t)ql * kCollectCap + h * k + c] = skey[c];
+      coll_row[(size_t)ql * kCollectCap + h * k + c] = srow[c];
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) sh[2] = atomicAdd(help_done + ql, 1) == n_help - 1;
+    __syncthreads();
+    if (sh[2]) {
+      __threadfence();
+      const int m = n_help * k;
+      const int n2 = armi::pow2_at_least(max(m, 2));
+      for (int e = tid; e < n2; e += 256) {
+        skey[e] = e < m ? coll_key[(size_t)ql * kCollectCap + e] : kNegInf;
+        srow[e] = e < m ? coll_row[(size_t)ql * kCollectCap + e] : kEndRow;
+      }
+      armi::lds_sort_approx_desc(skey, srow, n2);
+      __syncthreads();
+      write_out(ql);
+    }
   }
 }
 
@@ -1186,7 +1383,7 @@ struct Workspace {
   int32_t* cand_row;
   float* cand_bound;
   float* kth;
-  int* coll_count;
+  int* coll_count;  // [2 * kQB]: collect counts, then the helpers' done counters
   float* coll_key;
   int32_t* coll_row;
   size_t bytes;
@@ -1207,7 +1404,7 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   w.cand_row = cv.take<int32_t>(nr * kQB * kKW);
   w.cand_bound = cv.take<float>(nr * kQB);
   w.kth = cv.take<float>(kQB);
-  w.coll_count = cv.take<int>(kQB);
+  w.coll_count = cv.take<int>(2 * kQB);
   w.coll_key = cv.take<float>((size_t)kQB * kCollectCap);
   w.coll_row = cv.take<int32_t>((size_t)kQB * kCollectCap);
   w.bytes = cv.off + 256;
@@ -1493,26 +1690,14 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
 #else
   constexpr int dbg = 0;
 #endif
-  const size_t lds_collect = (size_t)kCollectCap * 8;
-  // dynamic-LDS limits raised once (no runtime calls but stream work per search: graph-capturable)
-  static const hipError_t raised = [&] {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_collect_merge_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_collect);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepLds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(pass_terms_bitmap_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPrepBmLds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(sparse_scan_kernel<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLds);
-    return e;
-  }();
-  ARMI_HIP(raised);
+  // dynamic-LDS limits raised once per device (no runtime calls but stream work per search:
+  // graph-capturable)
+  if (int rc = armi::allow_lds(sparse_collect_merge_kernel, kCollectLds)) return rc;
+  if (int rc = armi::allow_lds(pass_terms_kernel, kPrepLds)) return rc;
+  if (int rc = armi::allow_lds(pass_terms_bitmap_kernel, kPrepBmLds)) return rc;
+  if (int rc = armi::allow_lds(sparse_scan_kernel<false>, kScanLds)) return rc;
+  if (int rc = armi::allow_lds(sparse_scan_kernel<true>, kScanLds)) return rc;
+  const int n_help = std::max(1, std::min(kMaxHelp, kCollectCap / k));
   for (int q0 = 0; q0 < n_queries; q0 += kQB) {
     const int nqp = std::min(kQB, n_queries - q0);
     uint32_t* pflags = out_flags + q0;
@@ -1522,7 +1707,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       ARMI_HIP(hipMemsetAsync(out_ids + (size_t)q0 * k, 0xff, sizeof(int64_t) * nqp * k, stream));
       continue;
     }
-    ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * kQB, stream));
+    ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * 2 * kQB, stream));
     if (idx->vocab <= kBitmapVocab)
       pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
@@ -1573,9 +1758,12 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg,
         idx->dense_of, idx->dense_val, idx->dense_stride);
     ARMI_LAUNCHED("sparse_collect_kernel");
-    sparse_collect_merge_kernel<<<dim3(nqp), dim3(256), lds_collect, stream>>>(
-        w.coll_count, w.coll_key, w.coll_row, q0, k, idx->ordinal_base, out_scores, out_ids,
-        out_count, pflags);
+    sparse_collect_merge_kernel<<<dim3(nqp + n_help), dim3(256), kCollectLds, stream>>>(
+        w.coll_count, w.coll_key, w.coll_row, w.coll_count + kQB, nqp, q0,
+        k, idx->ordinal_base, idx->n_rows, row_mask, idx->term_ptr,
+        reinterpret_cast<const int2*>(idx->post), idx->dense_of, idx->dense_val,
+        idx->dense_stride, w.uterm, w.ql, w.qu, w.qcount, w.qof, out_scores, out_ids, out_count,
+        pflags);
     ARMI_LAUNCHED("sparse_collect_merge_kernel");
   }
   return ARMI_OK;

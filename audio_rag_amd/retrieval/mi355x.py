@@ -10,6 +10,8 @@ falls back to the CPU. search_batch() is the batched device API the pipeline and
 
 from __future__ import annotations
 
+import hashlib
+import json
 import logging
 import threading
 from dataclasses import dataclass
@@ -324,14 +326,14 @@ class MI355XRetriever(BaseRetriever):
         mode = self._mode(coll, search_type, queries.has_sparse)
         mask = coll.filter_mask(filter_metadata)
         if self._world > 1:
-            return self._search_sharded(coll, queries, top_k, mode, mask), mode
+            return self._search_sharded(coll, queries, top_k, mode, mask, filter_metadata), mode
         return self._search_device(coll, queries, top_k, mode, mask), mode
 
     def _search_sharded(self, coll: ChunkCollection, queries: QueryBatch, top_k: int, mode: str,
-                        mask: torch.Tensor | None) -> TopK:
+                        mask: torch.Tensor | None, mask_spec: dict | None = None) -> TopK:
         """search_batch over the corpus sharded across the process group (num_gpus > 1), a
-        COLLECTIVE call: every rank calls it with its own B queries (B equal on every rank) and
-        the same top_k, branch and filter, and gets the global top-k of its own queries.
+        COLLECTIVE call: every rank calls it with its own queries (any batch size, any branch)
+        and the same top_k, collection and filter, and gets the global top-k of its own queries.
         retrieval/shards.ShardedSearch: one RCCL all-gather of all ranks' queries, the local
         kernels over this rank's shard for all of them, one all-gather of the per-shard lists,
         the merge of this rank's queries (armi_topk_merge_shards_packed), RRF after the merge
@@ -347,11 +349,16 @@ class MI355XRetriever(BaseRetriever):
                            rrf=lambda a, b, k: rrf_fuse(a, b, k, rrf_k=self.config.rrf_k),
                            merge_packed=merge_shards_packed)
         csr = (queries.sparse_indptr, queries.sparse_indices, queries.sparse_values)
-        if mode == "hybrid":
-            return sh.hybrid(queries.dense, csr, top_k)
-        if mode == "sparse":
-            return sh.sparse(csr, top_k)
-        return sh.dense(queries.dense, top_k)
+        # the ranks agree on top_k and on collection + filter through the call's header (a
+        # mismatch raises on every rank); batch sizes and branches may differ
+        key = json.dumps([coll.name, coll.count, coll.hybrid, mask_spec or {}],
+                         sort_keys=True, default=str)
+        digest = int.from_bytes(hashlib.sha256(key.encode()).digest()[:8], "little")
+        try:
+            return sh.search(queries.dense, csr if queries.has_sparse else None, mode, top_k,
+                             digest)
+        except ValueError as e:
+            raise RetrievalError(str(e))
 
     def _search_device(self, coll: ChunkCollection, queries: QueryBatch, top_k: int, mode: str,
                        mask: torch.Tensor | None) -> TopK:
@@ -378,8 +385,10 @@ class MI355XRetriever(BaseRetriever):
         parts = [query_sparse_arrays(q.sparse) for q in query_embeddings]
         indptr = np.zeros(len(parts) + 1, dtype=np.int32)
         np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
-        idx = np.concatenate([p[0] for p in parts]).astype(np.int32)
-        val = np.concatenate([p[1] for p in parts]).astype(np.float32)
+        # one unused entry past indptr[-1] keeps the term arrays' device pointers non-null when
+        # every query is an empty SparseVector (the C ABI refuses null arrays)
+        idx = np.concatenate([p[0] for p in parts] + [np.zeros(1, np.int32)]).astype(np.int32)
+        val = np.concatenate([p[1] for p in parts] + [np.zeros(1, np.float32)]).astype(np.float32)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
         return QueryBatch(dense=dense, sparse_indptr=t(indptr), sparse_indices=t(idx),
                           sparse_values=t(val))

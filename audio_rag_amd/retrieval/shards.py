@@ -237,6 +237,63 @@ class ShardedSearch:
         d, s = self._exchange([d, s], 2 * k, nb)
         return self.rrf(d, s, k)
 
+    # ------------------------------------------------------- plugin call (mixed branches)
+
+    def search(self, q_local: torch.Tensor, q_local_csr, mode: str, k: int,
+               digest: int = 0) -> TopK:
+        """One collective search_batch call of MI355XRetriever (num_gpus > 1). Unlike the
+        dense / sparse / hybrid steps above (the bench's lockstep batches), the ranks' calls may
+        differ in batch size and branch: the reference's search() is an independent per-call
+        operation (retrieval/qdrant.py:227-352, branch chosen per call at 272-332), so a rank
+        whose query has no lexical weights (sparse=None: dense) can meet one that searches
+        hybrid. A fixed-size header is all-gathered first (batch size, top_k, branch, the
+        caller's digest of collection + filter, whether the rank can search sparse); every rank
+        reads the same header, so a top_k or filter disagreement raises ValueError on every
+        rank alike instead of leaving some ranks waiting in a collective. Then the queries
+        (padded to the largest batch; term slots always present when any rank needs them) and
+        both candidate lists travel in one all-gather each, and each rank takes its own branch's
+        answer: the dense or sparse merged list, or RRF of the two (lists of 2k when any rank
+        fuses; the first k of a merged 2k list are the global top k).
+        mode: "dense" (or "legacy_dense"), "sparse" or "hybrid"; q_local_csr may be None for
+        dense."""
+        code = {"dense": 0, "legacy_dense": 0, "sparse": 1, "hybrid": 2}[mode]
+        nb = int(q_local.shape[0])
+        dev = q_local.device
+        hdr = torch.tensor([nb, k, code, int(digest) & ((1 << 62) - 1),
+                            int(self.local_sparse is not None)], dtype=torch.int64, device=dev)
+        h = self._gather(hdr).cpu()                        # [G, 5], identical on every rank
+        if not bool((h[:, 1] == k).all()):
+            raise ValueError(f"sharded search: top_k differs across ranks ({h[:, 1].tolist()})")
+        if not bool((h[:, 3] == h[0, 3]).all()):
+            raise ValueError("sharded search: collection or filter differs across ranks")
+        codes = set(h[:, 2].tolist())
+        need_sparse = bool(codes & {1, 2})
+        if need_sparse and not bool(h[:, 4].all()):
+            raise ValueError("sharded search: a rank's collection has no sparse vectors")
+        nb_max = int(h[:, 0].max())
+        if nb_max == 0:
+            return _head(None, 0, k, dev)
+        q_pad = _pad_rows(q_local, nb_max)
+        csr = None
+        if need_sparse:
+            csr = q_local_csr if q_local_csr is not None and code != 0 else _empty_csr(nb, dev)
+            csr = _pad_csr_rows(csr, nb_max)
+        if codes == {0}:
+            out = self.dense(q_pad, k)
+        elif codes == {1}:
+            out = self.sparse(csr, k)
+        elif codes == {2}:
+            out = self.hybrid(q_pad, csr, k)
+        else:
+            kl = 2 * k if 2 in codes else k
+            # two or more branches: some rank needs sparse lists and some dense ones
+            all_q, all_csr = self._gather_queries(q_pad, csr)
+            d, s = self._local_pair(all_q, all_csr, kl)
+            d, s = self._exchange([d, s], kl, nb_max)
+            out = (_head(d, nb_max, k) if code == 0 else _head(s, nb_max, k) if code == 1
+                   else self.rrf(d, s, k))
+        return _head(out, nb, k) if nb != nb_max else out
+
     def _local_pair(self, all_q, all_csr, k: int) -> tuple[TopK, TopK]:
         if not all_q.is_cuda:
             return self.local_dense(all_q, k), self.local_sparse(all_csr, k)
@@ -253,3 +310,45 @@ class ShardedSearch:
         for t in s.tensors():
             t.record_stream(main)
         return d, s
+
+
+def _head(t: TopK | None, n: int, k: int, dev=None) -> TopK:
+    """The first n queries and first k entries of a merged list (None: an empty answer)."""
+    if t is None:
+        return TopK(scores=torch.empty((0, k), dtype=torch.float32, device=dev),
+                    ids=torch.empty((0, k), dtype=torch.int64, device=dev),
+                    rank=torch.empty((0, k), dtype=torch.float64, device=dev),
+                    count=torch.empty(0, dtype=torch.int32, device=dev))
+    rank = t.rank
+    return TopK(scores=t.scores[:n, :k].contiguous(), ids=t.ids[:n, :k].contiguous(),
+                rank=None if rank is None else rank[:n, :k].contiguous(),
+                count=t.count[:n].clamp(max=k).to(torch.int32))
+
+
+def _pad_rows(q: torch.Tensor, n: int) -> torch.Tensor:
+    """q [nb, dim] -> [n, dim]: padding rows copy row 0 (zeros for an empty batch), so padded
+    queries cost what a real one does; their answers are sliced away."""
+    nb = int(q.shape[0])
+    if nb == n:
+        return q
+    fill = q[:1].expand(n - nb, -1) if nb else torch.zeros((n, q.shape[1]), dtype=q.dtype,
+                                                                device=q.device)[nb:]
+    return torch.cat([q, fill], dim=0).contiguous()
+
+
+def _empty_csr(n: int, dev) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """n queries without terms (a dense-branch rank's part of a gathered sparse batch); the term
+    arrays hold one unused entry so their device pointers are never null."""
+    return (torch.zeros(n + 1, dtype=torch.int32, device=dev),
+            torch.zeros(1, dtype=torch.int32, device=dev),
+            torch.zeros(1, dtype=torch.float32, device=dev))
+
+
+def _pad_csr_rows(csr, n: int):
+    """A query CSR of nb rows -> n rows (the extra rows empty)."""
+    indptr, idx, val = csr
+    nb = int(indptr.numel()) - 1
+    if nb == n:
+        return csr
+    tail = indptr[-1:].expand(n - nb).to(indptr.dtype)
+    return torch.cat([indptr, tail]).contiguous(), idx, val

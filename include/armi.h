@@ -51,7 +51,11 @@ extern "C" {
 #define ARMI_ERR_HIP 2         /* a HIP runtime call failed */
 #define ARMI_ERR_UNSUPPORTED 3 /* valid request that this build does not implement */
 
-#define ARMI_ABI_VERSION 1
+/* ABI history. 1: rounds 1-3. 2 (round 5): armi_enc_cls_head_sigmoid takes the dense weight
+ * transposed ([in][out], was [out][in]); armi_dense_topk_ex / _first / _second_pass,
+ * armi_index_set_scan_cus and armi_cu_split_streams removed. A caller built against version 1
+ * must not bind this library (armi_abi_version() tells). */
+#define ARMI_ABI_VERSION 2
 
 /* flags written per query by the top-k entry points */
 #define ARMI_FLAG_CERTIFIED 1u /* fast path proved its top-k equal to the exact ranking */
@@ -268,9 +272,11 @@ size_t armi_sparse_workspace_bytes(const armi_sparse_index* index, int n_queries
  * q_indices ascending int32 (at most 256 per query: a longer query is scored on its first 256
  * terms and gets flag bit 8; the Python layer refuses such queries before the call), q_values float.
  * out_flags: ARMI_FLAG_CERTIFIED (merged lists proved exact) or ARMI_FLAG_FALLBACK (answer from
- * the collecting rescan; bit 4 = more than 4096 rows tied at the threshold, answer truncated). score = sum over shared indices, ascending index order, of
- * fl32(q*d) accumulated in fp32 (mul and add rounded separately). Only rows that share at
- * least one index with the query are results. Ranking (score desc, ordinal asc). */
+ * the collecting rescan, or, when more than 4096 rows reach its threshold, from an exact
+ * term-at-a-time rescoring of the shard by helper workgroups: exact either way). score = sum
+ * over shared indices, ascending index order, of fl32(q*d) accumulated in fp32 (mul and add
+ * rounded separately). Only rows that share at least one index with the query are results.
+ * Ranking (score desc, ordinal asc). */
 int armi_sparse_topk(const armi_sparse_index* index, const int32_t* q_indptr,
                      const int32_t* q_indices, const float* q_values, int n_queries, int k,
                      const uint64_t* row_mask, float* out_scores, int64_t* out_ids,

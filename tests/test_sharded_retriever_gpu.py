@@ -76,6 +76,30 @@ def _worker(rank, world, port, out_dir):
         out[key + "_ids"] = np.array([[int(r.chunk.text.split()[1]) for r in rs] + [-1] * (K - len(rs))
                                       for rs in res])
         out[key + "_sc"] = np.array([[r.score for r in rs] + [0.0] * (K - len(rs)) for rs in res])
+    # mixed branches and batch sizes across ranks in one collective call (qdrant.py:272-332
+    # chooses the branch per call): even ranks fuse / search sparse, odd ranks bring queries
+    # without lexical weights (dense) or with empty SparseVectors (hybrid of the dense list alone)
+    empty = ret.to_query_batch([EmbeddingResult(dense=e.dense, sparse=SparseVector([], []))
+                                for e in embs[:2]])
+    for name, (st, qb) in (("mixA", ("hybrid", batch) if rank % 2 == 0 else
+                            ("hybrid", ret.to_query_batch([EmbeddingResult(dense=e.dense)
+                                                            for e in embs[:B - 3]]))),
+                           ("mixB", ("sparse", batch) if rank % 2 == 0 else ("hybrid", empty))):
+        tk, mode = ret.search_batch(qb, K, None, None, st)
+        out[name + "_mode"] = np.array(mode)
+        res = ret.materialize_batch(tk, mode, coll.name)
+        out[name + "_ids"] = [[int(r.chunk.text.split()[1]) for r in rs] for rs in res]
+        out[name + "_sc"] = [[r.score for r in rs] for rs in res]
+        out[name + "_ids"] = np.array([x + [-1] * (K - len(x)) for x in out[name + "_ids"]])
+        out[name + "_sc"] = np.array([x + [0.0] * (K - len(x)) for x in out[name + "_sc"]])
+    # a top_k disagreement raises RetrievalError on every rank instead of hanging
+    from audio_rag_amd.core.exceptions import RetrievalError
+
+    try:
+        ret.search_batch(dense_only, K + rank, None, None, "dense")
+        out["raised"] = np.array(0)
+    except RetrievalError:
+        out["raised"] = np.array(1)
     # search() one query per rank (collective), then the rank-local rerank of its own slice
     rr = BGEReranker(RerankingConfig(top_k=3), device=torch.device("cuda", 0), arch=RR_ARCH)
     rr.load()
@@ -139,6 +163,22 @@ def test_sharded_retriever_plugin_equals_global(tmp_path, oracle_mod, world):
                 ids, sc = want(st, flt, r * B + q)
                 assert list(z[key + "_ids"][q, :len(ids)]) == [int(x) for x in ids], (r, key, q)
                 assert [float(x) for x in z[key + "_sc"][q, :len(sc)]] == [float(x) for x in sc]
+        assert int(z["raised"]) == 1, r
+        for name in ("mixA", "mixB"):
+            mode = str(z[name + "_mode"])
+            nq = z[name + "_ids"].shape[0]
+            want_mode = {("mixA", 0): "hybrid", ("mixA", 1): "dense", ("mixB", 0): "sparse",
+                         ("mixB", 1): "hybrid"}[(name, r % 2)]
+            assert mode == want_mode and nq == {("mixA", 1): B - 3, ("mixB", 1): 2}.get((name, r % 2), B)
+            for q in range(nq):
+                if name == "mixB" and r % 2:  # empty SparseVector: RRF of the dense 2k list alone
+                    d = o.dense_topk(rows, qd[r * B + q:r * B + q + 1], 2 * K)
+                    f = o.rrf([list(d.ids[0, :d.count[0]]), []], K)
+                    ids, sc = [p for p, _ in f], [v for _, v in f]
+                else:
+                    ids, sc = want(mode, None, r * B + q)
+                assert list(z[name + "_ids"][q, :len(ids)]) == [int(x) for x in ids], (r, name, q)
+                assert [float(x) for x in z[name + "_sc"][q, :len(sc)]] == [float(x) for x in sc]
         ids, _ = want("hybrid", None, r * B)
         assert list(z["single_ids"]) == [int(x) for x in ids]
         # rank-local rerank of its own slice vs transformers fp32 (bge.py:119-123)

@@ -136,6 +136,130 @@ def test_two_rank_sharded_search_equals_global(tmp_path, oracle_mod):
             assert [float(x) for x in z["h_sc"][q, :len(want)]] == [v for _, v in want]
 
 
+def _mixed_worker(rank, world, port, out_dir):
+    """Each rank brings its own batch size and branch to ShardedSearch.search (the plugin's
+    collective call): rank 0 / 1 / ... alternate over the cases below."""
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audio_rag_amd.retrieval.shards import ShardedSearch, shard_range
+    from oracle import oracle as o
+
+    rows = o.unit_fp16(N, DIM, seed=3)
+    csr = o.sparse_corpus(N, seed=4)
+    lo, hi = shard_range(N, rank, world)
+    shard_csr = (csr[0][lo:hi + 1] - csr[0][lo], csr[1][csr[0][lo]:csr[0][hi]], csr[2][csr[0][lo]:csr[0][hi]])
+
+    def local_dense(q, k):
+        r = o.dense_topk(rows[lo:hi], q.numpy().view(np.uint16), k, ordinal_base=lo)
+        return _topk_t(r.ids, r.scores, r.rank, r.count)
+
+    def local_sparse(qcsr, k):
+        qi, qx, qv = (t.numpy() for t in qcsr)
+        r = o.sparse_topk(*shard_csr, qi, qx, qv, k, ordinal_base=lo)
+        return _topk_t(r.ids, r.scores, r.scores.astype(np.float64), r.count)
+
+    def merge(rank_, scores, ids, count, k):
+        return cpu_merge(rank_.numpy(), scores.numpy(), ids.numpy(), count.numpy(), k)
+
+    def rrf(d, s, k):
+        b = d.ids.shape[0]
+        ids = np.full((b, k), -1, np.int64)
+        sc = np.zeros((b, k), np.float64)
+        cnt = np.zeros(b, np.int32)
+        for q in range(b):
+            f = o.rrf([list(d.ids[q, :d.count[q]].tolist()), list(s.ids[q, :s.count[q]].tolist())], k)
+            cnt[q] = len(f)
+            for j, (p, v) in enumerate(f):
+                ids[q, j], sc[q, j] = p, v
+        return _topk_t(ids, sc.astype(np.float32), sc, cnt)
+
+    ss = ShardedSearch(local_dense, merge, local_sparse=local_sparse, rrf=rrf)
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    qi, qx, qv = o.sparse_queries(B * world, seed=6)
+    out = {}
+    for case, plan in enumerate(MIXED_CASES):
+        mode, nb, empty_terms = plan[rank % len(plan)]
+        g0 = rank * B
+        q_mine = torch.from_numpy(q_all[g0:g0 + nb].view(np.float16).copy())
+        q_csr = None
+        if mode != "dense":
+            a, b = qi[g0], qi[g0 + nb]
+            ip = qi[g0:g0 + nb + 1] - a
+            if empty_terms:  # every query an empty SparseVector: hybrid of the dense list alone
+                ip = np.zeros_like(ip)
+            q_csr = (torch.from_numpy(ip), torch.from_numpy(qx[a:b] if b > a else qx[:1]),
+                     torch.from_numpy(qv[a:b] if b > a else qv[:1]))
+        t = ss.search(q_mine, q_csr, mode, K, digest=7)
+        out[f"c{case}_ids"] = t.ids.numpy()
+        out[f"c{case}_sc"] = t.rank.numpy()
+        out[f"c{case}_cnt"] = t.count.numpy()
+    # disagreements raise on every rank (no rank left waiting in a collective)
+    for kk, dg in ((K + rank, 7), (K, 7 + rank)):
+        try:
+            ss.search(torch.from_numpy(q_all[:2].view(np.float16).copy()), None, "dense", kk, dg)
+            out["raised"] = out.get("raised", 0)
+        except ValueError:
+            out["raised"] = out.get("raised", 0) + 1
+    t = ss.search(torch.from_numpy(q_all[:2].view(np.float16).copy()), None, "dense", K, 7)
+    out["after_ids"] = t.ids.numpy()
+    np.savez(Path(out_dir) / f"mixed{rank}.npz", **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+# per case: (branch, batch size, empty term lists) of rank 0, rank 1 (ranks cycle over the list)
+MIXED_CASES = [
+    [("hybrid", B, False), ("dense", B - 2, False)],
+    [("sparse", 2, False), ("hybrid", B, True)],
+    [("dense", B, False), ("sparse", B - 1, False)],
+    [("hybrid", 0, False), ("hybrid", 3, False)],
+]
+
+
+def test_two_rank_mixed_branches_and_sizes(tmp_path, oracle_mod):
+    """The plugin's collective call with different branches / batch sizes per rank (a rank whose
+    query has sparse=None searches dense while another fuses): every rank gets the global answer
+    of its own branch; a top_k or filter disagreement raises on both ranks, and the group stays
+    usable afterwards."""
+    world = 2
+    mp.spawn(_mixed_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    o = oracle_mod
+    rows = o.unit_fp16(N, DIM, seed=3)
+    csr = o.sparse_corpus(N, seed=4)
+    q_all = o.unit_fp16(B * world, DIM, seed=5)
+    qi, qx, qv = o.sparse_queries(B * world, seed=6)
+
+    def want(mode, g, empty):
+        one = (np.array([0, 0 if empty else qi[g + 1] - qi[g]], np.int32), qx[qi[g]:qi[g + 1]],
+               qv[qi[g]:qi[g + 1]])
+        if mode == "dense":
+            d = o.dense_topk(rows, q_all[g:g + 1], K)
+            return list(d.ids[0, :d.count[0]]), list(d.rank[0, :d.count[0]])
+        if mode == "sparse":
+            s = o.sparse_topk(*csr, *one, K)
+            return list(s.ids[0, :s.count[0]]), [float(x) for x in s.scores[0, :s.count[0]]]
+        d = o.dense_topk(rows, q_all[g:g + 1], 2 * K)
+        s = o.sparse_topk(*csr, *one, 2 * K)
+        f = o.rrf([list(d.ids[0, :d.count[0]]), list(s.ids[0, :s.count[0]])], K)
+        return [p for p, _ in f], [v for _, v in f]
+
+    for r in range(world):
+        z = np.load(tmp_path / f"mixed{r}.npz")
+        assert int(z["raised"]) == 2, r
+        gd = o.dense_topk(rows, q_all[:2], K)
+        np.testing.assert_array_equal(z["after_ids"], gd.ids)
+        for case, plan in enumerate(MIXED_CASES):
+            mode, nb, empty = plan[r % len(plan)]
+            assert z[f"c{case}_ids"].shape == (nb, K), (r, case)
+            for q in range(nb):
+                ids, sc = want(mode, r * B + q, empty)
+                c = int(z[f"c{case}_cnt"][q])
+                assert c == len(ids), (r, case, q)
+                assert [int(x) for x in z[f"c{case}_ids"][q, :c]] == [int(x) for x in ids], (r, case, q)
+                assert [float(x) for x in z[f"c{case}_sc"][q, :c]] == [float(x) for x in sc], (r, case, q)
+
+
 def test_pad_unpad_csr_roundtrip():
     """The fixed-slot query layout of the one-collective query exchange: ragged, empty and
     full (MAX_QUERY_TERMS) queries survive pad -> unpad with the CSR order intact."""

@@ -202,3 +202,75 @@ def test_sparse_pass_term_numbering_paths(gpu, oracle_mod, vocab):
     for k in (3, 20):
         want = oracle_mod.sparse_topk(indptr, indices, values, qi, qx, qv, k, ordinal_base=5)
         _same(_run(idx, (qi, qx, qv), k, gpu), want)
+
+
+def _overflow_corpus(n=200_000, pile=6000, t_rows=5000, seed=81):
+    """n rows of 8 stratified terms (ascending, < 50 000) with U(0.01, 0.40) values; even rows
+    also hold term 60 000 (a dense value column: present in half the rows); rows [0, t_rows) hold
+    term 70 000 with a value from {0.1, 0.2, 0.3} (many ties); rows 0, 20, 40, ... (pile of them)
+    copy row 0's first nine entries exactly (a pile of re-uploaded identical chunks)."""
+    rng = np.random.default_rng(seed)
+    base = (rng.integers(0, 6250, size=(n, 8)) + 6250 * np.arange(8)).astype(np.int32)
+    bval = rng.uniform(0.01, 0.40, size=(n, 8)).astype(np.float32)
+    even = (np.arange(n) % 2 == 0)
+    tee = np.arange(n) < t_rows
+    p_rows = np.arange(pile) * 20
+    base[p_rows] = base[0]
+    bval[p_rows] = bval[0]
+    dval = rng.uniform(0.01, 0.40, size=n).astype(np.float32)
+    dval[p_rows] = dval[0]
+    tval = rng.choice(np.array([0.1, 0.2, 0.3], np.float32), size=n)
+    lens = 8 + even.astype(np.int64) + tee.astype(np.int64)
+    indptr = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    indices = np.empty(indptr[-1], np.int32)
+    values = np.empty(indptr[-1], np.float32)
+    cols = np.arange(8)
+    pos = indptr[:-1, None] + cols
+    indices[pos.ravel()] = base.ravel()
+    values[pos.ravel()] = bval.ravel()
+    e = np.nonzero(even)[0]
+    indices[indptr[e] + 8] = 60000
+    values[indptr[e] + 8] = dval[e]
+    t = np.nonzero(tee)[0]
+    at = indptr[t] + 8 + even[t].astype(np.int64)
+    indices[at] = 70000
+    values[at] = tval[t]
+    return (indptr, indices, values), p_rows
+
+
+def test_sparse_collect_overflow_is_exact(gpu, oracle_mod):
+    """More than kCollectCap = 4096 rows reach the collect threshold: (a) a pile of 6 000
+    identical rows tying at the top (the k-th candidate's score is the pile's), (b) a query whose
+    one term lies in rows [0, 5 000) only, so at k = 240 the merge pools fewer than k candidates
+    (threshold -inf: every overlapping row is collected). The helper workgroups of the collect
+    merge must answer both exactly (ids by ascending ordinal among ties), filtered and not."""
+    csr, p_rows = _overflow_corpus()
+    indptr, indices, values = csr
+    rng = np.random.default_rng(82)
+    r0 = slice(indptr[0], indptr[0] + 9)  # row 0: 8 base terms + the dense-column term
+    pile_q = (indices[r0], rng.uniform(0.05, 0.35, 9).astype(np.float32))
+    tee_q = (np.array([70000], np.int32), np.array([0.3], np.float32))
+    mixed = oracle_mod.sparse_queries(6, seed=83)
+    parts = [pile_q, tee_q] + [(mixed[1][mixed[0][i]:mixed[0][i + 1]],
+                                mixed[2][mixed[0][i]:mixed[0][i + 1]]) for i in range(6)]
+    qi = np.zeros(len(parts) + 1, np.int32)
+    np.cumsum([len(p[0]) for p in parts], out=qi[1:])
+    q = (qi, np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    idx = _sparse_index(csr, gpu, base=11)
+    n = indptr.size - 1
+    mask = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for r in np.nonzero(rng.random(n) < 0.5)[0]:
+        mask[r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    for k in (5, 40, 240):
+        for m in (None, mask):
+            got = _run(idx, q, k, gpu, mask=m)
+            _same(got, oracle_mod.sparse_topk(*csr, *q, k, row_mask=m, ordinal_base=11))
+            assert not (got["flags"] & 4).any(), got["flags"]
+            # the pile query always needs the overflow path
+            assert got["flags"][0] & 2, got["flags"]
+            if m is None:
+                np.testing.assert_array_equal(got["ids"][0, :k], p_rows[:k] + 11)
+    # the -inf threshold case: 5 000 overlapping rows in <= 7 ranges pool < 240 candidates
+    got = _run(idx, q, 240, gpu)
+    assert got["flags"][1] & 2 and got["count"][1] == 240
