@@ -94,6 +94,9 @@ SIGNATURES: dict[str, tuple] = {
     "armi_enc_bias_gelu": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "armi_enc_embed": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p]),
+    "armi_enc_embed_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                   c_void_p]),
     "armi_enc_cls_head_sigmoid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_int, c_int, c_int, c_void_p]),
     "armi_enc_attention_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

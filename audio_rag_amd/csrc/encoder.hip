@@ -125,10 +125,13 @@ __global__ __launch_bounds__(256) void bias_gelu_kernel(float* __restrict__ x,
 
 // XLM-R embeddings (transformers create_position_ids_from_input_ids): position id of token t is
 // padding_idx + number of non-pad tokens in [0, t] for a non-pad token, padding_idx for a pad.
+// T = float (fp32 tables) or _Float16 (the fp16 model's own tables, no fp32 copy; the sums are
+// the same fp32 operations on the same values)
+template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
-                                                    const float* __restrict__ word,
-                                                    const float* __restrict__ pos,
-                                                    const float* __restrict__ type0,
+                                                    const T* __restrict__ word,
+                                                    const T* __restrict__ pos,
+                                                    const T* __restrict__ type0,
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta,
                                                     float* __restrict__ out, int n_seq, int L,
@@ -150,14 +153,14 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
   int pid = (id != pad_id) ? pad_id + count : pad_id;
   if (id < 0 || id >= vocab) id = 3;  // <unk>
   pid = pid < n_pos ? pid : n_pos - 1;
-  const float* w = word + (int64_t)id * width;
-  const float* pp = pos + (int64_t)pid * width;
+  const T* w = word + (int64_t)id * width;
+  const T* pp = pos + (int64_t)pid * width;
   float v[kMaxPerLane];
 #pragma unroll
   for (int i = 0; i < kMaxPerLane; ++i) {
     const int c = lane + 64 * i;
     v[i] = 0.f;
-    if (c < width) v[i] = w[c] + pp[c] + type0[c];
+    if (c < width) v[i] = (float)w[c] + (float)pp[c] + (float)type0[c];
   }
   layernorm_row(v, width, lane, gamma, beta, eps, out + tok * width);
 }
@@ -284,8 +287,28 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
   ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
                "embed: null pointer argument");
   const int64_t toks = (int64_t)n_seq * L;
-  embed_kernel<<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
+  embed_kernel<float><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
       ids, word, pos, type0, gamma, beta, out, n_seq, L, width, pad_id, vocab, n_pos, eps);
+  ARMI_LAUNCHED("embed_kernel");
+  return ARMI_OK;
+}
+
+int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t* pos,
+                       const uint16_t* type0, const float* gamma, const float* beta, float* out,
+                       int n_seq, int L, int width, int pad_id, int vocab, int n_pos, float eps,
+                       hipStream_t stream) {
+  ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane, "embed_f16: width must be in [1, 1024]");
+  ARMI_REQUIRE(vocab > 3 && n_pos > pad_id + 1 && pad_id >= 0,
+               "embed_f16: bad vocab / n_pos / pad_id");
+  ARMI_REQUIRE(L >= 1, "embed_f16: L must be >= 1");
+  if (n_seq <= 0) return ARMI_OK;
+  ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
+               "embed_f16: null pointer argument");
+  const int64_t toks = (int64_t)n_seq * L;
+  embed_kernel<_Float16><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
+      ids, reinterpret_cast<const _Float16*>(word), reinterpret_cast<const _Float16*>(pos),
+      reinterpret_cast<const _Float16*>(type0), gamma, beta, out, n_seq, L, width, pad_id, vocab,
+      n_pos, eps);
   ARMI_LAUNCHED("embed_kernel");
   return ARMI_OK;
 }

@@ -358,18 +358,23 @@ __global__ __launch_bounds__(kThreads) void linear_f16_kernel(
 }
 
 
-// out[m][n] = epi(x . w^T + bias) for a few token rows (m <= 32: the batch-1 query encode of
-// BGE-M3, embeddings/xlmr_f16.py), where the GEMM is a weight stream: workgroup j owns output
-// columns 16j .. 16j + 15 and its WAVES waves split K evenly; each wave runs
-// v_mfma_f32_16x16x32_f16 over its slice with the weight rows read straight from HBM (lane l:
-// column l & 15, k 8 (l >> 4) .. + 7 of each 32-step, i.e. 16 contiguous bytes of the [n][k]
-// row), the token rows from L2; the partial tiles are summed in LDS in wave order (the same
-// result every run), then bias (+ exact GELU) and the fp16 store.
+// out[m][n] = epi(x . w^T + bias) for a few token rows (the query encodes of BGE-M3,
+// embeddings/xlmr_f16.py), where the GEMM is a weight stream: workgroup (j, b) owns output
+// columns 16j .. 16j + 15 of token rows 32b .. 32b + 31 and its WAVES waves split K evenly; each
+// wave runs v_mfma_f32_16x16x32_f16 over its slice with the weight rows read straight from HBM
+// (lane l: column l & 15, k 8 (l >> 4) .. + 7 of each 32-step, i.e. 16 contiguous bytes of the
+// [n][k] row), the token rows from L2; the partial tiles are summed in LDS in wave order (the
+// same result every run), then bias (+ exact GELU) and the fp16 store. A row's arithmetic
+// depends only on k (the wave split), never on m or on the other rows: a query encoded alone
+// and inside a batch gets the same bits (round 5: the batched query encode uses this too).
 template <int EPI, int STEPS, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void linear_small_m_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
     uint16_t* __restrict__ out, int m, int n, int k) {
   __shared__ float part[WAVES][2][16][17];  // [wave][row tile][row][col] (+1: bank spread)
+  x += (size_t)blockIdx.y * 32 * k;
+  out += (size_t)blockIdx.y * 32 * n;
+  m = min(m - 32 * (int)blockIdx.y, 32);
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
   const int n0 = blockIdx.x * 16;
@@ -459,7 +464,7 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
 int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float* bias,
                               uint16_t* out, int m, int n, int k, int epilogue,
                               hipStream_t stream) {
-  ARMI_REQUIRE(m >= 0 && m <= 32, "enc_linear_small_f16: m must be in [0, 32]");
+  ARMI_REQUIRE(m >= 0 && m <= 32 * 65535, "enc_linear_small_f16: m must be in [0, 32 * 65535]");
   ARMI_REQUIRE(n >= 16 && n % 16 == 0, "enc_linear_small_f16: n must be a multiple of 16");
   ARMI_REQUIRE(k >= 256 && k % 256 == 0 && (int64_t)n * k < (int64_t(1) << 31),
                "enc_linear_small_f16: k must be a multiple of 256 (n * k < 2^31)");
@@ -473,14 +478,14 @@ int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float*
   if (k == 4096 || k == 3072) {
     auto kern = k == 4096 ? (g ? linear_small_m_kernel<1, 8, 16> : linear_small_m_kernel<0, 8, 16>)
                           : (g ? linear_small_m_kernel<1, 6, 16> : linear_small_m_kernel<0, 6, 16>);
-    kern<<<dim3(n / 16), dim3(1024), 0, stream>>>(x, w, bias, out, m, n, k);
+    kern<<<dim3(n / 16, (m + 31) / 32), dim3(1024), 0, stream>>>(x, w, bias, out, m, n, k);
     ARMI_LAUNCHED("linear_small_m_kernel");
     return ARMI_OK;
   }
   auto kern = k == 1024 ? (g ? linear_small_m_kernel<1, 4, 8> : linear_small_m_kernel<0, 4, 8>)
               : k == 768  ? (g ? linear_small_m_kernel<1, 3, 8> : linear_small_m_kernel<0, 3, 8>)
                           : (g ? linear_small_m_kernel<1, 0, 8> : linear_small_m_kernel<0, 0, 8>);
-  kern<<<dim3(n / 16), dim3(512), 0, stream>>>(x, w, bias, out, m, n, k);
+  kern<<<dim3(n / 16, (m + 31) / 32), dim3(512), 0, stream>>>(x, w, bias, out, m, n, k);
   ARMI_LAUNCHED("linear_small_m_kernel");
   return ARMI_OK;
 }

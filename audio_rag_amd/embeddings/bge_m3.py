@@ -7,9 +7,16 @@ BGEM3FlagModel (flagembedding >= 1.3.5, not installed):
   * dense  = L2-normalised hidden state of <s> (fp16 values, bge.py:149 .tolist())
   * sparse = relu(Linear(1024 -> 1)(hidden)) per token, max per token id, special tokens and
     weights <= 0 dropped, keys in first-occurrence order (_convert_sparse, bge.py:95-102)
-Weights: BAAI/bge-m3 is not on disk and cannot be downloaded here; the encoder and the sparse
-head are initialised from EmbeddingConfig.seed (documented in DESIGN.md). Token ids come from
-audio_rag_amd.text (stand-in tokenizer) or are passed directly (embed_query_ids).
+Weights (load(), as BGEM3FlagModel(config.model) at bge.py:47-55): config.model naming a local
+checkpoint directory or a cached hub snapshot loads its model.safetensors (or a weights-only
+pytorch_model.bin), sparse_linear.pt and tokenizer.json (audio_rag_amd.checkpoints); otherwise
+the encoder and the sparse head are initialised from EmbeddingConfig.seed and token ids come from
+the stand-in tokenizer audio_rag_amd.text (BAAI/bge-m3 is not on disk here and cannot be
+downloaded; documented in DESIGN.md). Token ids can also be passed directly (encode_ids).
+
+Query encodes (embed_query, and embed_queries for QueryPipeline.query_batch) run on the armi
+kernels (embeddings/xlmr_f16.py), whose arithmetic is row-independent: a query gets the same
+vector alone and in a batch. embed() of corpus chunks runs transformers' fp16 forward.
 """
 
 from __future__ import annotations
@@ -19,6 +26,7 @@ import logging
 
 import torch
 
+from audio_rag_amd.checkpoints import tokenizer_for
 from audio_rag_amd.config.schema import EmbeddingConfig
 from audio_rag_amd.core.base import BaseEmbedder, EmbeddingResult, SparseVector
 from audio_rag_amd.core.exceptions import EmbeddingError
@@ -51,16 +59,43 @@ def build_bge_m3(seed: int, arch: dict | None = None):
     return model, sparse_linear
 
 
-def lexical_weights(token_weights: list[float], input_ids: list[int]) -> dict[int, float]:
+def lexical_weights(token_weights: list[float], input_ids: list[int],
+                    special_ids=SPECIAL_IDS) -> dict[int, float]:
     """FlagEmbedding's _process_token_weights: per token id the max weight, ids of special
-    tokens and weights <= 0 skipped, first-occurrence key order."""
+    tokens (cls, eos, pad, unk) and weights <= 0 skipped, first-occurrence key order."""
     result: dict[int, float] = {}
     for w, idx in zip(token_weights, input_ids):
-        if idx in SPECIAL_IDS or not w > 0:
+        if idx in special_ids or not w > 0:
             continue
         if w > result.get(idx, 0.0):
             result[idx] = w
     return result
+
+
+def load_bge_m3(name: str, seed: int, arch: dict | None = None):
+    """(encoder fp32 CPU, sparse head, tokenizer or None): the checkpoint config.model names when
+    it is on disk (a directory or a cached hub snapshot), else the seeded stand-in."""
+    from transformers import XLMRobertaModel
+
+    from audio_rag_amd.checkpoints import load_pretrained, load_tokenizer, resolve_local
+
+    path = resolve_local(name)
+    if path is None:
+        logger.warning(f"{name}: no local checkpoint; using seeded stand-in weights (seed {seed}) "
+                       "and the stand-in tokenizer")
+        model, sparse = build_bge_m3(seed, arch)
+        return model, sparse, None
+    model = load_pretrained(XLMRobertaModel, path, add_pooling_layer=False)
+    sparse = torch.nn.Linear(model.config.hidden_size, 1)
+    sp = path / "sparse_linear.pt"
+    if sp.exists():
+        sparse.load_state_dict(torch.load(str(sp), map_location="cpu", weights_only=True))
+    else:
+        logger.warning(f"{path}: no sparse_linear.pt; the sparse head is seeded (seed {seed})")
+        with torch.random.fork_rng():
+            torch.manual_seed(seed)
+            sparse = torch.nn.Linear(model.config.hidden_size, 1)
+    return model, sparse, load_tokenizer(path)
 
 
 @EmbeddingsRegistry.register("bge-m3")
@@ -76,7 +111,8 @@ class BGEM3Embedder(BaseEmbedder):
         self._sparse = None
         self._graphs: dict[int, tuple] = {}
         self._fast = None  # XLMREncoderF16 of the captured query encode (load())
-        self.tokenizer = HashTokenizer()
+        # the checkpoint's tokenizer.json when config.model is on disk, else the stand-in
+        self.tokenizer = tokenizer_for(config.model) or HashTokenizer()
         logger.info(f"BGEM3Embedder initialized: model={config.model}, device={self._device}, "
                     f"sparse={self._use_sparse}")
 
@@ -89,9 +125,11 @@ class BGEM3Embedder(BaseEmbedder):
         if self._model is not None:
             return
         try:
-            model, sparse = build_bge_m3(self.config.seed, self._arch)
+            logger.info(f"Loading {self.config.model} on {self._device}...")
+            model, sparse, _ = load_bge_m3(self.config.model, self.config.seed, self._arch)
             self._model = model.to(self._device, dtype=torch.float16)
             self._sparse = sparse.to(self._device, dtype=torch.float16)
+            self._dimension = model.config.hidden_size
         except Exception as e:
             raise EmbeddingError(f"Failed to load embedding model: {e}")
         self._fast = None
@@ -100,6 +138,7 @@ class BGEM3Embedder(BaseEmbedder):
 
             self._fast = XLMREncoderF16(self._model, self._sparse if self._use_sparse else None,
                                         self._device)
+        logger.info(f"BGE-M3 loaded (dim={self._dimension}, sparse={self._use_sparse})")
 
     def unload(self) -> None:
         if self._model is None:
@@ -141,7 +180,8 @@ class BGEM3Embedder(BaseEmbedder):
         lex = None
         if self._use_sparse:
             tw = torch.relu(self._sparse(hidden)).squeeze(-1).float().cpu().tolist()
-            lex = [lexical_weights(tw[i][: len(s)], s) for i, s in enumerate(seqs)]
+            sp = self.tokenizer.special_ids
+            lex = [lexical_weights(tw[i][: len(s)], s, sp) for i, s in enumerate(seqs)]
         return dense.contiguous(), lex
 
     # ------------------------------------------------------------- captured query encode
@@ -189,7 +229,7 @@ class BGEM3Embedder(BaseEmbedder):
         L = len(seq)
         bucket = next((b for b in self.GRAPH_BUCKETS if b >= L), None)
         if not self.config.query_graphs or bucket is None:
-            return self.encode_ids([seq])
+            return self.encode_query_batch([seq])
         graph, ids_t, mask_t, dense, tw = self._graph_for(bucket)
         ids_t.fill_(1)
         mask_t.zero_()
@@ -198,7 +238,7 @@ class BGEM3Embedder(BaseEmbedder):
         graph.replay()
         lex = None
         if self._use_sparse:
-            lex = [lexical_weights(tw[0, :L].cpu().tolist(), seq)]
+            lex = [lexical_weights(tw[0, :L].cpu().tolist(), seq, self.tokenizer.special_ids)]
         return dense.clone(), lex
 
     def _results(self, dense: torch.Tensor, lex) -> list[EmbeddingResult]:
@@ -246,6 +286,24 @@ class BGEM3Embedder(BaseEmbedder):
     @require_loaded
     def embed_queries(self, queries: list[str]):
         """Batched query encode for the batched pipeline: (dense fp16 [B, d] device, lexical
-        weights per query or None)."""
+        weights per query or None). On the armi query encoder (row-independent arithmetic), so
+        every query gets exactly the vector and weights embed_query gives it."""
         seqs = [self.tokenizer.encode(q, self.config.max_length) for q in queries]
-        return self.encode_ids(seqs)
+        return self.encode_query_batch(seqs)
+
+    @torch.inference_mode()
+    def encode_query_batch(self, seqs: list[list[int]]):
+        """encode_ids for queries: the armi query encoder when loaded on the GPU (the same bits
+        as encode_query_ids per sequence), else transformers' forward."""
+        if getattr(self, "_fast", None) is None or not seqs:
+            return self.encode_ids(seqs)
+        ids, mask = pad_batch(seqs)
+        ids_t = torch.tensor(ids, dtype=torch.int32, device=self._device)
+        mask_t = torch.tensor(mask, dtype=torch.int32, device=self._device)
+        dense, tw = self._fast.forward(ids_t, mask_t)
+        lex = None
+        if self._use_sparse:
+            rows = tw.cpu().tolist()
+            sp = self.tokenizer.special_ids
+            lex = [lexical_weights(rows[i][: len(s)], s, sp) for i, s in enumerate(seqs)]
+        return dense.contiguous(), lex

@@ -216,19 +216,32 @@ class QueryPipeline:
         try:
             retriever = self.retriever
             dense, lex = self.embedder.embed_queries(query_texts)
-            batch = QueryBatch(dense=dense)
-            if lex is not None and all(lex):
-                parts = [query_sparse_arrays(self.embedder._convert_sparse(x)) for x in lex]
-                indptr = np.zeros(len(parts) + 1, dtype=np.int32)
-                np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
-                t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(retriever.device)
-                batch = QueryBatch(dense=dense, sparse_indptr=t(indptr),
-                                   sparse_indices=t(np.concatenate([p[0] for p in parts])),
-                                   sparse_values=t(np.concatenate([p[1] for p in parts])))
             use_rerank = enable_reranking and self.reranker is not None
             k = self.config.reranking.initial_k if use_rerank else final_top_k
-            out, mode = retriever.search_batch(batch, k, resolved, filter_metadata, search_type)
-            per_query = [retriever.materialize(out, mode, resolved, b) for b in range(len(query_texts))]
+            # query() searches a query without lexical weights (_convert_sparse -> None) dense
+            # and the others with their sparse vector: one device batch per such group
+            has_lex = [bool(x) for x in lex] if lex is not None else [False] * len(query_texts)
+            per_query: list = [None] * len(query_texts)
+            for want in (True, False):
+                rows = [i for i, h in enumerate(has_lex) if h == want]
+                if not rows:
+                    continue
+                sel = torch.tensor(rows, dtype=torch.long, device=dense.device)
+                batch = QueryBatch(dense=dense.index_select(0, sel).contiguous())
+                if want:
+                    parts = [query_sparse_arrays(self.embedder._convert_sparse(lex[i])) for i in rows]
+                    indptr = np.zeros(len(parts) + 1, dtype=np.int32)
+                    np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
+                    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(retriever.device)
+                    batch = QueryBatch(dense=batch.dense, sparse_indptr=t(indptr),
+                                       sparse_indices=t(np.concatenate([p[0] for p in parts])),
+                                       sparse_values=t(np.concatenate([p[1] for p in parts])))
+                out, mode = retriever.search_batch(batch, k, resolved, filter_metadata, search_type)
+                thr = None  # search()'s score_threshold rule (qdrant.py:331: legacy dense only)
+                if mode == "legacy_dense" and self.config.retrieval.score_threshold > 0:
+                    thr = self.config.retrieval.score_threshold
+                for b, i in enumerate(rows):
+                    per_query[i] = retriever.materialize(out, mode, resolved, b, thr)
             results = []
             if use_rerank:
                 per_query = self._rerank_batch(query_texts, per_query, final_top_k)

@@ -7,8 +7,11 @@ rerank() keeps the reference's rules exactly:
     logit), build fresh RetrievalResult(chunk, score) with source=None (bge.py:116-131),
     stable sort descending, keep top_k (bge.py:134, 141)
   * any failure -> warning + the retrieval results sorted by score, top_k (bge.py:143-147)
-Weights: BAAI/bge-reranker-base is not on disk; the model is initialised from
-RerankingConfig.seed. Token ids: audio_rag_amd.text (stand-in tokenizer) or rerank_ids().
+Weights (load(), as CrossEncoder(config.model, max_length=512) at bge.py:50-55): config.model
+naming a local checkpoint directory or a cached hub snapshot loads its model.safetensors (or a
+weights-only pytorch_model.bin) and tokenizer.json (audio_rag_amd.checkpoints); otherwise
+(BAAI/bge-reranker-base is not on disk here) the model is initialised from RerankingConfig.seed
+and token ids come from the stand-in tokenizer audio_rag_amd.text. score_ids() takes ids directly.
 """
 
 from __future__ import annotations
@@ -21,10 +24,29 @@ from audio_rag_amd.config.schema import RerankingConfig
 from audio_rag_amd.core.base import RetrievalResult
 from audio_rag_amd.core.exceptions import RerankingError
 from audio_rag_amd.reranking.base import BaseReranker, RerankerRegistry
+from audio_rag_amd.checkpoints import tokenizer_for
 from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
 from audio_rag_amd.text import HashTokenizer, pad_batch, pair_ids
 
 logger = logging.getLogger(__name__)
+
+
+def load_reranker(name: str, seed: int, arch: dict | None = None):
+    """(XLMRobertaForSequenceClassification fp32 CPU, tokenizer or None): the checkpoint
+    config.model names when it is on disk, else the seeded stand-in."""
+    from transformers import XLMRobertaForSequenceClassification
+
+    from audio_rag_amd.checkpoints import load_pretrained, load_tokenizer, resolve_local
+
+    path = resolve_local(name)
+    if path is None:
+        logger.warning(f"{name}: no local checkpoint; using seeded stand-in weights (seed {seed}) "
+                       "and the stand-in tokenizer")
+        return build_reranker(seed, arch), None
+    hf = load_pretrained(XLMRobertaForSequenceClassification, path)
+    if hf.config.num_labels != 1:
+        raise ValueError(f"{path}: a cross-encoder has one output logit, not {hf.config.num_labels}")
+    return hf, load_tokenizer(path)
 
 
 @RerankerRegistry.register("bge-reranker")
@@ -38,7 +60,9 @@ class BGEReranker(BaseReranker):
         self._device = device or torch.device("cuda", 0)
         self._arch = arch
         self._model: CrossEncoderXLMR | None = None
-        self.tokenizer = HashTokenizer()
+        # the checkpoint's tokenizer.json when config.model is on disk (known before load(): a
+        # lazy load() inside rerank() must not change how that call tokenised), else the stand-in
+        self.tokenizer = tokenizer_for(config.model) or HashTokenizer()
 
     @property
     def vram_required(self) -> float:
@@ -48,7 +72,8 @@ class BGEReranker(BaseReranker):
         if self._is_loaded:
             return
         try:
-            hf = build_reranker(self.config.seed, self._arch)
+            logger.info(f"Loading reranker {self.config.model} on {self._device}")
+            hf, _ = load_reranker(self.config.model, self.config.seed, self._arch)
             self._model = CrossEncoderXLMR(hf, self._device)
             if self.config.dtype == "fp16":
                 self._model.to_dtype(torch.float16)

@@ -245,9 +245,19 @@ class CrossEncoderXLMR:
     # otherwise leave the GPU idle between kernels). Sequences are right-padded with <pad>
     # (mask 0) to the bucket: the real tokens' outputs, and so the <s> row the head reads, are
     # those of the unpadded batch.
+    # The pair count is bucketed too (multiples of 8 up to 128 pairs, of 64 above; the extra rows
+    # are <s>-only sequences whose scores are dropped), and every capture allocates from one
+    # shared memory pool (replays are serial on one stream and each result is copied out at
+    # once, so one graph's dead activations may back another's): variable candidate counts no
+    # longer pin one activation-sized pool per (n, L).
     use_graphs = True
     GRAPH_L_STEP = 32
     MAX_GRAPHS = 8
+
+    @staticmethod
+    def _n_bucket(n: int) -> int:
+        step = 8 if n <= 128 else 64
+        return -(-n // step) * step
 
     def _graph_for(self, n: int, L: int):
         key = (n, L)
@@ -268,7 +278,9 @@ class CrossEncoderXLMR:
                 self._forward_eager(ids_t, mask_t)
         torch.cuda.current_stream(self.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        if getattr(self, "_pool", None) is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._pool):
             probs = self._forward_eager(ids_t, mask_t)
         g = (graph, ids_t, mask_t, probs)
         self._graphs[key] = g
@@ -281,14 +293,20 @@ class CrossEncoderXLMR:
         Lb = min(-(-L // self.GRAPH_L_STEP) * self.GRAPH_L_STEP, self.pos.shape[0] - self.pad - 1)
         if Lb < L:
             return self._forward_eager(ids, mask)
-        graph, ids_t, mask_t, probs = self._graph_for(n, Lb)
+        nb = self._n_bucket(n)
+        graph, ids_t, mask_t, probs = self._graph_for(nb, Lb)
         if Lb > L:
-            ids_t[:, L:].fill_(self.pad)
-            mask_t[:, L:].zero_()
-        ids_t[:, :L].copy_(ids)
-        mask_t[:, :L].copy_(mask)
+            ids_t[:n, L:].fill_(self.pad)
+            mask_t[:n, L:].zero_()
+        ids_t[:n, :L].copy_(ids)
+        mask_t[:n, :L].copy_(mask)
+        if nb > n:  # padding pairs: <s> alone (their scores are dropped)
+            ids_t[n:].fill_(self.pad)
+            mask_t[n:].zero_()
+            ids_t[n:, 0] = 0
+            mask_t[n:, 0] = 1
         graph.replay()
-        return probs.clone()
+        return probs[:n].clone()
 
     @torch.inference_mode()
     def forward(self, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:

@@ -24,6 +24,8 @@ _WORD = re.compile(r"\w+|[^\w\s]", re.UNICODE)
 
 
 class HashTokenizer:
+    special_ids = SPECIAL_IDS
+
     def __init__(self, vocab_size: int = VOCAB):
         self.vocab_size = vocab_size
 

@@ -331,6 +331,13 @@ int armi_enc_bias_gelu(float* x, const float* bias, int64_t n_rows, int width,
 int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
                    int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
+/* The same over fp16 tables (the fp16 model's own word / position / type embeddings, no fp32
+ * copy: BGE-M3's word table is 0.5 GB in fp16); identical results (the fp16 values convert
+ * exactly, the sums are the same fp32 operations). */
+int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t* pos,
+                       const uint16_t* type0, const float* gamma, const float* beta, float* out,
+                       int n_seq, int L, int width, int pad_id, int vocab, int n_pos, float eps,
+                       hipStream_t stream);
 /* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)
  * hidden [n_seq][L][width] -> out [n_seq]; dense_wt = dense_w transposed, [width_in][width_out]
  * row-major (nn.Linear's weight.t()); width a multiple of 4, <= 1024 (8 sequences per
@@ -381,10 +388,11 @@ int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
 #define ARMI_EPI_BIAS_GELU 1
 int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out,
                         int64_t m, int n, int k, int epilogue, hipStream_t stream);
-/* The same layer for m <= 32 token rows (the batch-1 query encode of BGE-M3,
- * embeddings/bge.py:137-157 through embeddings/xlmr_f16.py): a weight stream, 16 output columns
- * per workgroup, K split over its 8 waves and summed in a fixed order. n % 16 == 0,
- * k % 256 == 0; bias fp32 [n]. */
+/* The same layer for the query encodes of BGE-M3 (embeddings/bge.py:137-157 through
+ * embeddings/xlmr_f16.py): a weight stream, 16 output columns x 32 token rows per workgroup, K
+ * split over its 8 (16 for k = 3072 / 4096) waves and summed in a fixed order. A row's result
+ * depends only on its own inputs and k, not on m: a query encoded alone and inside a batch gets
+ * the same bits. m <= 32 * 65535, n % 16 == 0, k % 256 == 0; bias fp32 [n]. */
 int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float* bias,
                               uint16_t* out, int m, int n, int k, int epilogue,
                               hipStream_t stream);
