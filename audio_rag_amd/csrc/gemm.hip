@@ -458,6 +458,15 @@ __device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
   return (threadIdx.x & 32) ? (uint32_t)p[0] : (uint32_t)p[1];
 }
 
+// sources of one tile of a linear_w4_kernel stream
+struct W4Src {
+  const unsigned char* pw;  // feature block of w
+  const unsigned char* px;  // token block of x
+  uint32_t ox[4];           // per-lane token row offsets (clamped for a partial block)
+  int tp;
+  int64_t q0;
+};
+
 template <int EPI>
 __global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void linear_w4_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
@@ -491,13 +500,7 @@ void linear_w4_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   uint32_t ow[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) ow[p] = (uint32_t)(((p * 64 + prow) * k + c * 8) * 2);
-  struct Src {
-    const unsigned char* pw;  // feature block of w
-    const unsigned char* px;  // token block of x
-    uint32_t ox[4];
-    int tp;
-    int64_t q0;
-  };
+  using Src = W4Src;
   auto tile_src = [&](int64_t j) {
     Src t;
     const int64_t jj = j < my_tiles ? j : my_tiles - 1;  // past the stream: clamped, never read
