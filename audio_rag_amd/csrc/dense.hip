@@ -2440,7 +2440,11 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
   const int64_t tiles = std::max<int64_t>(idx->n_tiles, 1);
   const int cus = std::min(std::max(idx->num_cus, 1), 256);
   p.n_qb = std::max(1, (nq + kQB - 1) / kQB);
-  int64_t want = cus;
+  // one block: at least one tile per wave of a workgroup (round 5). A small shard (10k rows: 313
+  // tiles) otherwise spread over 157 workgroups of 2 tiles, each paying the query-image phase and
+  // writing 64 x 16 candidates (2 MB of lists = 27 % over the 10 MB image, and a 2.5k-entry merge
+  // pool); 40 workgroups of 8 tiles finish as early and write a quarter of that.
+  int64_t want = p.n_qb > 1 ? cus : std::min<int64_t>(cus, (tiles + kWaves - 1) / kWaves);
   if (p.n_qb > 1) want = std::max<int64_t>(8, ((cus + p.n_qb - 1) / p.n_qb + 7) / 8 * 8);
   const int64_t wgs = std::min<int64_t>(want, tiles);
   p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
@@ -2721,7 +2725,12 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   int sel_col = 1, sel_rank = kc;
   merge_select(kc, n_wg, sel_col, sel_rank);
   if (use_gemm_scan(nq) && use_tiled_i8(idx, k)) sel_col = 0;  // exact pool selection
-#ifndef ARMI_POST_SEPARATE  // probe builds only: the round-4 three-launch chain, for A/B
+#ifdef ARMI_POST_FUSED
+  // Probe builds only (ARMI_BUILD_FLAGS=-DARMI_POST_FUSED). A/B on one box, 200-step benches
+  // (profiles/r05g_post_fused_ab.txt): fused 0.2442-0.2519 / 0.0709-0.0718 / 0.0518-0.0521 ms per
+  // step at 1M / 100k / 10k rows, the three launches 0.2445-0.2448 / 0.0700-0.0701 /
+  // 0.0513-0.0514 ms. The launches queue back to back, so one launch saves nothing and the
+  // agent-scope hand-offs cost a little; the default stays the chain below.
   if (!use_gemm_scan(nq) && use_i8_filter(idx, k)) {
     // merge + collect pass + collect merge in one launch (dense_post_kernel)
     const ScanPlan cp = plan_scan(idx, k, 1);

@@ -24,10 +24,11 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // LayerNorm of a row held as kMaxPerLane strided values per lane (two-pass mean / variance,
 // as torch.nn.functional.layer_norm computes it).
+template <typename OutT = float>
 __device__ __forceinline__ void layernorm_row(float (&v)[kMaxPerLane], int width, int lane,
                                               const float* __restrict__ gamma,
                                               const float* __restrict__ beta, float eps,
-                                              float* __restrict__ out) {
+                                              OutT* __restrict__ out) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxPerLane; ++i)
@@ -45,7 +46,7 @@ __device__ __forceinline__ void layernorm_row(float (&v)[kMaxPerLane], int width
 #pragma unroll
   for (int i = 0; i < kMaxPerLane; ++i) {
     const int c = lane + 64 * i;
-    if (c < width) out[c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    if (c < width) out[c] = (OutT)((v[i] - mean) * rstd * gamma[c] + beta[c]);
   }
 }
 
@@ -127,14 +128,14 @@ __global__ __launch_bounds__(256) void bias_gelu_kernel(float* __restrict__ x,
 // padding_idx + number of non-pad tokens in [0, t] for a non-pad token, padding_idx for a pad.
 // T = float (fp32 tables) or _Float16 (the fp16 model's own tables, no fp32 copy; the sums are
 // the same fp32 operations on the same values)
-template <typename T>
+template <typename T, typename OutT>
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
                                                     const T* __restrict__ word,
                                                     const T* __restrict__ pos,
                                                     const T* __restrict__ type0,
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta,
-                                                    float* __restrict__ out, int n_seq, int L,
+                                                    OutT* __restrict__ out, int n_seq, int L,
                                                     int width, int pad_id, int vocab, int n_pos,
                                                     float eps) {
   const int64_t tok = (int64_t)blockIdx.x * 4 + armi::wave_id();
@@ -287,14 +288,14 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
   ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
                "embed: null pointer argument");
   const int64_t toks = (int64_t)n_seq * L;
-  embed_kernel<float><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
+  embed_kernel<float, float><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
       ids, word, pos, type0, gamma, beta, out, n_seq, L, width, pad_id, vocab, n_pos, eps);
   ARMI_LAUNCHED("embed_kernel");
   return ARMI_OK;
 }
 
 int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t* pos,
-                       const uint16_t* type0, const float* gamma, const float* beta, float* out,
+                       const uint16_t* type0, const float* gamma, const float* beta, uint16_t* out,
                        int n_seq, int L, int width, int pad_id, int vocab, int n_pos, float eps,
                        hipStream_t stream) {
   ARMI_REQUIRE(width >= 1 && width <= 64 * kMaxPerLane, "embed_f16: width must be in [1, 1024]");
@@ -305,10 +306,10 @@ int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t*
   ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
                "embed_f16: null pointer argument");
   const int64_t toks = (int64_t)n_seq * L;
-  embed_kernel<_Float16><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
+  embed_kernel<_Float16, _Float16><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
       ids, reinterpret_cast<const _Float16*>(word), reinterpret_cast<const _Float16*>(pos),
-      reinterpret_cast<const _Float16*>(type0), gamma, beta, out, n_seq, L, width, pad_id, vocab,
-      n_pos, eps);
+      reinterpret_cast<const _Float16*>(type0), gamma, beta, reinterpret_cast<_Float16*>(out),
+      n_seq, L, width, pad_id, vocab, n_pos, eps);
   ARMI_LAUNCHED("embed_kernel");
   return ARMI_OK;
 }

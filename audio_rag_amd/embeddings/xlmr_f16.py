@@ -100,11 +100,10 @@ class XLMREncoderF16:
         d, H, dh = self.d, self.heads, self.dh
         s = stream_handle()
         rows = n * L
-        h = torch.empty((rows, d), dtype=torch.float32, device=self.device)
+        h16 = torch.empty((rows, d), dtype=torch.float16, device=self.device)
         call("armi_enc_embed_f16", ptr(ids), ptr(self.word), ptr(self.pos), ptr(self.type0),
-             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad,
+             ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h16), n, L, d, self.pad,
              self.word.shape[0], self.pos.shape[0], self.eps, s)
-        h16 = h.half()
         scale = 1.0 / math.sqrt(dh)
         for ly in self.layers:
             qkv = self._lin(h16, ly, "wqkv", "bqkv")                         # [n*L, 3d]

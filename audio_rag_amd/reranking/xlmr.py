@@ -92,11 +92,15 @@ class CrossEncoderXLMR:
             raise ValueError("residual must be 'fp16' or 'fp32'")
         self.residual = residual
         self.gemm_dtype = dtype
+        if dtype == torch.float16:
+            # fp16 embedding tables: the fp16 forward embeds straight to fp16 (armi_enc_embed_f16)
+            self.word16, self.pos16, self.type16 = (t.half() for t in (self.word, self.pos,
+                                                                       self.type0))
         for ly in self.layers:
             for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
                 ly[name + "_g"] = ly[name].to(dtype)
             if dtype == torch.float16:
-                # nn.Linear layout [out, in] for F.linear (the TN GEMM hipBLASLt tunes best)
+                # nn.Linear layout [out, in] for F.linear and the armi GEMMs
                 for name in ("wqkv_t", "wo_t", "wi_t", "wo2_t"):
                     ly[name[:-2] + "_h"] = ly[name].t().contiguous().half()
                 for name in ("bqkv", "bo", "bi", "bo2"):
@@ -108,14 +112,18 @@ class CrossEncoderXLMR:
         s = stream_handle()
         rows = n * L
         lin = torch.nn.functional.linear
+        if self.residual == "fp16":
+            h16 = torch.empty((rows, d), dtype=torch.float16, device=self.device)
+            call("armi_enc_embed_f16", ptr(ids), ptr(self.word16), ptr(self.pos16),
+                 ptr(self.type16), ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h16), n, L, d,
+                 self.pad, self.word.shape[0], self.pos.shape[0], self.eps, s)
+            return self._layers_f16_residual(h16, mask, n, L)
         h = torch.empty((rows, d), dtype=torch.float32, device=self.device)
         call("armi_enc_embed", ptr(ids), ptr(self.word), ptr(self.pos), ptr(self.type0),
              ptr(self.emb_ln[0]), ptr(self.emb_ln[1]), ptr(h), n, L, d, self.pad,
              self.word.shape[0], self.pos.shape[0], self.eps, s)
         h16 = h.half()
         scale = 1.0 / math.sqrt(dh)
-        if self.residual == "fp16":
-            return self._layers_f16_residual(h16, mask, n, L)
         for ly in self.layers:
             qkv = lin(h16, ly["wqkv_h"], ly["bqkv_h"])                     # [n*L, 3d] fp16
             ctx = torch.empty((rows, d), dtype=torch.float16, device=self.device)

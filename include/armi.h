@@ -332,10 +332,11 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
                    const float* gamma, const float* beta, float* out, int n_seq, int L,
                    int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
 /* The same over fp16 tables (the fp16 model's own word / position / type embeddings, no fp32
- * copy: BGE-M3's word table is 0.5 GB in fp16); identical results (the fp16 values convert
- * exactly, the sums are the same fp32 operations). */
+ * copy: BGE-M3's word table is 0.5 GB in fp16), writing the fp16 activations the fp16 forwards
+ * feed their first GEMM: out [n_seq][L][width] fp16, each value the round-to-nearest-even of
+ * what armi_enc_embed computes in fp32 from the same (fp16-exact) table values. */
 int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t* pos,
-                       const uint16_t* type0, const float* gamma, const float* beta, float* out,
+                       const uint16_t* type0, const float* gamma, const float* beta, uint16_t* out,
                        int n_seq, int L, int width, int pad_id, int vocab, int n_pos, float eps,
                        hipStream_t stream);
 /* classification head on token 0: sigmoid(out_w . tanh(dense_w h0 + dense_b) + out_b)

@@ -274,3 +274,72 @@ def test_sparse_collect_overflow_is_exact(gpu, oracle_mod):
     # the -inf threshold case: 5 000 overlapping rows in <= 7 ranges pool < 240 candidates
     got = _run(idx, q, 240, gpu)
     assert got["flags"][1] & 2 and got["count"][1] == 240
+
+
+def test_sparse_plain_and_other_passes(gpu, oracle_mod):
+    """The register scan (sparse_scan_reg_kernel) runs a pass only when every product of a shared
+    term is a normal float > 0; otherwise sparse_scan_kernel does. Both must give the oracle's
+    answer: a plain pass; a pass with one zero and one negative weight; a pass whose products
+    underflow to denormals; an index holding a zero value (never plain)."""
+    csr = oracle_mod.sparse_corpus(20000, seed=91)
+    qi, qx, qv = oracle_mod.sparse_queries(64, seed=92)
+    idx = _sparse_index(csr, gpu)
+    for k in (5, 40):
+        _same(_run(idx, (qi, qx, qv), k, gpu), oracle_mod.sparse_topk(*csr, qi, qx, qv, k))
+    odd = qv.copy()
+    odd[qi[3]] = 0.0
+    odd[qi[9]] = -0.2
+    _same(_run(idx, (qi, qx, odd), 20, gpu), oracle_mod.sparse_topk(*csr, qi, qx, odd, 20))
+    tiny = (qv * np.float32(1e-37)).astype(np.float32)
+    _same(_run(idx, (qi, qx, tiny), 20, gpu), oracle_mod.sparse_topk(*csr, qi, qx, tiny, 20))
+    indptr, indices, values = csr
+    values = values.copy()
+    values[::97] = 0.0
+    idx0 = _sparse_index((indptr, indices, values), gpu)
+    _same(_run(idx0, (qi, qx, qv), 20, gpu),
+          oracle_mod.sparse_topk(indptr, indices, values, qi, qx, qv, 20))
+
+
+def test_sparse_clustered_postings(gpu, oracle_mod):
+    """A posting-list term (below 1/8 of the rows) whose postings fill whole 128-row tiles: the
+    register scan's in-tile window of 64 postings is full, so it reads the tile's next windows."""
+    indptr, indices, values = oracle_mod.sparse_corpus(20000, seed=93)
+    t = 249_999  # not in the Zipf corpus's head
+    rows = np.r_[0:300, 5000:5090, 19_900:20000]
+    add = np.zeros(20000, dtype=bool)
+    add[rows] = True
+    new_ptr = np.zeros_like(indptr)
+    np.cumsum(np.diff(indptr) + add, out=new_ptr[1:])
+    ni = np.empty(new_ptr[-1], np.int32)
+    nv = np.empty(new_ptr[-1], np.float32)
+    rng = np.random.default_rng(94)
+    for r in range(20000):
+        a, b = indptr[r], indptr[r + 1]
+        c = new_ptr[r]
+        ids, vals = indices[a:b], values[a:b]
+        if add[r]:
+            keep = ids != t
+            ids = np.append(ids[keep], t)
+            vals = np.append(vals[keep], np.float32(rng.uniform(0.01, 0.4)))
+            o = np.argsort(ids, kind="stable")
+            ids, vals = ids[o], vals[o]
+        ni[c:c + len(ids)] = ids
+        nv[c:c + len(ids)] = vals
+    csr = (new_ptr, ni, nv)
+    qi, qx, qv = oracle_mod.sparse_queries(64, seed=95)
+    # every query also carries t (kept ascending)
+    xs, vs = [], []
+    for b in range(64):
+        x, v = qx[qi[b]:qi[b + 1]], qv[qi[b]:qi[b + 1]]
+        keep = x != t
+        x, v = np.append(x[keep], t), np.append(v[keep], np.float32(0.3))
+        o = np.argsort(x, kind="stable")
+        xs.append(x[o])
+        vs.append(v[o])
+    qx2 = np.concatenate(xs).astype(np.int32)
+    qv2 = np.concatenate(vs).astype(np.float32)
+    qi2 = np.zeros(65, np.int32)
+    np.cumsum([len(x) for x in xs], out=qi2[1:])
+    idx = _sparse_index(csr, gpu)
+    for k in (5, 40):
+        _same(_run(idx, (qi2, qx2, qv2), k, gpu), oracle_mod.sparse_topk(*csr, qi2, qx2, qv2, k))
