@@ -758,10 +758,13 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr, int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list,
     int col_cap,
-    int32_t* __restrict__ sync) {
+    int32_t* __restrict__ sync, int xcd_step) {
   // first pass: zero the post-scan kernel's arrival counters (it runs next on this stream)
   if (!COLLECT && sync && blockIdx.x == 0 && threadIdx.x < 4) sync[threadIdx.x] = 0;
-  scan_i8_body<DIM, COLLECT, NT>(blockIdx.x, rows8, a32, e32, row_mask, n_rows, n_tiles, tiles_per_wg, n_ranges, n_qb,
+  // xcd_step > 1 (small shards, plan_scan): only workgroups whose id is a multiple of xcd_step
+  // work, i.e. those on XCDs 0, xcd_step, ... (workgroup i runs on XCD i mod 8)
+  if (blockIdx.x % xcd_step != 0) return;
+  scan_i8_body<DIM, COLLECT, NT>(blockIdx.x / xcd_step, rows8, a32, e32, row_mask, n_rows, n_tiles, tiles_per_wg, n_ranges, n_qb,
       queries_all, q_stride, cand_key, cand_row, cand_bound, tile_ord, flags, thr, col_cnt,
       col_list, col_cap);
 }
@@ -2429,6 +2432,7 @@ size_t merge_lds_bytes(int pool2) { return (size_t)pool2 * 24 + 16; }
 struct ScanPlan {
   int n_qb = 1;   // 64-query blocks of the call
   int grid = 0;   // workgroups launched
+  int xcd_step = 1;  // single block on few workgroups: the working ones sit on 8 / xcd_step XCDs
   int n_wg = 0;   // tile ranges (candidate lists per query)
   int tiles_per_wg = 0;
   int pool2 = 0;
@@ -2450,6 +2454,17 @@ ScanPlan plan_scan(const armi_index* idx, int k, int nq) {
   p.tiles_per_wg = (int)((tiles + wgs - 1) / wgs);
   p.n_wg = (int)((tiles + p.tiles_per_wg - 1) / p.tiles_per_wg);
   p.grid = p.n_qb == 1 ? p.n_wg : p.n_qb * 8 * ((p.n_wg + 7) / 8);
+  // Probe builds only (ARMI_BUILD_FLAGS=-DARMI_XCD_COMPACT): a single block of <= 64 workgroups
+  // on two XCDs (workgroup i runs on XCD i mod 8; the others exit at once), so only two L2s fetch
+  // the fp16 queries (128 KB each). At 10k rows that takes the scan's HBM traffic from 1.18 to
+  // 1.06 x (one XCD) of its 10.4 MB but the step from 0.0518 to 0.0535-0.0537 ms: the 20
+  // workgroups' query-image reads then share one or two L2s (profiles/r05p_xcd_ab.txt).
+#ifdef ARMI_XCD_COMPACT
+  if (p.n_qb == 1 && p.n_wg <= 2 * std::max(1, cus / 8)) {
+    p.xcd_step = 4;
+    p.grid = p.n_wg * p.xcd_step;
+  }
+#endif
   p.pool2 = armi::pow2_at_least(p.n_wg * kKW);
   p.kc = std::max(4, std::min(armi::pow2_at_least(k + 8), 256));
   return p;
@@ -2705,7 +2720,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, w.sync);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, w.sync, sp.xcd_step);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -2779,7 +2794,7 @@ int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, in
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord,
-        out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap, nullptr);
+        out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap, nullptr, 1);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;

@@ -867,7 +867,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
         if (cx < 0) {
           // dense column: the tile's value bits, rows tlo + 2 lane and + 1 in .x / .y (zero past
           // the store). A 16-B load straight into sp[k] (.z / .w unused): an 8-B load into part
-          // of it would need a copy, i.e. a wait for the load here instead of in finish
+          // of it would need a copy, i.e. a wait for the load here instead of in finish (round 5:
+          // measured in the ISA, a vmcnt(0) before the load that drains every staged load)
           sp[k] = *reinterpret_cast<const p4*>(dense_val + (size_t)(-cx - 1) * dense_stride + tlo +
                                                2 * lane);
         } else {

@@ -294,8 +294,11 @@ def rrf_fuse(a: TopK, b: TopK, limit: int, rrf_k: int = 2) -> TopK:
 
 class ConcurrentHybrid:
     """The two prefetches of one hybrid search (qdrant.py:281-298) on two HIP streams: the
-    sparse top-k on a side stream overlaps the dense scan and merge on the caller's stream (the
-    two share nothing until the fusion), then RRF runs on the caller's stream."""
+    sparse top-k on a side stream, the dense scan and merge on the caller's stream (the two share
+    nothing until the fusion), then RRF on the caller's stream. The two scans cannot share a CU
+    (each fills its LDS and register file), so in a kernel trace they run one after the other
+    (profiles/r05m_hybrid_kernel_stats.csv); what overlaps is the small kernels of
+    one chain (merges, collect passes, pass_terms) with the other chain's scan tail."""
 
     def __init__(self, device: torch.device):
         self.side = torch.cuda.Stream(device=device)
@@ -333,3 +336,59 @@ def _device_copy(dst: int, src: int, nbytes: int) -> None:
     rc = _hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3)  # DeviceToDevice
     if rc != 0:
         raise RuntimeError(f"hipMemcpy failed: {rc}")
+
+
+class HybridGraph:
+    """One hybrid step over a fixed batch size (ConcurrentHybrid: dense top-k, sparse top-k, RRF)
+    captured as a HIP graph. A call copies the batch into the graph's static inputs and replays
+    every kernel of the step; the eager step's ~20 launches with their Python argument handling
+    take longer on the host than the step takes on the GPU, so eager steps leave the GPU idle
+    between them (30 us per 0.54 ms step in profiles/r05m_hybrid_kernel_stats.csv's trace).
+
+    The returned TopK's tensors are the graph's outputs: a later call overwrites them, so callers
+    consume (or clone) a result before the next call."""
+
+    def __init__(self, dense: DenseIndex, sparse: SparseIndex, batch: int, pre_k: int, limit: int,
+                 rrf_k: int = 2, max_terms: int = 256):
+        dev = dense.device
+        self.batch = int(batch)
+        self.q = torch.zeros((batch, dense.dim), dtype=torch.float16, device=dev)
+        self.qi = torch.zeros(batch + 1, dtype=torch.int32, device=dev)
+        self.qx = torch.zeros(batch * max_terms, dtype=torch.int32, device=dev)
+        self.qv = torch.zeros(batch * max_terms, dtype=torch.float32, device=dev)
+        ws = torch.empty(max(dense.workspace_bytes(batch, pre_k), 1), dtype=torch.uint8, device=dev)
+        sws = torch.empty(max(sparse.workspace_bytes(batch, pre_k), 1), dtype=torch.uint8,
+                          device=dev)
+        hybrid = ConcurrentHybrid(dev)
+
+        def run() -> TopK:
+            return hybrid(lambda: dense.topk(self.q, pre_k, workspace=ws),
+                          lambda: sparse.topk(self.qi, self.qx, self.qv, pre_k, workspace=sws),
+                          (self.qi, self.qx, self.qv), limit, rrf_k)
+
+        # warm-up on a side stream, then capture under inference mode (as _QueryGraph and the
+        # reranker's graphs do: the CUDA generator's graph state is shared by every capture)
+        with torch.inference_mode():
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    run()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = run()
+        self._keep = (ws, sws, hybrid, dense, sparse)
+
+    def __call__(self, queries: torch.Tensor, q_indptr: torch.Tensor, q_indices: torch.Tensor,
+                 q_values: torch.Tensor) -> TopK:
+        n = int(q_indices.numel())
+        if (tuple(queries.shape) != tuple(self.q.shape) or int(q_indptr.numel()) != self.batch + 1
+                or n > self.qx.numel() or int(q_values.numel()) != n):
+            raise ValueError("HybridGraph: batch shape differs from the captured one")
+        self.q.copy_(queries)
+        self.qi.copy_(q_indptr)
+        self.qx[:n].copy_(q_indices)
+        self.qv[:n].copy_(q_values)
+        self.graph.replay()
+        return self.out
