@@ -440,7 +440,8 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl) {
+    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl,
+    int32_t* __restrict__ coll_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem);               // [kBmWords]
   int32_t* wpre = reinterpret_cast<int32_t*>(smem + kBmWords * 4);  // [kBmWords]
@@ -452,6 +453,7 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
   const int lane = tid & 63;
   const int nw = (vocab + 31) >> 5;
   for (int i = tid; i < nw; i += kScanThreads) bits[i] = 0u;
+  if (tid < 2 * kQB) coll_count[tid] = 0;  // the pass's collect counters and helper counters
   if (tid < kQB) deal_queries(q_indptr, nq, tid, off, qslot, qof, flags);
   __syncthreads();
   const int total = off[kQB];
@@ -543,7 +545,8 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl) {
+    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl,
+    int32_t* __restrict__ coll_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
   float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
@@ -553,6 +556,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
   const int tid = threadIdx.x;
   const int wave = armi::wave_id();
   const int lane = tid & 63;
+  if (tid < 2 * kQB) coll_count[tid] = 0;  // the pass's collect counters and helper counters
   if (tid < kQB) deal_queries(q_indptr, nq, tid, off, qslot, qof, flags);
   __syncthreads();
   const int total = off[kQB];
@@ -2286,17 +2290,16 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       ARMI_HIP(hipMemsetAsync(out_ids + (size_t)q0 * k, 0xff, sizeof(int64_t) * nqp * k, stream));
       continue;
     }
-    ARMI_HIP(hipMemsetAsync(w.coll_count, 0, sizeof(int) * 2 * kQB, stream));
     GroupLists gl = w.gl;  // built by pass_terms only for the register scan
     if (!use_reg_scan(idx)) gl.gn = nullptr;
     if (idx->vocab <= kBitmapVocab)
       pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLaunchLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl);
+          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl, w.coll_count);
     else
       pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl);
+          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl, w.coll_count);
     ARMI_LAUNCHED("pass_terms_kernel");
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;

@@ -296,9 +296,10 @@ class ConcurrentHybrid:
     """The two prefetches of one hybrid search (qdrant.py:281-298) on two HIP streams: the
     sparse top-k on a side stream, the dense scan and merge on the caller's stream (the two share
     nothing until the fusion), then RRF on the caller's stream. The two scans cannot share a CU
-    (each fills its LDS and register file), so in a kernel trace they run one after the other
-    (profiles/r05m_hybrid_kernel_stats.csv); what overlaps is the small kernels of
-    one chain (merges, collect passes, pass_terms) with the other chain's scan tail."""
+    (each fills its LDS and register file), so in a kernel trace they run nearly one after the
+    other (profiles/r05m_hybrid_kernel_stats.csv); what overlaps is the small kernels
+    of one chain (merges, collect passes, pass_terms) with the other chain's scan and tail: both
+    chains on one stream measured 0.550 against 0.522 ms per step on one box (r05t)."""
 
     def __init__(self, device: torch.device):
         self.side = torch.cuda.Stream(device=device)
@@ -340,10 +341,12 @@ def _device_copy(dst: int, src: int, nbytes: int) -> None:
 
 class HybridGraph:
     """One hybrid step over a fixed batch size (ConcurrentHybrid: dense top-k, sparse top-k, RRF)
-    captured as a HIP graph. A call copies the batch into the graph's static inputs and replays
-    every kernel of the step; the eager step's ~20 launches with their Python argument handling
-    take longer on the host than the step takes on the GPU, so eager steps leave the GPU idle
-    between them (30 us per 0.54 ms step in profiles/r05m_hybrid_kernel_stats.csv's trace).
+    captured as a HIP graph. The step's inputs live in one staging buffer (fp16 queries, query
+    CSR indptr / indices / values at fixed offsets): a call copies a batch into it, one copy for
+    a batch prepared by pack() (or one per array), and replays every kernel of the step. The
+    eager step's ~20 launches with their Python argument handling take longer on the host than
+    the step takes on the GPU, so eager steps leave the GPU idle between them (30 us per 0.54 ms
+    step in profiles/r05m_hybrid_kernel_stats.csv's trace).
 
     The returned TopK's tensors are the graph's outputs: a later call overwrites them, so callers
     consume (or clone) a result before the next call."""
@@ -351,11 +354,10 @@ class HybridGraph:
     def __init__(self, dense: DenseIndex, sparse: SparseIndex, batch: int, pre_k: int, limit: int,
                  rrf_k: int = 2, max_terms: int = 256):
         dev = dense.device
-        self.batch = int(batch)
-        self.q = torch.zeros((batch, dense.dim), dtype=torch.float16, device=dev)
-        self.qi = torch.zeros(batch + 1, dtype=torch.int32, device=dev)
-        self.qx = torch.zeros(batch * max_terms, dtype=torch.int32, device=dev)
-        self.qv = torch.zeros(batch * max_terms, dtype=torch.float32, device=dev)
+        self.batch, self.dim, self.max_terms = int(batch), dense.dim, int(max_terms)
+        self._off = self._layout(self.batch, self.dim, self.max_terms)
+        self.stage = torch.zeros(self._off[-1], dtype=torch.uint8, device=dev)
+        self.q, self.qi, self.qx, self.qv = self._views(self.stage)
         ws = torch.empty(max(dense.workspace_bytes(batch, pre_k), 1), dtype=torch.uint8, device=dev)
         sws = torch.empty(max(sparse.workspace_bytes(batch, pre_k), 1), dtype=torch.uint8,
                           device=dev)
@@ -380,15 +382,55 @@ class HybridGraph:
                 self.out = run()
         self._keep = (ws, sws, hybrid, dense, sparse)
 
-    def __call__(self, queries: torch.Tensor, q_indptr: torch.Tensor, q_indices: torch.Tensor,
-                 q_values: torch.Tensor) -> TopK:
+    @staticmethod
+    def _layout(batch: int, dim: int, max_terms: int) -> tuple[int, int, int, int, int]:
+        def up(x: int) -> int:
+            return (x + 255) // 256 * 256
+
+        o_qi = up(batch * dim * 2)
+        o_qx = o_qi + up((batch + 1) * 4)
+        o_qv = o_qx + up(batch * max_terms * 4)
+        return 0, o_qi, o_qx, o_qv, o_qv + up(batch * max_terms * 4)
+
+    def _views(self, buf: torch.Tensor):
+        o_q, o_qi, o_qx, o_qv, end = self._off
+        b, n = self.batch, self.batch * self.max_terms
+        return (buf[o_q:o_qi].view(torch.float16)[: b * self.dim].view(b, self.dim),
+                buf[o_qi:o_qx].view(torch.int32)[: b + 1], buf[o_qx:o_qv].view(torch.int32)[:n],
+                buf[o_qv:end].view(torch.float32)[:n])
+
+    def _check(self, queries, q_indptr, q_indices, q_values) -> int:
         n = int(q_indices.numel())
-        if (tuple(queries.shape) != tuple(self.q.shape) or int(q_indptr.numel()) != self.batch + 1
-                or n > self.qx.numel() or int(q_values.numel()) != n):
+        if (tuple(queries.shape) != (self.batch, self.dim) or int(q_indptr.numel()) != self.batch + 1
+                or n > self.batch * self.max_terms or int(q_values.numel()) != n):
             raise ValueError("HybridGraph: batch shape differs from the captured one")
-        self.q.copy_(queries)
-        self.qi.copy_(q_indptr)
-        self.qx[:n].copy_(q_indices)
-        self.qv[:n].copy_(q_values)
+        return n
+
+    def pack(self, queries: torch.Tensor, q_indptr: torch.Tensor, q_indices: torch.Tensor,
+             q_values: torch.Tensor) -> torch.Tensor:
+        """A batch in the staging layout (one device buffer), for __call__(packed)."""
+        n = self._check(queries, q_indptr, q_indices, q_values)
+        buf = torch.zeros_like(self.stage)
+        q, qi, qx, qv = self._views(buf)
+        q.copy_(queries)
+        qi.copy_(q_indptr)
+        qx[:n].copy_(q_indices)
+        qv[:n].copy_(q_values)
+        return buf
+
+    def __call__(self, *batch: torch.Tensor) -> TopK:
+        """hg(packed) with a pack() buffer (one copy), or hg(queries, q_indptr, q_indices,
+        q_values)."""
+        if len(batch) == 1:
+            if batch[0].shape != self.stage.shape or batch[0].dtype != torch.uint8:
+                raise ValueError("HybridGraph: not a pack() buffer of this graph")
+            self.stage.copy_(batch[0])
+        else:
+            queries, q_indptr, q_indices, q_values = batch
+            n = self._check(queries, q_indptr, q_indices, q_values)
+            self.q.copy_(queries)
+            self.qi.copy_(q_indptr)
+            self.qx[:n].copy_(q_indices)
+            self.qv[:n].copy_(q_values)
         self.graph.replay()
         return self.out

@@ -22,11 +22,11 @@ def test_hybrid_graph_matches_eager(gpu):
         g = torch.Generator(device=gpu).manual_seed(seed)
         q = torch.randn((batch, rows.shape[1]), generator=g, device=gpu).half()
         qs = synthetic.make_sparse_queries(batch, gpu, seed)
-        got = hg(q, *qs)
         want = eager(lambda: dense.topk(q, pre_k), lambda: sparse.topk(*qs, pre_k), qs, limit)
-        torch.cuda.synchronize()
-        assert torch.equal(got.count, want.count)
-        assert torch.equal(got.ids, want.ids)
-        assert torch.equal(got.rank, want.rank)
+        for got in (hg(q, *qs), hg(hg.pack(q, *qs))):  # per-array copies; one packed copy
+            torch.cuda.synchronize()
+            assert torch.equal(got.count, want.count)
+            assert torch.equal(got.ids, want.ids)
+            assert torch.equal(got.rank, want.rank)
     with pytest.raises(ValueError):
         hg(q[:8], *synthetic.make_sparse_queries(8, gpu, 1))
