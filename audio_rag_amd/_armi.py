@@ -108,8 +108,6 @@ SIGNATURES: dict[str, tuple] = {
     "armi_enc_gelu_f16": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "armi_enc_linear_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                     c_int, c_void_p]),
-    "armi_enc_linear_w4_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
-                                       c_int, c_int, c_void_p]),
     "armi_enc_linear_small_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                           c_int, c_int, c_void_p]),
     "armi_enc_add_layernorm_f16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,

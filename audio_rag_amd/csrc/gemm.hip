@@ -427,263 +427,6 @@ __global__ __launch_bounds__(WAVES * 64) void linear_small_m_kernel(
 }
 
 
-// ------------------------------------------------------------------------- four-wave form
-// linear_w4_kernel (round 5): the cross-encoder's linears on the structure of the dense path's
-// four-wave tiled scan (dense_gemm_scan_w4_kernel): one wave per SIMD, each wave owning a
-// 128-feature x 128-token block of the 256 x 256 output tile as 16 v_mfma_f32_32x32x16_f16
-// accumulators (256 AccVGPRs), so a 16-deep k-step is 16 MFMAs against 4 + 4 ds_read_b128
-// (half the fragment reads per MFMA of linear_f16_kernel's 16x16x32 waves: the LDS traffic, not
-// the MFMA, bounded that loop, profiles/r04j_gemm_ablation.txt).
-//   * LDS ring of four 32-wide k-step stages (512 image rows x 64 B = 32 KB: 256 feature rows of
-//     w, then 256 token rows of x; 16-B chunk c of image row ir at slot c ^ ((ir >> 2) & 3)), three
-//     in flight, filled by 1-KB global_load_lds_dwordx4 pieces (8 per wave per stage);
-//   * per k-step s: the 16 MFMAs of sub-step 0 with the sub-step 1 reads of stage s and pieces 0-3
-//     of stage s + 3 between them -> vmcnt(12) retires stage s + 1 -> s_barrier -> the 16 MFMAs of
-//     sub-step 1 with the sub-step 0 reads of stage s + 1 and pieces 4-7 of s + 3;
-//   * the stream of stages runs across the workgroup's tiles (tile j's stages are j * KT ..), so
-//     the next tile's first stages load during a tile's epilogue; stages past the last tile are
-//     issued too (clamped, never read), so every wait keeps its count;
-//   * epilogue: bias (+ exact-erf GELU), fp16; lane (r, h) holds token r of each 32-token block
-//     and features 4 h + 8 g + 0..3 of each 32-feature block; one v_permlane32_swap per dword
-//     pair gives each lane 8 consecutive features (a 16-B store).
-constexpr int kW4T = 256;                 // tile rows of each operand
-constexpr int kW4Threads = 256;
-constexpr int kW4Stage = 2 * kW4T * 64;   // one 32-wide k-step stage (32 KB)
-constexpr int kW4Bias = 4 * kW4Stage;     // two 1-KB bias slots (tile parity) after the ring
-constexpr size_t kW4Lds = (size_t)kW4Bias + 2048;
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
-  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return (threadIdx.x & 32) ? (uint32_t)p[0] : (uint32_t)p[1];
-}
-
-// sources of one tile of a linear_w4_kernel stream
-struct W4Src {
-  const unsigned char* pw;  // feature block of w
-  const unsigned char* px;  // token block of x
-  uint32_t ox[4];           // per-lane token row offsets (clamped for a partial block)
-  int tp;
-  int64_t q0;
-};
-
-template <int EPI>
-__global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void linear_w4_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                      const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t m,
-                      int n, int k, int n_tiles_p, int64_t n_tiles) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = armi::wave_id();
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int wr = wave >> 1;  // feature group: features wr * 128 + ...
-  const int wq = wave & 1;   // token group: tokens wq * 128 + ...
-  const int KT = k / 32;     // stages per tile
-
-  // workgroup -> tiles: slot (XCD-major, bijective), tiles slot, slot + G, ...
-  const int G = gridDim.x;
-  const int b = blockIdx.x;
-  int slot;
-  {
-    const int q8 = G / 8, r8 = G % 8, xcd = b % 8;
-    slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-  }
-  const int64_t my_tiles = slot < n_tiles ? (n_tiles - 1 - slot) / G + 1 : 0;
-  if (my_tiles == 0) return;
-
-  // piece p of a stage, this wave: image rows p * 64 + prow (p < 4: feature rows of the tile,
-  // p >= 4: token rows); lane slot lane % 4 holds chunk c. Per-lane byte offsets over a scalar
-  // base: fixed for the feature rows, per tile for the token rows (clamped to the last token).
-  const int prow = wave * 16 + (lane >> 2);
-  const int c = (lane & 3) ^ ((lane >> 4) & 3);
-  uint32_t ow[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) ow[p] = (uint32_t)(((p * 64 + prow) * k + c * 8) * 2);
-  using Src = W4Src;
-  auto tile_src = [&](int64_t j) {
-    Src t;
-    const int64_t jj = j < my_tiles ? j : my_tiles - 1;  // past the stream: clamped, never read
-    const int64_t tile = (int64_t)slot + jj * G;
-    t.tp = (int)(tile % n_tiles_p);
-    t.q0 = (tile / n_tiles_p) * kW4T;
-    t.pw = reinterpret_cast<const unsigned char*>(w + (size_t)t.tp * kW4T * k);
-    t.px = reinterpret_cast<const unsigned char*>(x + (size_t)t.q0 * k);
-    const int64_t qlim = m - 1 - t.q0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int64_t rq = p * 64 + prow;
-      t.ox[p] = (uint32_t)(((rq < qlim ? rq : qlim) * k + c * 8) * 2);
-    }
-    return t;
-  };
-  Src cur = tile_src(0), nxt = tile_src(1);
-  // piece p of stage `ring` (ring slot), K-offset t (stage within its tile) of tile src ts
-  auto issue_piece = [&](const Src& ts, int ring, int t, int p) {
-    lds_ptr_t dst = (lds_ptr_t)(smem + ring * kW4Stage + (p * 4 + wave) * 1024);
-    if (p < 4)
-      __builtin_amdgcn_global_load_lds(ts.pw + t * 64 + ow[p], dst, 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds(ts.px + t * 64 + ts.ox[p - 4], dst, 16, 0, 0);
-  };
-  // the bias of a tile, with the tile's first stage (wave 0, one 1-KB LDS-DMA): read in the
-  // epilogue by an asm ds_read (a compiler-visible LDS read after an LDS-DMA gets a vmcnt(0),
-  // which would drain the next tile's staging)
-  auto issue_bias = [&](const Src& ts, int64_t j) {
-    if (wave == 0 && j < my_tiles)
-      __builtin_amdgcn_global_load_lds(bias + ts.tp * kW4T + 4 * lane,
-                                       (lds_ptr_t)(smem + kW4Bias + (j & 1) * 1024), 16, 0, 0);
-  };
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  const int swz = (r >> 2) & 3;
-  const uint32_t a_lane = lds0 + (uint32_t)(wr * 128 + r) * 64;
-  const uint32_t b_lane = lds0 + (uint32_t)(kW4T + wq * 128 + r) * 64;
-  const uint32_t co0 = (uint32_t)(((0 + h) ^ swz) << 4);
-  const uint32_t co1 = (uint32_t)(((2 + h) ^ swz) << 4);
-  u32x4 fa[2][4], fb[2][4];
-  auto read_item = [&](int ring_slot, int sub, int i) {
-    const uint32_t stage = (uint32_t)(ring_slot * kW4Stage) + (sub ? co1 : co0);
-    if (i < 4) {
-      const uint32_t addr = a_lane + stage;
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[sub][i]) : "v"(addr), "i"(i * 2048));
-    } else {
-      const uint32_t addr = b_lane + stage;
-      asm volatile("ds_read_b128 %0, %1 offset:%2"
-                   : "=v"(fb[sub][i - 4]) : "v"(addr), "i"((i - 4) * 2048));
-    }
-  };
-  auto frags_ready = [&](int sub) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(fa[sub][0]), "+v"(fa[sub][1]), "+v"(fa[sub][2]), "+v"(fa[sub][3]),
-                   "+v"(fb[sub][0]), "+v"(fb[sub][1]), "+v"(fb[sub][2]), "+v"(fb[sub][3])
-                 :: "memory");
-  };
-  {
-    int zero = 0;  // an AGPR operand makes hipcc keep the accumulators in AccVGPRs
-    asm volatile("; agpr-form hint %0" ::"a"(zero));
-  }
-  f32x16 acc[4][4];
-  auto mma = [&](u32x4 a, u32x4 bb, f32x16 cc) -> f32x16 {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a),
-                                                  __builtin_bit_cast(half8, bb), cc, 0, 0, 0);
-  };
-
-  auto epilogue = [&](int64_t j) {
-    const int64_t q0 = cur.q0;
-    const int f0 = cur.tp * kW4T + wr * 128;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      __builtin_amdgcn_sched_barrier(0);
-      // features f0 + 32 mb + 4 h + 8 g + e (g = 0..3, e = 0..3) of this lane
-      float bv[16];
-      {
-        const uint32_t ba = lds0 + kW4Bias + (uint32_t)(j & 1) * 1024u +
-                            (uint32_t)(wr * 128 + 32 * mb + 4 * h) * 4u;
-        u32x4 t4[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t4[g]) : "v"(ba), "i"(32 * g));
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(t4[0]), "+v"(t4[1]), "+v"(t4[2]), "+v"(t4[3])::"memory");
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bv[4 * g + e] = __uint_as_float(t4[g][e]);
-      }
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" : "+a"(acc[mb][nb]));
-        uint32_t pk[4][2];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = acc[mb][nb][4 * g + e] + bv[4 * g + e];
-            if constexpr (EPI == 1) v[e] = gelu_erf(v[e]);
-          }
-          pk[g][0] = pack_h2(v[0], v[1]);
-          pk[g][1] = pack_h2(v[2], v[3]);
-        }
-        const int64_t tok = q0 + wq * 128 + nb * 32 + r;
-#pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
-          // pair (2 gp, 2 gp + 1): lane h = 0 ends with group 2 gp (features 8 (2 gp) .. + 7),
-          // lane h = 1 with group 2 gp + 1
-          const int g0 = 2 * gp, g1 = 2 * gp + 1;
-          const uint32_t s0 = h ? pk[g0][0] : pk[g1][0];
-          const uint32_t s1 = h ? pk[g0][1] : pk[g1][1];
-          const uint32_t r0 = lane_xor32(s0), r1 = lane_xor32(s1);
-          const u32x4 st = h ? u32x4{r0, r1, pk[g1][0], pk[g1][1]}
-                             : u32x4{pk[g0][0], pk[g0][1], r0, r1};
-          if (tok < m)
-            *reinterpret_cast<u32x4*>(out + (size_t)tok * n + f0 + 32 * mb + 8 * (g0 + h)) = st;
-        }
-      }
-    }
-  };
-
-  issue_bias(cur, 0);
-#pragma unroll
-  for (int st = 0; st < 3; ++st)  // KT >= 4: the first three stages are tile 0's
-#pragma unroll
-    for (int p = 0; p < 8; ++p) issue_piece(cur, st, st, p);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) read_item(0, 0, i);
-  frags_ready(0);
-  __builtin_amdgcn_sched_barrier(0);
-  int ring = 0;  // ring slot of stage s (s mod 4)
-  for (int64_t j = 0; j < my_tiles; ++j) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x16{};
-    for (int kt = 0; kt < KT; ++kt) {
-      // stage s + 3: K-offset kt + 3 of this tile, or of the next one
-      const bool ahead = kt + 3 >= KT;
-      const int t3 = ahead ? kt + 3 - KT : kt + 3;
-      const Src& s3src = ahead ? nxt : cur;
-      const int ring3 = (ring + 3) & 3;
-      if (ahead && t3 == 0) issue_bias(nxt, j + 1);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc[i >> 2][i & 3] = mma(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
-        if (i < 8) read_item(ring, 1, i);
-        if (i >= 8 && (i & 1)) issue_piece(s3src, ring3, t3, (i - 8) >> 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      frags_ready(1);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc[i >> 2][i & 3] = mma(fa[1][i >> 2], fb[1][i & 3], acc[i >> 2][i & 3]);
-        if (i < 8) read_item((ring + 1) & 3, 0, i);
-        if (i >= 8 && (i & 1)) issue_piece(s3src, ring3, t3, 4 + ((i - 8) >> 1));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      ring = (ring + 1) & 3;
-      frags_ready(0);
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) asm volatile("" : "+a"(acc[mb][nb]));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    epilogue(j);
-    __builtin_amdgcn_sched_barrier(0);
-    cur = nxt;
-    nxt = tile_src(j + 2);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail stages land before exit
-}
 
 }  // namespace
 
@@ -719,34 +462,6 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
   return tl.end();
 }
 
-
-int armi_enc_linear_w4_f16(const uint16_t* x, const uint16_t* w, const float* bias,
-                           uint16_t* out, int64_t m, int n, int k, int epilogue,
-                           hipStream_t stream) {
-  ARMI_REQUIRE(n >= kW4T && n % kW4T == 0, "enc_linear_w4_f16: n must be a multiple of 256");
-  ARMI_REQUIRE(k >= 128 && k % 32 == 0 && k <= 8192,
-               "enc_linear_w4_f16: k must be a multiple of 32 in [128, 8192]");
-  ARMI_REQUIRE(epilogue == ARMI_EPI_BIAS || epilogue == ARMI_EPI_BIAS_GELU,
-               "enc_linear_w4_f16: unknown epilogue");
-  if (m <= 0) return ARMI_OK;
-  ARMI_REQUIRE(x && w && bias && out, "enc_linear_w4_f16: null pointer argument");
-  const int n_tp = n / kW4T;
-  const int64_t n_tiles = (m + kW4T - 1) / kW4T * n_tp;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    ARMI_HIP(hipGetDevice(&dev));
-    ARMI_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int grid = (int)std::min<int64_t>(n_tiles, cus);
-  auto kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_w4_kernel<1> : linear_w4_kernel<0>;
-  if (int rc = armi::allow_lds(kern, kW4Lds)) return rc;
-  armi::TimedLaunch tl;
-  if (tl.begin(ARMI_TIMING_ENCODER_GEMM, stream) < 0) return ARMI_ERR_HIP;
-  kern<<<dim3(grid), dim3(kW4Threads), kW4Lds, stream>>>(x, w, bias, out, m, n, k, n_tp, n_tiles);
-  ARMI_LAUNCHED("linear_w4_kernel");
-  return tl.end();
-}
 
 int armi_enc_linear_small_f16(const uint16_t* x, const uint16_t* w, const float* bias,
                               uint16_t* out, int m, int n, int k, int epilogue,

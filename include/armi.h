@@ -389,12 +389,6 @@ int armi_enc_gelu_f16(uint16_t* x, const float* bias, int64_t n_rows, int width,
 #define ARMI_EPI_BIAS_GELU 1
 int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out,
                         int64_t m, int n, int k, int epilogue, hipStream_t stream);
-/* The same layer on the four-wave form (round 5): 256 x 256 output tiles, one wave per SIMD
- * owning 128 x 128 of it on v_mfma_f32_32x32x16_f16 (half the LDS fragment reads per MFMA of
- * armi_enc_linear_f16). n % 256 == 0, k % 32 == 0, 128 <= k <= 8192. */
-int armi_enc_linear_w4_f16(const uint16_t* x, const uint16_t* w, const float* bias,
-                           uint16_t* out, int64_t m, int n, int k, int epilogue,
-                           hipStream_t stream);
 /* The same layer for the query encodes of BGE-M3 (embeddings/bge.py:137-157 through
  * embeddings/xlmr_f16.py): a weight stream, 16 output columns x 32 token rows per workgroup, K
  * split over its 8 (16 for k = 3072 / 4096) waves and summed in a fixed order. A row's result

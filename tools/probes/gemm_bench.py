@@ -1,4 +1,4 @@
-"""armi_enc_linear_f16 and armi_enc_linear_w4_f16 (hand-written gfx950 GEMMs, fused bias / bias +
+"""armi_enc_linear_f16 (hand-written gfx950 GEMM, fused bias / bias +
 exact GELU) against torch's hipBLASLt linear (+ the standalone armi GELU pass) on the
 cross-encoder's four GEMM shapes at configs[2]'s token count (1280 pairs x 256 tokens). Prints
 one JSON line per shape."""
@@ -50,13 +50,8 @@ def main():
                 call("armi_enc_gelu_f16", ptr(y), None, M, n, s)
             return y
 
-        out4 = torch.empty((M, n), dtype=torch.float16, device=dev)
-
-        def w4():
-            call("armi_enc_linear_w4_f16", ptr(x), ptr(w), ptr(b), ptr(out4), M, n, k, epi, s)
 
         ta = timeit(armi)
-        t4 = timeit(w4)
         tl = timeit(lt) if not os.environ.get("GEMM_NO_LT") else float("nan")
         flops = 2.0 * M * n * k
         # correctness on a slice (first and last tokens)
@@ -65,14 +60,12 @@ def main():
             ref = x[sl].float() @ w.float().t() + b
             if epi:
                 ref = torch.nn.functional.gelu(ref)
-            errs.append(max((out[sl].float() - ref).abs().max().item(),
-                            (out4[sl].float() - ref).abs().max().item()))
+            errs.append((out[sl].float() - ref).abs().max().item())
         print(json.dumps({"shape": name, "m": M, "n": n, "k": k, "epilogue": ["bias", "bias+gelu"][epi],
                           "armi_ms": ta, "armi_tflops": flops / ta / 1e9,
-                          "w4_ms": t4, "w4_tflops": flops / t4 / 1e9,
                           "hipblaslt_ms": tl, "hipblaslt_tflops": flops / tl / 1e9,
                           "max_abs_err_vs_fp32": max(errs)}), flush=True)
-        del x, w, out, out4
+        del x, w, out
 
 
 if __name__ == "__main__":
