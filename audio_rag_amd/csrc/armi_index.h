@@ -73,9 +73,6 @@ struct armi_sparse_index {
   int64_t dense_stride = 0;      // words per column (rows rounded up, + one tile of zeros)
   int32_t* dense_of = nullptr;   // [vocab] column of the term, -1
   uint32_t* dense_val = nullptr; // [n_dense][dense_stride]
-  // Round 5: the smallest value (0 when some value is <= 0; +inf without postings). A positive
-  // index lets a pass with positive weights run the register scan (sparse_scan_reg_kernel).
-  float min_value = __builtin_inff();
 };
 
 namespace armi {

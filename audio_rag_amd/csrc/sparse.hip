@@ -63,7 +63,6 @@ constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + wei
 constexpr int kBitmapVocab = 1 << 18;   // vocabularies up to which a pass numbers its terms by bitmap
 constexpr int kBmWords = kBitmapVocab / 32;
 constexpr size_t kPrepBmLds = (size_t)kBmWords * 8;    // term bitmap + per-word prefix, 64 KB
-                                                       // (build_groups: kGroupLds, 80 KB)
 constexpr int32_t kEndRow = 0x7fffffff;
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 static_assert(kQW * kKW == 64, "one 16-lane list segment per query of the wave");
@@ -78,19 +77,12 @@ __global__ void entry_rows_kernel(const int64_t* __restrict__ indptr, int64_t n_
     row_of[e] = (int32_t)r;
 }
 
-// bad[0] += non-finite values; bad[1] = min over the values of (v > 0 ? bits(v) : 0) (the bits
-// of positive floats order as uint32): 0 when some value is <= 0, else the smallest value's bits
 __global__ void count_nonfinite_kernel(const float* __restrict__ values, int64_t nnz,
                                        unsigned long long* __restrict__ bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const float v = i < nnz ? values[i] : 1.f;
-  const bool b = !isfinite(v);
+  const bool b = i < nnz && !isfinite(values[i]);
   const unsigned long long m = __ballot(b);
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
-  unsigned long long key = v > 0.f ? (unsigned long long)__float_as_uint(v) : 0ull;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) key = min(key, (unsigned long long)__shfl_xor(key, o));
-  if ((threadIdx.x & 63) == 0) atomicMin(bad + 1, key);
 }
 
 __global__ void term_keys_kernel(const int32_t* __restrict__ indices, int64_t nnz, int32_t vocab,
@@ -262,174 +254,6 @@ __device__ __forceinline__ void deal_queries(const int32_t* __restrict__ q_indpt
   qof[slot] = r < nq ? q : -1;
 }
 
-// ------------------------------------------------------------------ group lists (register scan)
-//
-// The register scan (sparse_scan_reg_kernel) gives each wave a group of kGQ = 8 query slots
-// (slots 8 g .. 8 g + 7; the snake deal above balances their term counts) and walks the
-// group's distinct terms once per tile. Per group g:
-//   gn[g]                          distinct terms (ascending u), j = 0 .. gn - 1
-//   gdesc[g][j]                    -(d + 1) for a dense column d, else the term id
-//   goff[g][j] .. goff[g][j + 1]   the term's (weight, 2 * slot) pairs in gpair[g][.], their count
-//                                  rounded up to even with a (0, 0) pair (adds +0 to slot 0)
-// plus the pass's `plain` word: every weight of the pass is finite and > 0 and fl32(min weight *
-// min index value) is a normal float (the index's values are all > 0), so every product of a
-// shared term is > 0 and a row shares a term with a query iff its fp32 sum is > 0, and every group
-// fits the register scan's LDS lists (kRegMaxU, kRegMaxP). The register scan needs both (it keeps
-// no hit bits); other passes run sparse_scan_kernel.
-constexpr int kGQ = 8;                   // query slots per group (= per wave of the register scan)
-constexpr int kGroups = kQB / kGQ;       // 8
-constexpr int kGThreads = 1024 / kGroups;  // build_groups: threads per group
-constexpr int kGWaves = kGThreads / 64;
-constexpr int kGMaxU = kGQ * kMaxTerms;  // distinct terms of a group, at most
-constexpr int kGPairs = 2 * kGMaxU;      // pair slots of a group (counts rounded up to even)
-constexpr int kGOffStride = kGMaxU + 16; // goff entries per group (+ slack for batch reads)
-constexpr int kGWords = kMaxU / 32;      // u-bitmap words per group
-constexpr size_t kGroupLds = (size_t)kGroups * kGWords * 4 * 2 + (size_t)kGroups * kGMaxU * 4;
-// the register scan holds a group's lists in LDS: at most kRegMaxU terms and kRegMaxP pair slots
-// (BGE-M3 queries: ~10-30 terms, so a group stays below ~250 / ~300); larger passes are not plain
-constexpr int kRegMaxU = 512;
-constexpr int kRegMaxP = 1024;
-constexpr size_t kPrepBmLaunchLds = kPrepBmLds > kGroupLds ? kPrepBmLds : kGroupLds;
-static_assert(kPrepLds >= kGroupLds, "pass_terms_kernel's LDS holds the group build");
-
-struct alignas(8) GPair {
-  float w;
-  int32_t q2;  // 2 * (slot within the group): the accumulator pair of the slot
-};
-
-struct GroupLists {
-  int32_t* gn;     // [kGroups], then [kGroups] = plain
-  int32_t* gdesc;  // [kGroups][kGMaxU]
-  int32_t* goff;   // [kGroups][kGOffStride]
-  GPair* gpair;    // [kGroups][kGPairs]
-};
-
-// All 1024 threads of a pass_terms block, after the slot lists (ql, qu, qcount, qof) are written
-// by this block (read back after a barrier: same CU, write-through L1). smem >= kGroupLds.
-__device__ void build_groups(int tid, unsigned char* smem, const int32_t* __restrict__ uterm,
-                             const QTerm* __restrict__ ql, const int32_t* __restrict__ qu,
-                             const int32_t* __restrict__ qcount, const int32_t* __restrict__ dense_of,
-                             float min_value, GroupLists gl) {
-  uint32_t* gb = reinterpret_cast<uint32_t*>(smem);                    // [kGroups][kGWords]
-  int32_t* gpre = reinterpret_cast<int32_t*>(smem + kGroups * kGWords * 4);  // [kGroups][kGWords]
-  int32_t* gcnt = reinterpret_cast<int32_t*>(smem + kGroups * kGWords * 8);  // [kGroups][kGMaxU]
-  __shared__ int32_t wsum[16];
-  __shared__ uint32_t min_w;
-  __shared__ int32_t bad, over;
-  const int lane = tid & 63, wave = tid >> 6;
-  __syncthreads();  // the slot lists are written; smem's previous use is over
-  for (int i = tid; i < kGroups * kGWords; i += 1024) gb[i] = 0u;
-  for (int i = tid; i < kGroups * kGMaxU; i += 1024) gcnt[i] = 0;
-  if (tid == 0) {
-    min_w = 0x7f800000u;
-    bad = 0;
-    over = 0;
-  }
-  __syncthreads();
-  // entries: slot s = tid / 16 walks its list with stride 16
-  const int s = tid >> 4, e0 = tid & 15, g = s / kGQ;
-  const int ns = qcount[s];
-  for (int e = e0; e < ns; e += 16) {
-    const int u = qu[s * kQStride + e];
-    const float w = ql[s * kQStride + e].w;
-    atomicOr(&gb[g * kGWords + (u >> 5)], 1u << (u & 31));
-    if (!(w > 0.f) || !(w <= 3.402823466e38f)) bad = 1;
-    else atomicMin(&min_w, __float_as_uint(w));
-  }
-  __syncthreads();
-  // per group: exclusive prefix of the words' set-bit counts (256 threads, 2 words each) and the
-  // descriptor of every distinct term
-  {
-    constexpr int kPer = kGWords / kGThreads;  // words per thread
-    const int gg = tid / kGThreads, wi = (tid % kGThreads) * kPer;
-    uint32_t wv[kPer];
-    int c = 0;
-#pragma unroll
-    for (int h = 0; h < kPer; ++h) {
-      wv[h] = gb[gg * kGWords + wi + h];
-      c += __popc(wv[h]);
-    }
-    int x = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(x, d);
-      if (lane >= d) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    int before = x - c;
-    for (int v = gg * kGWaves; v < wave; ++v) before += wsum[v];
-    if (tid % kGThreads == kGThreads - 1) gl.gn[gg] = before + c;
-    int r = before;
-#pragma unroll
-    for (int h = 0; h < kPer; ++h) {
-      gpre[gg * kGWords + wi + h] = r;
-      uint32_t b = wv[h];
-      while (b) {
-        const int u = (wi + h) * 32 + __builtin_ctz(b);
-        const int32_t t = uterm[u];
-        const int32_t d = dense_of[t];
-        gl.gdesc[gg * kGMaxU + r++] = d >= 0 ? -(d + 1) : t;
-        b &= b - 1u;
-      }
-    }
-  }
-  __syncthreads();
-  auto rank = [&](int u) {
-    return gpre[g * kGWords + (u >> 5)] + __popc(gb[g * kGWords + (u >> 5)] & ((1u << (u & 31)) - 1u));
-  };
-  for (int e = e0; e < ns; e += 16) atomicAdd(&gcnt[g * kGMaxU + rank(qu[s * kQStride + e])], 1);
-  __syncthreads();
-  // per group: offsets of the even-rounded counts (256 threads, 16 consecutive terms each), the
-  // (0, 0) pad pairs; gcnt becomes the fill pointer
-  {
-    constexpr int kPer = kGMaxU / kGThreads;  // terms per thread
-    const int gg = tid / kGThreads, j0 = (tid % kGThreads) * kPer;
-    const int n = gl.gn[gg];
-    int c[kPer], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      c[i] = j0 + i < n ? gcnt[gg * kGMaxU + j0 + i] : 0;
-      sum += (c[i] + 1) & ~1;
-    }
-    int x = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(x, d);
-      if (lane >= d) x += y;
-    }
-    __syncthreads();  // wsum's previous use is over
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    int off = x - sum;
-    for (int v = gg * kGWaves; v < wave; ++v) off += wsum[v];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int j = j0 + i;
-      if (j < n) {
-        gl.goff[gg * kGOffStride + j] = off;
-        gcnt[gg * kGMaxU + j] = off;
-        if (c[i] & 1) gl.gpair[gg * kGPairs + off + c[i]] = GPair{0.f, 0};
-      }
-      off += (c[i] + 1) & ~1;
-    }
-    if (tid % kGThreads == kGThreads - 1) {
-      gl.goff[gg * kGOffStride + n] = off;  // the group's pair total
-      if (n > kRegMaxU || off > kRegMaxP) over = 1;
-    }
-  }
-  __syncthreads();
-  for (int e = e0; e < ns; e += 16) {
-    const int p = atomicAdd(&gcnt[g * kGMaxU + rank(qu[s * kQStride + e])], 1);
-    gl.gpair[g * kGPairs + p] = GPair{ql[s * kQStride + e].w, 2 * (s & (kGQ - 1))};
-  }
-  if (tid == 0) {
-    const float mw = __uint_as_float(min_w);
-    // fl32(min w * min value) >= FLT_MIN: every product of the pass is a normal float > 0
-    gl.gn[kGroups] = (!bad && !over && min_value > 0.f && mw * min_value >= 1.17549435e-38f) ? 1 : 0;
-  }
-}
-
 // The pass's query terms when vocab <= kBitmapVocab (BGE-M3: 250 002), without a sort: the
 // distinct terms are the set bits of an LDS bitmap over the vocabulary, u(t) = the number of set
 // bits below t (per-word prefix counts + a popcount), and since every query's indices ascend
@@ -440,7 +264,6 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl,
     int32_t* __restrict__ coll_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem);               // [kBmWords]
@@ -532,7 +355,6 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     if (lane < kBatch) ql[slot * kQStride + m + lane] = QTerm{0.f, 0};
     if (lane == 0) qcount[slot] = m;
   }
-  if (gl.gn) build_groups(tid, smem, uterm, ql, qu, qcount, dense_of, min_value, gl);
 }
 
 // One block for the pass. Sorts the pass's (term, query) pairs by (term, slot) where query q sits
@@ -545,7 +367,6 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    const int32_t* __restrict__ dense_of, float min_value, GroupLists gl,
     int32_t* __restrict__ coll_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
@@ -690,7 +511,6 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     if (lane < kBatch) ql[(wave * kQW + i) * kQStride + run[i] + lane] = QTerm{0.f, 0};
   if (lane < kQW)
     qcount[wave * kQW + lane] = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
-  if (gl.gn) build_groups(tid, smem, uterm, ql, qu, qcount, dense_of, min_value, gl);
 }
 
 // ------------------------------------------------------------------------- scan
@@ -769,10 +589,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
     int32_t* __restrict__ coll_row, int dbg, const int32_t* __restrict__ dense_of,
-    const uint32_t* __restrict__ dense_val, int64_t dense_stride,
-    const int32_t* __restrict__ skip) {
+    const uint32_t* __restrict__ dense_val, int64_t dense_stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][kTile]
-  if (skip && *skip) return;  // a plain pass, scanned by sparse_scan_reg_kernel
   const int g = blockIdx.x;
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
@@ -1178,381 +996,6 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   }
 }
 
-// ------------------------------------------------------------------------- register scan
-//
-// Round 5, for plain passes (build_groups): workgroup = one row range, wave = one group of 16
-// query slots, lane = two adjacent rows of a 128-row tile, no barriers. Per tile the wave walks
-// its group's distinct terms in ascending u, 8 per batch: a dense column's two values come
-// straight from HBM into registers (one 8-B load per lane), a posting list's in-tile postings
-// are scattered into a wave-private LDS row and read back. Then every (weight, slot) pair of the
-// term adds fl32(w * v) into the slot's pair of fp32 accumulators: one packed multiply and one
-// packed add whose accumulator operand is selected by the slot through VGPR index mode
-// (s_set_gpr_idx_on), so the 32 accumulators stay in registers however the pairs fall. Each
-// (row, query) sum therefore runs over the query's terms in ascending order, as the oracle and
-// Qdrant sum them; a term without a posting in the row adds fl32(w * 0) = +0, which leaves a
-// positive sum unchanged. The loads of the next kRD batches are in flight while a batch is summed.
-// Against sparse_scan_kernel: each staged value is read once per group that uses it instead of
-// once per (query, term) pair through LDS, and no block-wide barrier per tile.
-constexpr int kRB = 8;            // group terms per batch
-constexpr int kRD = 3;            // batches whose loads are in flight ahead of the summed one
-constexpr int kRRing = kRD + 1;
-constexpr int kRegThreads = kGroups * 64;
-// LDS per wave: its group's cursors, term offsets (+ 16 past the end for batch reads) and pairs
-// (+ 8 for the reads past a list), 8 scatter rows and a scratch row
-constexpr size_t kRegCurBytes = (size_t)kRegMaxU * 8;
-constexpr size_t kRegOffBytes = (size_t)(kRegMaxU + 16) * 4;
-constexpr size_t kRegPairBytes = (size_t)(kRegMaxP + 8) * 8;
-constexpr size_t kRegImgBytes = (size_t)kRB * kTile * 4 + 64 * 4;
-constexpr size_t kRegWaveLds = kRegCurBytes + kRegOffBytes + kRegPairBytes + kRegImgBytes;
-constexpr size_t kRegLds = kGroups * kRegWaveLds;  // 8 x 18.3 KB
-typedef float v16f __attribute__((ext_vector_type(16)));
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-
-template <int R>
-struct Slot {
-  static constexpr int value = R;
-};
-
-__global__ __launch_bounds__(kRegThreads) void sparse_scan_reg_kernel(
-    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
-    const int32_t* __restrict__ long_of, const int32_t* __restrict__ start_tab, int64_t n_rows,
-    int64_t range_rows, int n_ranges, const uint64_t* __restrict__ row_mask,
-    const int32_t* __restrict__ gn, const int32_t* __restrict__ gdesc,
-    const int32_t* __restrict__ goff, const GPair* __restrict__ gpair,
-    const int32_t* __restrict__ qof, const uint32_t* __restrict__ dense_val, int64_t dense_stride,
-    float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
-  if (gn[kGroups] == 0) return;  // not a plain pass: sparse_scan_kernel scans it
-  const int g = blockIdx.x;
-  const int grp = armi::wave_id();
-  const int lane = threadIdx.x & 63;
-  unsigned char* const wl = rsm + grp * kRegWaveLds;
-  int2* const cur = reinterpret_cast<int2*>(wl);
-  int32_t* const loff = reinterpret_cast<int32_t*>(wl + kRegCurBytes);
-  int4* const lpair = reinterpret_cast<int4*>(wl + kRegCurBytes + kRegOffBytes);  // 2 pairs each
-  float* const img = reinterpret_cast<float*>(wl + kRegCurBytes + kRegOffBytes + kRegPairBytes);
-  float* const trash = img + kRB * kTile + lane;
-  const int n = gn[grp];
-  const int64_t lo = (int64_t)g * range_rows;
-  const int64_t hi = min(lo + range_rows, n_rows);
-  const int n_tiles = hi > lo && n > 0 ? (int)((hi - lo + kTile - 1) / kTile) : 0;
-  const int32_t* const D = gdesc + grp * kGMaxU;
-  const int32_t* const O = goff + grp * kGOffStride;
-  const GPair* const P = gpair + grp * kGPairs;
-
-  // cursors: a dense column keeps (-(d + 1), 0); a posting list its first posting at or after lo;
-  // the term offsets and the pairs (even counts: 16-B pairs of pairs) into LDS
-  for (int j = lane; j < n; j += 64) {
-    const int32_t d = D[j];
-    cur[j] = d < 0 ? make_int2(d, 0)
-                   : range_cursor(d, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
-  }
-  for (int j = lane; j <= n; j += 64) loff[j] = O[j];
-  const int np = n > 0 ? O[n] : 0;
-  for (int p = lane; 2 * p < np; p += 64) lpair[p] = reinterpret_cast<const int4*>(P)[p];
-  // (a wave's LDS operations complete in order: the reads below see these writes)
-
-  float l1s[kGQ], l2s[kGQ], disc[kGQ];
-  int32_t l1r[kGQ], l2r[kGQ];
-#pragma unroll
-  for (int i = 0; i < kGQ; ++i) {
-    l1s[i] = kNegInf;
-    l2s[i] = kNegInf;
-    disc[i] = kNegInf;
-    l1r[i] = kEndRow;
-    l2r[i] = kEndRow;
-  }
-  v16f acc = 0.f;  // slot i: rows 2 lane (2 i) and 2 lane + 1 (2 i + 1) of the tile
-  u2v raw[kRRing][kRB];
-  uint32_t am[kRRing], dm[kRRing];  // per ring slot: terms with data, dense columns
-#pragma unroll
-  for (int r = 0; r < kRRing; ++r) {
-    am[r] = 0u;
-    dm[r] = 0u;
-  }
-
-  const int nb = (n + kRB - 1) / kRB;
-  const int nbp = max(nb, kRD);  // >= kRD batches per tile: a cursor is never read before its
-                                 // previous tile's update (issue runs kRD batches ahead)
-  const int S = n_tiles * nbp;
-  auto tile_lo = [&](int t) __attribute__((always_inline)) { return lo + (int64_t)t * kTile; };
-  auto tile_hi = [&](int t) __attribute__((always_inline)) { return (int32_t)min(lo + (int64_t)(t + 1) * kTile, hi); };
-
-  // Every batch issues exactly kRB loads (a term without data loads posting 0..63, unused), so the
-  // compiler's counted waits keep the next batches in flight.
-  auto issue = [&](auto slot, int t, int b) __attribute__((always_inline)) {
-    constexpr int r = decltype(slot)::value;
-    uint32_t a = 0u, dd = 0u;
-    const bool live = t < n_tiles;
-    const int64_t tlo = tile_lo(t);
-    const int32_t thi = tile_hi(t);
-    int4 cq[kRB / 2];  // the batch's cursors, read together (past n: unused)
-#pragma unroll
-    for (int h = 0; h < kRB / 2; ++h) cq[h] = reinterpret_cast<const int4*>(cur + b * kRB)[h];
-#pragma unroll
-    for (int k = 0; k < kRB; ++k) {
-      const int j = b * kRB + k;
-      const int32_t cx = __builtin_amdgcn_readfirstlane((k & 1) ? cq[k >> 1].z : cq[k >> 1].x);
-      const int32_t cy = __builtin_amdgcn_readfirstlane((k & 1) ? cq[k >> 1].w : cq[k >> 1].y);
-      const bool on = live && j < n;
-      const bool dense = on && cx < 0;
-      const bool sparse = on && cx >= 0 && cy < thi;
-      a |= (dense || sparse ? 1u : 0u) << k;
-      dd |= (dense ? 1u : 0u) << k;
-      const size_t col = dense ? (size_t)(-cx - 1) : 0;
-      const int32_t pc = sparse ? cx : 0;
-      const u2v* src = dense ? reinterpret_cast<const u2v*>(dense_val + col * dense_stride + tlo +
-                                                            2 * lane)
-                             : reinterpret_cast<const u2v*>(post + pc + 63 - lane);
-      raw[r][k] = *src;
-    }
-    am[r] = a;
-    dm[r] = dd;
-  };
-
-  // the batch's values: dense columns from the loads, posting lists scattered to their LDS rows
-  // (lane l holds posting c + 63 - l; the in-tile postings are a prefix of the list, i.e. the
-  // lanes from 63 down) and read back; the cursors advance past the tile
-  auto values = [&](auto slot, int t, int b, f2 (&vv)[kRB]) __attribute__((always_inline)) {
-    constexpr int r = decltype(slot)::value;
-    const int64_t tlo = tile_lo(t);
-    const int32_t thi = tile_hi(t);
-    const uint32_t sm = am[r] & ~dm[r];
-#pragma unroll
-    for (int k = 0; k < kRB; ++k) {
-      if ((sm >> k) & 1u) {
-        const int j = b * kRB + k;
-        float* const row = img + k * kTile;
-        reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
-        int32_t c = __builtin_amdgcn_readfirstlane(cur[j].x);
-        auto scatter = [&](u2v w) __attribute__((always_inline)) {
-          const uint64_t be = __ballot((int32_t)w.x < thi);
-          const int m = be == ~0ull ? 64 : __builtin_clzll(~be);  // in-tile postings here
-          float* const d0 = 63 - lane < m ? row + ((int32_t)w.x - (int32_t)tlo) : trash;
-          *d0 = __uint_as_float(w.y);
-          c += m;
-          return m;
-        };
-        const u2v w = raw[r][k];
-        const int m = scatter(w);
-        int32_t nr;
-        if (m < 64) {
-          nr = rl_i((int32_t)w.x, 63 - m);
-        } else {
-          // 64 in-tile postings: the tile may hold more (rare: a term below 1/8 of the rows).
-          // Each window's load is consumed in its own trip, so no load is left in flight here.
-          u2v w2;
-          int m2;
-          do {
-            w2 = *reinterpret_cast<const u2v*>(post + c + 63 - lane);
-            m2 = scatter(w2);
-          } while (m2 == 64);
-          nr = rl_i((int32_t)w2.x, 63 - m2);
-        }
-        if (lane == 0) cur[j] = make_int2(c, nr);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kRB; ++k) {
-      if ((sm >> k) & 1u) {
-        vv[k] = reinterpret_cast<const f2*>(img + k * kTile)[lane];
-      } else {
-        vv[k] = f2{__uint_as_float(raw[r][k].x), __uint_as_float(raw[r][k].y)};
-      }
-    }
-  };
-
-  // acc[q2], acc[q2 + 1] += x (q2 uniform, even): the accumulator operand through index mode
-  auto add_pair = [&](int32_t q2, f2 x) __attribute__((always_inline)) {
-    asm volatile(
-        "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
-        "v_pk_add_f32 v[64:65], v[64:65], %2\n\t"
-        "s_set_gpr_idx_off"
-        : "+{v[64:79]}"(acc)
-        : "s"(q2), "v"(x));  // (M0, which index mode rewrites, is reserved: no other use here)
-  };
-
-  // the batch's pairs from LDS (broadcast reads of two pairs, the next two requested before the
-  // current two are summed); the weight stays a VGPR operand, the slot goes to an SGPR
-  auto sum_pairs = [&](auto slot, int b, const f2 (&vv)[kRB]) __attribute__((always_inline)) {
-    constexpr int r = decltype(slot)::value;
-    const uint32_t a = am[r];
-    if (a == 0u) return;
-    int o[kRB + 1];
-#pragma unroll
-    for (int k = 0; k <= kRB; ++k) o[k] = __builtin_amdgcn_readfirstlane(loff[b * kRB + k]);
-    // a term's first 8 pairs in 4 reads, the next active term's requested before this one's math
-    int4 cp[4], np[4];
-    auto fetch = [&](int p2, int4 (&t)[4]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int h = 0; h < 4; ++h) t[h] = lpair[p2 + h];  // (past the term: unused)
-    };
-    auto two = [&](const int4& t, const f2& v) __attribute__((always_inline)) {
-      const float wa = __int_as_float(t.x), wb = __int_as_float(t.z);
-      add_pair(__builtin_amdgcn_readfirstlane(t.y), v * f2{wa, wa});
-      add_pair(__builtin_amdgcn_readfirstlane(t.w), v * f2{wb, wb});
-    };
-    fetch(o[__builtin_ctz(a)] >> 1, cp);
-#pragma unroll
-    for (int k = 0; k < kRB; ++k) {
-      if ((a >> k) & 1u) {
-        const uint32_t later = a & ~((2u << k) - 1u);
-        if (later) fetch(o[__builtin_ctz(later)] >> 1, np);
-        const int p2 = o[k] >> 1, n2 = (o[k + 1] >> 1) - p2;  // pairs of pairs, >= 1
-        two(cp[0], vv[k]);
-        if (n2 > 1) two(cp[1], vv[k]);
-        if (n2 > 2) two(cp[2], vv[k]);
-        if (n2 > 3) two(cp[3], vv[k]);
-        for (int h = 4; h < n2; ++h) two(lpair[p2 + h], vv[k]);  // > 8 pairs: rare
-#pragma unroll
-        for (int h = 0; h < 4; ++h) cp[h] = np[h];
-      }
-    }
-  };
-
-  auto candidates = [&](int t) __attribute__((always_inline)) {
-    const int64_t tlo = tile_lo(t);
-    const int32_t thi = tile_hi(t);
-    const int32_t r0 = (int32_t)tlo + 2 * lane;
-    uint64_t m0 = ~0ull, m1 = ~0ull;
-    if (row_mask) {
-      m0 = row_mask[tlo >> 6];
-      m1 = tlo + 64 < hi ? row_mask[(tlo >> 6) + 1] : 0ull;
-    }
-    const uint64_t mw = lane < 32 ? m0 : m1;
-    const bool ok0 = ((mw >> ((2 * lane) & 63)) & 1ull) && r0 < thi;
-    const bool ok1 = ((mw >> ((2 * lane + 1) & 63)) & 1ull) && r0 + 1 < thi;
-#pragma unroll
-    for (int i = 0; i < kGQ; ++i) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float sc = acc[2 * i + h];
-        // plain pass: a row shares a term with the query iff its sum is > 0
-        const float x = (h == 0 ? ok0 : ok1) && sc > 0.f ? sc : kNegInf;
-        const int32_t rr = r0 + h;
-        const bool c1 = x > l1s[i];
-        const bool c2 = x > l2s[i];
-        disc[i] = fmaxf(disc[i], c2 ? l2s[i] : x);
-        l2s[i] = c1 ? l1s[i] : (c2 ? x : l2s[i]);
-        l2r[i] = c1 ? l1r[i] : (c2 ? rr : l2r[i]);
-        l1s[i] = c1 ? x : l1s[i];
-        l1r[i] = c1 ? rr : l1r[i];
-      }
-    }
-    acc = 0.f;
-  };
-
-  // prologue: the first kRD batches in flight
-  int it = 0, ib = 0;  // next batch to issue
-  auto advance = [&](int& t, int& b) __attribute__((always_inline)) {
-    if (++b == nbp) {
-      b = 0;
-      ++t;
-    }
-  };
-  if (S > 0) {
-    issue(Slot<0>{}, it, ib);
-    advance(it, ib);
-    issue(Slot<1>{}, it, ib);
-    advance(it, ib);
-    issue(Slot<2>{}, it, ib);
-    advance(it, ib);
-  }
-  static_assert(kRD == 3 && kRRing == 4, "the prologue and the ring below are unrolled for 3 + 1");
-  int pt = 0, pb = 0;  // batch being summed
-  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long t_a = 0, t_b = 0;
-  (void)tp;
-  (void)t_a;
-  (void)t_b;
-  auto step = [&](auto slot, auto next) __attribute__((always_inline)) {
-    f2 vv[kRB];
-    ARMI_PROF_T(t_a);
-    values(slot, pt, pb, vv);
-    ARMI_PROF_T(t_b);
-    ARMI_PROF_ADD(3, t_a, t_b);
-    issue(next, it, ib);
-    advance(it, ib);
-    ARMI_PROF_T(t_a);
-    ARMI_PROF_ADD(0, t_b, t_a);
-    sum_pairs(slot, pb, vv);
-    ARMI_PROF_T(t_b);
-    ARMI_PROF_ADD(1, t_a, t_b);
-    if (pb == nbp - 1) candidates(pt);
-    ARMI_PROF_T(t_a);
-    ARMI_PROF_ADD(2, t_b, t_a);
-    advance(pt, pb);
-  };
-  for (int s0 = 0; s0 < S; s0 += kRRing) {
-    step(Slot<0>{}, Slot<3>{});
-    if (s0 + 1 >= S) break;
-    step(Slot<1>{}, Slot<0>{});
-    if (s0 + 2 >= S) break;
-    step(Slot<2>{}, Slot<1>{});
-    if (s0 + 3 >= S) break;
-    step(Slot<3>{}, Slot<2>{});
-  }
-
-#ifdef ARMI_SPARSE_PROFILE
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) g_sparse_prof[((size_t)g * kWaves + grp) * 8 + i] = tp[i];
-    g_sparse_prof[((size_t)g * kWaves + grp) * 8 + 6] = n;
-    g_sparse_prof[((size_t)g * kWaves + grp) * 8 + 7] = S;
-  }
-#endif
-  // per query slot: top 16 of the 128 lane entries (as sparse_scan_kernel), four slots at a time
-#pragma unroll
-  for (int i0 = 0; i0 < kGQ; i0 += kQW) {
-    float ka[kQW], kb[kQW], ck[kQW], bq[kQW];
-    int32_t ra[kQW], rb[kQW], cr[kQW];
-#pragma unroll
-    for (int i = 0; i < kQW; ++i) {
-      ka[i] = l1s[i0 + i];
-      ra[i] = l1r[i0 + i];
-      kb[i] = l2s[i0 + i];
-      rb[i] = l2r[i0 + i];
-    }
-    armi::wave_sort_approx_desc_n<kQW>(ka, ra);
-    armi::wave_sort_approx_desc_n<kQW>(kb, rb);
-#pragma unroll
-    for (int i = 0; i < kQW; ++i) {
-      const float kbr = __shfl(kb[i], (15 - lane) & 63);
-      const int32_t rbr = __shfl(rb[i], (15 - lane) & 63);
-      const float kb16 = __shfl(kb[i], 16);
-      float lose = kNegInf;
-      ck[i] = kNegInf;
-      cr[i] = kEndRow;
-      if (lane < 16) {
-        const bool take_a = armi::approx_better(ka[i], ra[i], kbr, rbr);
-        ck[i] = take_a ? ka[i] : kbr;
-        cr[i] = take_a ? ra[i] : rbr;
-        lose = take_a ? kbr : ka[i];
-      } else if (lane == 16) {
-        lose = fmaxf(ka[i], kb16);
-      }
-      bq[i] = fmaxf(disc[i0 + i], lose);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int i = 0; i < kQW; ++i) bq[i] = fmaxf(bq[i], armi::xor_stride(bq[i], o));
-    armi::wave_sort_approx_desc_n<kQW>(ck, cr);
-#pragma unroll
-    for (int i = 0; i < kQW; ++i) {
-      const int q = qof[grp * kGQ + i0 + i];
-      if (q >= 0) {
-        const size_t base = (size_t)g * kQB + q;
-        if (lane < kKW) {
-          cand_key[base * kKW + lane] = ck[i];
-          cand_row[base * kKW + lane] = cr[i];
-        }
-        if (lane == 0) cand_bound[base] = bq[i];
-      }
-    }
-  }
-}
-
 // Order-preserving map of a float to uint32 (larger float -> larger key; -inf lowest).
 __device__ __forceinline__ uint32_t ord_key_f(float x) {
   const uint32_t u = __float_as_uint(x);
@@ -1948,7 +1391,6 @@ struct Workspace {
   int* coll_count;  // [2 * kQB]: collect counts, then the helpers' done counters
   float* coll_key;
   int32_t* coll_row;
-  GroupLists gl;
   size_t bytes;
 };
 
@@ -1970,10 +1412,6 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   w.coll_count = cv.take<int>(2 * kQB);
   w.coll_key = cv.take<float>((size_t)kQB * kCollectCap);
   w.coll_row = cv.take<int32_t>((size_t)kQB * kCollectCap);
-  w.gl.gn = cv.take<int32_t>(kGroups + 1);
-  w.gl.gdesc = cv.take<int32_t>((size_t)kGroups * kGMaxU);
-  w.gl.goff = cv.take<int32_t>((size_t)kGroups * kGOffStride);
-  w.gl.gpair = cv.take<GPair>((size_t)kGroups * kGPairs);
   w.bytes = cv.off + 256;
   return w;
 }
@@ -1993,17 +1431,6 @@ struct Scratch {
   }
 };
 
-// The register scan for indexes whose values are all > 0: probe builds only
-// (ARMI_BUILD_FLAGS=-DARMI_SPARSE_REG) until it beats sparse_scan_kernel.
-bool use_reg_scan(const armi_sparse_index* idx) {
-#ifdef ARMI_SPARSE_REG
-  return idx->min_value > 0.f && idx->n_ranges > 0;
-#else
-  (void)idx;
-  return false;
-#endif
-}
-
 unsigned grid_for(int64_t n, int block) { return (unsigned)std::max<int64_t>(1, (n + block - 1) / block); }
 
 int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t* indices,
@@ -2022,17 +1449,14 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(tmp.alloc(&scan, (size_t)vocab + 1));
   if (nnz > 0) {
     unsigned long long* bad;
-    ARMI_HIP(tmp.alloc(&bad, 2));
+    ARMI_HIP(tmp.alloc(&bad, 1));
     ARMI_HIP(hipMemsetAsync(bad, 0, 8, stream));
-    ARMI_HIP(hipMemsetAsync(bad + 1, 0xff, 8, stream));
     count_nonfinite_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(values, nnz, bad);
     ARMI_LAUNCHED("count_nonfinite_kernel");
-    unsigned long long n_bad[2] = {0, 0};
-    ARMI_HIP(hipMemcpyAsync(n_bad, bad, 16, hipMemcpyDeviceToHost, stream));
+    unsigned long long n_bad = 0;
+    ARMI_HIP(hipMemcpyAsync(&n_bad, bad, 8, hipMemcpyDeviceToHost, stream));
     ARMI_HIP(hipStreamSynchronize(stream));
-    ARMI_REQUIRE(n_bad[0] == 0, "armi_sparse_index_create: values must be finite");
-    const uint32_t mb = (uint32_t)n_bad[1];
-    idx->min_value = mb == 0u ? 0.f : __builtin_bit_cast(float, mb);
+    ARMI_REQUIRE(n_bad == 0, "armi_sparse_index_create: values must be finite");
     entry_rows_kernel<<<grid_for(idx->n_rows, 4), 256, 0, stream>>>(indptr, idx->n_rows, row_of);
     ARMI_LAUNCHED("entry_rows_kernel");
     term_keys_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(indices, nnz, vocab, keys, ent);
@@ -2275,11 +1699,9 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
   // graph-capturable)
   if (int rc = armi::allow_lds(sparse_collect_merge_kernel, kCollectLds)) return rc;
   if (int rc = armi::allow_lds(pass_terms_kernel, kPrepLds)) return rc;
-  if (int rc = armi::allow_lds(pass_terms_bitmap_kernel, kPrepBmLaunchLds)) return rc;
+  if (int rc = armi::allow_lds(pass_terms_bitmap_kernel, kPrepBmLds)) return rc;
   if (int rc = armi::allow_lds(sparse_scan_kernel<false>, kScanLds)) return rc;
   if (int rc = armi::allow_lds(sparse_scan_kernel<true>, kScanLds)) return rc;
-  if (use_reg_scan(idx))
-    if (int rc = armi::allow_lds(sparse_scan_reg_kernel, kRegLds)) return rc;
   const int n_help = std::max(1, std::min(kMaxHelp, kCollectCap / k));
   for (int q0 = 0; q0 < n_queries; q0 += kQB) {
     const int nqp = std::min(kQB, n_queries - q0);
@@ -2290,35 +1712,22 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       ARMI_HIP(hipMemsetAsync(out_ids + (size_t)q0 * k, 0xff, sizeof(int64_t) * nqp * k, stream));
       continue;
     }
-    GroupLists gl = w.gl;  // built by pass_terms only for the register scan
-    if (!use_reg_scan(idx)) gl.gn = nullptr;
     if (idx->vocab <= kBitmapVocab)
-      pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLaunchLds, stream>>>(
+      pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl, w.coll_count);
+          w.qcount, w.qof, pflags, w.coll_count);
     else
       pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, idx->dense_of, idx->min_value, gl, w.coll_count);
+          w.qcount, w.qof, pflags, w.coll_count);
     ARMI_LAUNCHED("pass_terms_kernel");
     armi::TimedLaunch tl;
     if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    // An index whose values are all > 0 launches both scans: the pass's plain word (build_groups)
-    // lets exactly one of them run, the other returns at once.
-    const bool reg = use_reg_scan(idx);
-    if (reg) {
-      sparse_scan_reg_kernel<<<dim3(idx->n_ranges), dim3(kRegThreads), kRegLds, stream>>>(
-          idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab,
-          idx->n_rows, idx->range_rows, idx->n_ranges, row_mask, w.gl.gn, w.gl.gdesc, w.gl.goff,
-          w.gl.gpair, w.qof, idx->dense_val, idx->dense_stride, w.cand_key, w.cand_row,
-          w.cand_bound);
-      ARMI_LAUNCHED("sparse_scan_reg_kernel");
-    }
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg,
-        idx->dense_of, idx->dense_val, idx->dense_stride, reg ? w.gl.gn + kGroups : nullptr);
+        idx->dense_of, idx->dense_val, idx->dense_stride);
     ARMI_LAUNCHED("sparse_scan_kernel");
     if (int rc = tl.end()) return rc;
 #ifdef ARMI_SPARSE_PROFILE
@@ -2351,7 +1760,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg,
-        idx->dense_of, idx->dense_val, idx->dense_stride, nullptr);
+        idx->dense_of, idx->dense_val, idx->dense_stride);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp + n_help), dim3(256), kCollectLds, stream>>>(
         w.coll_count, w.coll_key, w.coll_row, w.coll_count + kQB, nqp, q0,

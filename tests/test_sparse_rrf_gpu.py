@@ -276,11 +276,10 @@ def test_sparse_collect_overflow_is_exact(gpu, oracle_mod):
     assert got["flags"][1] & 2 and got["count"][1] == 240
 
 
-def test_sparse_plain_and_other_passes(gpu, oracle_mod):
-    """The register scan (sparse_scan_reg_kernel) runs a pass only when every product of a shared
-    term is a normal float > 0; otherwise sparse_scan_kernel does. Both must give the oracle's
-    answer: a plain pass; a pass with one zero and one negative weight; a pass whose products
-    underflow to denormals; an index holding a zero value (never plain)."""
+def test_sparse_zero_negative_and_denormal_products(gpu, oracle_mod):
+    """Products that are not normal positive floats keep the oracle's answer: a pass with one
+    zero and one negative weight, a pass whose products underflow to denormals, and an index
+    holding zero values (rows sharing only a zero-valued term are still results, score 0)."""
     csr = oracle_mod.sparse_corpus(20000, seed=91)
     qi, qx, qv = oracle_mod.sparse_queries(64, seed=92)
     idx = _sparse_index(csr, gpu)
@@ -301,8 +300,9 @@ def test_sparse_plain_and_other_passes(gpu, oracle_mod):
 
 
 def test_sparse_clustered_postings(gpu, oracle_mod):
-    """A posting-list term (below 1/8 of the rows) whose postings fill whole 128-row tiles: the
-    register scan's in-tile window of 64 postings is full, so it reads the tile's next windows."""
+    """A posting-list term (below 1/8 of the rows) whose postings fill whole 128-row tiles, so
+    the scan's staged window of 128 postings is entirely inside the tile (its next posting row is
+    only bounded, not read) and the following tiles start from the advanced cursor."""
     indptr, indices, values = oracle_mod.sparse_corpus(20000, seed=93)
     t = 249_999  # not in the Zipf corpus's head
     rows = np.r_[0:300, 5000:5090, 19_900:20000]
