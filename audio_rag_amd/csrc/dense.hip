@@ -757,10 +757,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const int32_t* __restrict__ tile_ord, const uint32_t* __restrict__ flags,
     const float* __restrict__ thr, int32_t* __restrict__ col_cnt, int32_t* __restrict__ col_list,
-    int col_cap,
-    int32_t* __restrict__ sync, int xcd_step) {
-  // first pass: zero the post-scan kernel's arrival counters (it runs next on this stream)
-  if (!COLLECT && sync && blockIdx.x == 0 && threadIdx.x < 4) sync[threadIdx.x] = 0;
+    int col_cap, int xcd_step) {
   // xcd_step > 1 (small shards, plan_scan): only workgroups whose id is a multiple of xcd_step
   // work, i.e. those on XCDs 0, xcd_step, ... (workgroup i runs on XCD i mod 8)
   if (blockIdx.x % xcd_step != 0) return;
@@ -1607,7 +1604,7 @@ __device__ __forceinline__ void merge_body(
   const double inv_q = n2q > 0 ? 1.0 / sqrt((double)n2q) : 0.0;
   const double qnorm_real = sqrt((double)n2q) * (1.0 / 16777216.0);
   if (tid == 0) {
-    // read by the collect merge, possibly on another XCD inside dense_post_kernel: agent scope
+    // read by the collect merge (agent-scope stores: past this XCD's L2)
     __hip_atomic_store(inv_q_out + qg, inv_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(qnorm_out + qg, qnorm_real, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ctr[0] = 0;
@@ -1951,8 +1948,7 @@ __device__ __forceinline__ void merge_body(
     // an uncertified query's count is the collect merge's to write (one writer per address: two
     // XCDs' L2s writing the same line back in either order could leave this one's 0 last)
     if (certified) out_count[qg] = n_out;
-    // what the collect pass reads, stored past this XCD's L2 (agent scope: `sc1`), so that
-    // dense_post_kernel's collect workgroups on any XCD see it once this workgroup has signalled
+    // what the collect pass reads, stored past this XCD's L2 (agent scope: `sc1`)
     __hip_atomic_store(out_flags + qg, certified ? ARMI_FLAG_CERTIFIED : 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(thr_out + qg, certified ? __builtin_inff() : thr, __ATOMIC_RELAXED,
@@ -2148,113 +2144,6 @@ __global__ __launch_bounds__(kDenseMergeThreads) void dense_collect_merge_kernel
       out_rank, out_count, flags);
 }
 
-
-// The post-scan chain of an int8-filter call in ONE launch (round 5): the merge (one workgroup
-// per query), then, only when some query is uncertified, the collect pass
-// (dense_scan_i8_kernel<COLLECT>'s workgroups) and the collect merge (query workgroups +
-// overflow helpers). Arrival counters live in the workspace (sync[0..3], zeroed by the first pass,
-// which runs just before on this stream):
-//   sync[0]  merges done, + 2^16 per uncertified query (one relaxed agent-scope add per merge);
-//   sync[2]  the decision, written by the last merge to arrive: 1 = every query certified,
-//            2 = collect (the other groups poll it and, on 1, exit without touching anything);
-//   sync[1]  collect workgroups done (the collect merge waits for all of them).
-// Cross-workgroup visibility follows MI355X_MICROARCH.md (per-XCD L2s are not coherent, a CU's
-// L1 is never refreshed by other CUs): what the collect pass reads from the merge (flags,
-// thresholds, counts) is stored with agent-scope stores and polled / read past L1; the rare
-// collect path adds an agent-scope release after its stores and an acquire before its reads.
-// Workgroups are dispatched in index order, so a waiting workgroup only waits for lower-indexed
-// ones that are already dispatched. On a certified call (nearly every call) this replaces the
-// merge + two no-op launches (merge + ~9 us + two launch gaps) by the merge + ~1 us. A wait gives
-// up after ~2 s (a bug, never a hang of the GPU) and then takes the safe (collect) path.
-__device__ __forceinline__ int post_poll(int32_t* ctr, int target) {
-  int v = 0;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while ((v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target &&
-           __builtin_amdgcn_s_memrealtime() - t0 < 200000000ull)
-      __builtin_amdgcn_s_sleep(2);
-  }
-  return v;
-}
-__device__ __forceinline__ void post_acquire() {
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void post_release_arrive(int32_t* ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-static_assert(kThreads == kDenseMergeThreads, "one block size for the three groups");
-
-template <int DIM, bool NT>
-__global__ __launch_bounds__(kThreads) void dense_post_kernel(
-    int nq, int n_collect, int n_help, int32_t* __restrict__ sync,
-    // merge
-    const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
-    const float* __restrict__ cand_bound, int n_wg, const uint16_t* __restrict__ rows,
-    const double* __restrict__ inv_norm, const int64_t* __restrict__ norm2,
-    const uint16_t* __restrict__ queries, double* __restrict__ inv_q, double* __restrict__ qnorm,
-    int k, int kc, int sel_col, int sel_rank, int64_t ordinal_base, float* __restrict__ out_scores,
-    int64_t* __restrict__ out_ids, double* __restrict__ out_rank, int32_t* __restrict__ out_count,
-    uint32_t* __restrict__ out_flags, float* __restrict__ thr, int32_t* __restrict__ col_cnt,
-    int32_t* __restrict__ help_done, int two_stage,
-    // collect pass
-    const int8_t* __restrict__ rows8, const float* __restrict__ a32, const float* __restrict__ e32,
-    const uint64_t* __restrict__ mask_i8, int64_t n_rows, int64_t n_tiles, int tiles_per_wg,
-    int n_ranges, int n_qb, const int32_t* __restrict__ tile_ord, int32_t* __restrict__ col_list,
-    // collect merge
-    const uint64_t* __restrict__ row_mask) {
-  __shared__ int s_go;
-  const int b = (int)blockIdx.x;
-  if (b < nq) {
-    merge_body<DIM>(b, cand_key, cand_row, cand_bound, n_wg, nq, rows, inv_norm, queries, inv_q,
-                    qnorm, k, kc, sel_col, sel_rank, ordinal_base, out_scores, out_ids, out_rank,
-                    out_count, out_flags, thr, col_cnt, help_done, two_stage);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's agent-scope stores are out
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // thread 0 stored this query's flag itself (merge_body's lane 0 of wave 0)
-      const bool cert = (__hip_atomic_load(out_flags + b, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT) & ARMI_FLAG_CERTIFIED) != 0;
-      const int add = cert ? 1 : 1 + (1 << 16);
-      const int old = __hip_atomic_fetch_add(sync + 0, add, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      if ((old & 0xffff) == nq - 1)  // the last merge: decide for the whole call
-        __hip_atomic_store(sync + 2, ((old + add) >> 16) > 0 ? 2 : 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  // collect groups: the decision first (nothing else is read on a certified call)
-  {
-    const int d = post_poll(sync + 2, 1);
-    if (threadIdx.x == 0) s_go = d != 1;
-    __syncthreads();
-    if (!s_go) return;  // workgroup-uniform
-  }
-  if (b < nq + n_collect) {
-    post_acquire();
-    scan_i8_body<DIM, true, NT>(b - nq, rows8, a32, e32, mask_i8, n_rows, n_tiles, tiles_per_wg,
-                                n_ranges, n_qb, queries, nq, nullptr, nullptr, nullptr, tile_ord,
-                                out_flags, thr, col_cnt, col_list, kCollectCap);
-    post_release_arrive(sync + 1);
-    return;
-  }
-  post_poll(sync + 1, n_collect);
-  post_acquire();
-  collect_merge_body<DIM>(b - nq - n_collect, n_help, col_cnt, col_list, kCollectCap, help_done,
-                          nq, rows, inv_norm, norm2, row_mask, n_rows, queries, inv_q, k,
-                          ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags);
-}
 
 // First kernel of a filtered int8-scan call: the caller's row filter in int8 image order: bit p
 // of the output = bit img_to_ord(p) of the caller's ordinal mask (0 for padding positions), one
@@ -2601,7 +2490,6 @@ struct Workspace {
   int32_t* col_cnt;    // [nq] rows appended by the collect pass
   int32_t* col_list;   // [nq][kCollectCap] local rows
   int32_t* help_done;  // [nq] helper workgroups done with an overflowed query
-  int32_t* sync;       // [4] dense_post_kernel arrival counters (zeroed by the first pass)
   uint64_t* mask_img;  // row filter in int8 image order
   int8_t* q8;          // [nq][dim] int8 queries of the int8 tiled scan
   float4* qsc;         // [nq] their scales (query_i8_kernel)
@@ -2621,7 +2509,6 @@ Workspace carve(void* base, const armi_index* idx, int nq, int k, bool fast) {
     w.col_cnt = cv.take<int32_t>(nq);
     w.col_list = cv.take<int32_t>((size_t)nq * kCollectCap);
     w.help_done = cv.take<int32_t>(nq);
-    w.sync = cv.take<int32_t>(4);
     w.mask_img = cv.take<uint64_t>((size_t)(std::max<int64_t>(idx->n_tiles, 1) * 32 + 63) / 64);
     if (use_gemm_scan(nq) && use_tiled_i8(idx, k)) {
       w.q8 = cv.take<int8_t>((size_t)nq * idx->dim);
@@ -2720,7 +2607,7 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
         sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, w.sync, sp.xcd_step);
+        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, sp.xcd_step);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
     if (int rc = tl.end()) return rc;
   } else {
@@ -2740,33 +2627,6 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
   int sel_col = 1, sel_rank = kc;
   merge_select(kc, n_wg, sel_col, sel_rank);
   if (use_gemm_scan(nq) && use_tiled_i8(idx, k)) sel_col = 0;  // exact pool selection
-#ifdef ARMI_POST_FUSED
-  // Probe builds only (ARMI_BUILD_FLAGS=-DARMI_POST_FUSED). A/B on one box, 200-step benches
-  // (profiles/r05g_post_fused_ab.txt): fused 0.2442-0.2519 / 0.0709-0.0718 / 0.0518-0.0521 ms per
-  // step at 1M / 100k / 10k rows, the three launches 0.2445-0.2448 / 0.0700-0.0701 /
-  // 0.0513-0.0514 ms. The launches queue back to back, so one launch saves nothing and the
-  // agent-scope hand-offs cost a little; the default stays the chain below.
-  if (!use_gemm_scan(nq) && use_i8_filter(idx, k)) {
-    // merge + collect pass + collect merge in one launch (dense_post_kernel)
-    const ScanPlan cp = plan_scan(idx, k, 1);
-    const int n_qb = (nq + kQB - 1) / kQB;
-    const int n_collect = n_qb == 1 ? cp.n_wg : n_qb * 8 * ((cp.n_wg + 7) / 8);
-    const int n_help = std::max(1, std::min<int>(kMaxHelp, kCollectCap / k));
-    auto kern = use_nt_stream(idx) ? dense_post_kernel<DIM, true> : dense_post_kernel<DIM, false>;
-    constexpr size_t lds = std::max(std::max(kMergeLds, kColMergeLds),
-                                    (size_t)scan_i8_lds_bytes<DIM>());
-    if (int rc = allow_lds(kern, lds)) return rc;
-    kern<<<dim3(nq + n_collect + nq + n_help), dim3(kThreads), lds, stream>>>(
-        nq, n_collect, n_help, w.sync, w.cand_key, w.cand_row, w.cand_bound, n_wg, idx->rows,
-        idx->inv_norm, idx->norm2, queries, w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
-        idx->ordinal_base, out_scores, out_ids, out_rank, out_count, out_flags, w.thr, w.col_cnt,
-        w.help_done, merge_two_stage(kc) ? 1 : 0, idx->rows8, idx->a32, idx->e32, mask_i8,
-        idx->n_rows, idx->n_tiles, cp.tiles_per_wg, cp.n_wg, n_qb, idx->tile_ord, w.col_list,
-        row_mask);
-    ARMI_LAUNCHED("dense_post_kernel");
-    return ARMI_OK;
-  }
-#endif
   dense_merge_kernel<DIM><<<dim3(nq), dim3(kDenseMergeThreads), kMergeLds, stream>>>(
       w.cand_key, w.cand_row, w.cand_bound, n_wg, nq, idx->rows, idx->inv_norm, queries,
       w.inv_q, w.qnorm, k, kc, sel_col, sel_rank,
@@ -2794,7 +2654,7 @@ int dense_second_pass(const armi_index* idx, const uint16_t* queries, int nq, in
     kern<<<dim3(grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
         idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, cp.tiles_per_wg,
         cp.n_wg, n_qb, queries, nq, nullptr, nullptr, nullptr, idx->tile_ord,
-        out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap, nullptr, 1);
+        out_flags, w.thr, w.col_cnt, w.col_list, kCollectCap, 1);
     ARMI_LAUNCHED("dense_scan_i8_kernel(collect)");
   }
   if (int rc = allow_lds(dense_collect_merge_kernel<DIM>, kColMergeLds)) return rc;
