@@ -166,6 +166,97 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
   layernorm_row(v, width, lane, gamma, beta, eps, out + tok * width);
 }
 
+// The fp16 embedding for widths that are multiples of 256 (XLM-R base 768, large 1024), round 5:
+// workgroup = kEmbTok consecutive tokens of one sequence, one wave per token in turn. The
+// position ids come from one count of the sequence's non-pad tokens before the chunk
+// (__syncthreads_count over its ids) plus a ballot prefix inside it (embed_kernel recounted the
+// sequence prefix per token: a chain of dependent loads per row); each lane owns four contiguous
+// components per 256 (8-B loads and stores instead of one 2-B access per component), type0,
+// gamma and beta stay in registers across the wave's tokens. Same fp32 arithmetic per component
+// as embed_kernel ((word + pos) + type0, two-pass LayerNorm); the lane sums run over another
+// component order, so the outputs agree to fp32 rounding of the statistics, not bitwise.
+constexpr int kEmbTok = 32;
+template <int NC>  // NC = width / 256
+__global__ __launch_bounds__(256) void embed_seq_f16_kernel(
+    const int32_t* __restrict__ ids, const _Float16* __restrict__ word,
+    const _Float16* __restrict__ pos, const _Float16* __restrict__ type0,
+    const float* __restrict__ gamma, const float* __restrict__ beta, _Float16* __restrict__ out,
+    int L, int pad_id, int vocab, int n_pos, float eps) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  constexpr int width = 256 * NC;
+  __shared__ int32_t pid_s[kEmbTok], id_s[kEmbTok];
+  const int chunks = (L + kEmbTok - 1) / kEmbTok;
+  const int seq = blockIdx.x / chunks;
+  const int t0 = (blockIdx.x % chunks) * kEmbTok;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t* row_ids = ids + (int64_t)seq * L;
+  int before = 0;  // non-pad tokens in [0, t0)
+  for (int c = 0; c < t0; c += 256) {
+    const int i = c + tid;
+    before += __syncthreads_count(i < t0 && row_ids[i] != pad_id);
+  }
+  if (wave == 0) {
+    const int t = t0 + lane;
+    const int32_t id = (lane < kEmbTok && t < L) ? row_ids[t] : pad_id;
+    const uint64_t nonpad = __ballot(lane < kEmbTok && t < L && id != pad_id);
+    const int count = before + __popcll(nonpad & ((2ull << lane) - 1ull));  // [0, t]
+    if (lane < kEmbTok) {
+      int p = id != pad_id ? pad_id + count : pad_id;
+      pid_s[lane] = p < n_pos ? p : n_pos - 1;
+      id_s[lane] = (id < 0 || id >= vocab) ? 3 : id;  // <unk>
+    }
+  }
+  __syncthreads();
+  float ty[NC][4], ga[NC][4], be[NC][4];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = 256 * j + 4 * lane;
+    const h4 tv = *reinterpret_cast<const h4*>(type0 + c);
+    const float4 g4 = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(beta + c);
+    ty[j][0] = (float)tv[0], ty[j][1] = (float)tv[1], ty[j][2] = (float)tv[2], ty[j][3] = (float)tv[3];
+    ga[j][0] = g4.x, ga[j][1] = g4.y, ga[j][2] = g4.z, ga[j][3] = g4.w;
+    be[j][0] = b4.x, be[j][1] = b4.y, be[j][2] = b4.z, be[j][3] = b4.w;
+  }
+  for (int k = wave; k < kEmbTok && t0 + k < L; k += 4) {
+    const _Float16* w = word + (int64_t)id_s[k] * width;
+    const _Float16* pp = pos + (int64_t)pid_s[k] * width;
+    h4 wv[NC], pv[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      wv[j] = *reinterpret_cast<const h4*>(w + 256 * j + 4 * lane);
+      pv[j] = *reinterpret_cast<const h4*>(pp + 256 * j + 4 * lane);
+    }
+    float v[NC][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[j][e] = (float)wv[j][e] + (float)pv[j][e] + ty[j][e];
+        s += v[j][e];
+      }
+    const float mean = wave_sum(s) / (float)width;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mean;
+        ss += d * d;
+      }
+    const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)width + eps);
+    _Float16* o = out + ((int64_t)seq * L + t0 + k) * width;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      h4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = (_Float16)((v[j][e] - mean) * rstd * ga[j][e] + be[j][e]);
+      *reinterpret_cast<h4*>(o + 256 * j + 4 * lane) = r;
+    }
+  }
+}
+
 // Classification head on <s> (RobertaClassificationHead + sigmoid): h = tanh(W1 x0 + b1),
 // logit = w2 . h + b2, out = sigmoid(logit). kHeadSeq sequences per workgroup, one thread per
 // output feature (blockDim = width rounded up to 64): thread o walks the transposed dense weight
@@ -306,6 +397,34 @@ int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t*
   ARMI_REQUIRE(ids && word && pos && type0 && gamma && beta && out,
                "embed_f16: null pointer argument");
   const int64_t toks = (int64_t)n_seq * L;
+  if (width % 256 == 0) {
+    const int64_t blocks = (int64_t)n_seq * ((L + kEmbTok - 1) / kEmbTok);
+    ARMI_REQUIRE(blocks < (int64_t(1) << 31), "embed_f16: too many sequences");
+    auto* w16 = reinterpret_cast<const _Float16*>(word);
+    auto* p16 = reinterpret_cast<const _Float16*>(pos);
+    auto* t16 = reinterpret_cast<const _Float16*>(type0);
+    auto* o16 = reinterpret_cast<_Float16*>(out);
+    switch (width / 256) {
+      case 1:
+        embed_seq_f16_kernel<1><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+            ids, w16, p16, t16, gamma, beta, o16, L, pad_id, vocab, n_pos, eps);
+        break;
+      case 2:
+        embed_seq_f16_kernel<2><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+            ids, w16, p16, t16, gamma, beta, o16, L, pad_id, vocab, n_pos, eps);
+        break;
+      case 3:
+        embed_seq_f16_kernel<3><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+            ids, w16, p16, t16, gamma, beta, o16, L, pad_id, vocab, n_pos, eps);
+        break;
+      default:
+        embed_seq_f16_kernel<4><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(
+            ids, w16, p16, t16, gamma, beta, o16, L, pad_id, vocab, n_pos, eps);
+        break;
+    }
+    ARMI_LAUNCHED("embed_seq_f16_kernel");
+    return ARMI_OK;
+  }
   embed_kernel<_Float16, _Float16><<<dim3((unsigned)((toks + 3) / 4)), dim3(256), 0, stream>>>(
       ids, reinterpret_cast<const _Float16*>(word), reinterpret_cast<const _Float16*>(pos),
       reinterpret_cast<const _Float16*>(type0), gamma, beta, reinterpret_cast<_Float16*>(out),
