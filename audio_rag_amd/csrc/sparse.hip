@@ -519,7 +519,8 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
 // Profiling build only (ARMI_BUILD_FLAGS=-DARMI_SPARSE_PROFILE): per-wave phase timers and the
 // ARMI_SPARSE_DBG knobs (1 = skip compute, 2 = stage nothing, 4 = no step barrier, 8 = report,
 // 16 = clear every staged row each step).
-__device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 8];
+// 12 words per wave: 6 phase sums, term count, steps, setup, tail, entry and exit stamps
+__device__ unsigned long long g_sparse_prof[kMaxRanges * kWaves * 12];
 #define ARMI_PROF_T(x) x = wall_clock64()
 #define ARMI_PROF_ADD(i, a, b) tp[i] += (b) - (a)
 #else
@@ -591,6 +592,9 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     int32_t* __restrict__ coll_row, int dbg, const int32_t* __restrict__ dense_of,
     const uint32_t* __restrict__ dense_val, int64_t dense_stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][kTile]
+#ifdef ARMI_SPARSE_PROFILE
+  const unsigned long long t_entry = wall_clock64();
+#endif
   const int g = blockIdx.x;
   const int wave = armi::wave_id();
   const int lane = threadIdx.x & 63;
@@ -885,6 +889,9 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   (void)t_a;
   (void)t_b;
   ARMI_PROF_T(t_a);
+#ifdef ARMI_SPARSE_PROFILE
+  const unsigned long long t_setup = t_a - t_entry;
+#endif
   if (S > 0) {
     issue(0, 0);
     finish(0, 0, 0);
@@ -935,12 +942,7 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     seg = seg1;
   }
 #ifdef ARMI_SPARSE_PROFILE
-  if ((dbg & 8) && lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) g_sparse_prof[((size_t)g * kWaves + wave) * 8 + i] = tp[i];
-    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 6] = qn[0] + qn[1] + qn[2] + qn[3];
-    g_sparse_prof[((size_t)g * kWaves + wave) * 8 + 7] = S;
-  }
+  const unsigned long long t_loop_end = wall_clock64();
 #endif
   if constexpr (!kCollect) {
     if (has_q) {
@@ -994,6 +996,20 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       }
     }
   }
+#ifdef ARMI_SPARSE_PROFILE
+  if ((dbg & 8) && lane == 0) {
+    const unsigned long long t_exit = wall_clock64();
+    unsigned long long* pr = g_sparse_prof + ((size_t)g * kWaves + wave) * 12;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) pr[i] = tp[i];
+    pr[6] = qn[0] + qn[1] + qn[2] + qn[3];
+    pr[7] = S;
+    pr[8] = t_setup;
+    pr[9] = t_exit - t_loop_end;
+    pr[10] = t_entry;
+    pr[11] = t_exit;
+  }
+#endif
 }
 
 // Order-preserving map of a float to uint32 (larger float -> larger key; -inf lowest).
@@ -1732,24 +1748,33 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
     if (int rc = tl.end()) return rc;
 #ifdef ARMI_SPARSE_PROFILE
     if (dbg & 8) {
-      std::vector<unsigned long long> h((size_t)kMaxRanges * kWaves * 8);
+      std::vector<unsigned long long> h((size_t)kMaxRanges * kWaves * 12);
       ARMI_HIP(hipStreamSynchronize(stream));
       ARMI_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_sparse_prof), h.size() * 8));
-      double sum[8] = {0}, mx[8] = {0};
+      double sum[10] = {0}, mx[10] = {0};
+      unsigned long long e_min = ~0ull, e_max = 0, x_min = ~0ull, x_max = 0;
       int cnt = 0;
       for (int g = 0; g < idx->n_ranges; ++g)
         for (int wv = 0; wv < kWaves; ++wv) {
+          const unsigned long long* pr = &h[((size_t)g * kWaves + wv) * 12];
           ++cnt;
-          for (int i = 0; i < 8; ++i) {
-            sum[i] += (double)h[((size_t)g * kWaves + wv) * 8 + i];
-            mx[i] = std::max(mx[i], (double)h[((size_t)g * kWaves + wv) * 8 + i]);
+          for (int i = 0; i < 10; ++i) {
+            sum[i] += (double)pr[i];
+            mx[i] = std::max(mx[i], (double)pr[i]);
           }
+          e_min = std::min(e_min, pr[10]);
+          e_max = std::max(e_max, pr[10]);
+          x_min = std::min(x_min, pr[11]);
+          x_max = std::max(x_max, pr[11]);
         }
       fprintf(stderr, "sparse prof (us, 100MHz clock) avg/max: issue %.1f/%.1f compute %.1f/%.1f "
-              "cand %.1f/%.1f finish %.1f/%.1f barrier %.1f/%.1f prologue %.1f/%.1f n_w %.1f/%.0f S %.0f\n",
+              "cand %.1f/%.1f finish %.1f/%.1f barrier %.1f/%.1f prologue %.1f/%.1f n_w %.1f/%.0f S %.0f "
+              "setup %.1f/%.1f tail %.1f/%.1f entry-spread %.1f exit-spread %.1f span %.1f\n",
               sum[0] / cnt / 100, mx[0] / 100, sum[1] / cnt / 100, mx[1] / 100, sum[2] / cnt / 100,
               mx[2] / 100, sum[3] / cnt / 100, mx[3] / 100, sum[4] / cnt / 100, mx[4] / 100,
-              sum[5] / cnt / 100, mx[5] / 100, sum[6] / cnt, mx[6], mx[7]);
+              sum[5] / cnt / 100, mx[5] / 100, sum[6] / cnt, mx[6], mx[7], sum[8] / cnt / 100,
+              mx[8] / 100, sum[9] / cnt / 100, mx[9] / 100, (e_max - e_min) / 100.0,
+              (x_max - x_min) / 100.0, (x_max - e_min) / 100.0);
     }
 #endif
     sparse_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(

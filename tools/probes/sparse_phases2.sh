@@ -4,8 +4,8 @@
 # (1 = no compute, 2 = stage nothing, 4 = no step barrier; 8 = report).
 TAG=${1:-sph}
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1; mkdir -p gpurun_out
-for d in 8 9 10 11 12 15; do
-  ARMI_LIB_PATH=ablibs/libarmi_sprof.so ARMI_SPARSE_DBG=$d timeout -k 10 200 python bench.py --workload hybrid --steps 10 --warmup 2 --no-cpu-baseline --no-extras \
+for d in ${DBGS:-8 9 10 11 12 15}; do
+  ARMI_LIB_PATH=ablibs/libarmi_sprof.so ARMI_SPARSE_DBG=$d timeout -k 10 200 python bench.py --workload hybrid --eager-hybrid --steps 10 --warmup 2 --no-cpu-baseline --no-extras \
     > gpurun_out/${TAG}_$d.log 2>&1 || exit 1
   # the first report is a 64-query pass (the bench's single-query latency calls come last)
   echo "dbg=$d: $(grep 'sparse prof' gpurun_out/${TAG}_$d.log | head -1)"
