@@ -4,8 +4,8 @@ configs[2] (1 x MI355X, 1M chunks, hybrid dense + BM25 with RRF, top-20 -> cross
   * MI355XRetriever.search_batch in hybrid mode over 1M x 1024 fp16 rows + the SURVEY §8(d) Zipf
     sparse corpus: prefetch 40 + 40 -> RRF 20 (qdrant.py:281-298). The dense and sparse prefetch
     lists and the fused ids / fp64 RRF scores must equal the oracle's bit for bit.
-  * the cross-encoder (reranking/bge.py:86-147) on the fused candidates of 2 queries (40 pairs of
-    L = 256 tokens, all 12 layers, fp16 path) within 1e-3 of transformers' fp32 forward.
+  * the cross-encoder (reranking/bge.py:86-147) on the top-20 candidates of 16 queries (320 pairs
+    of L = 256 tokens, all 12 layers, fp16 path) within 1e-3 of transformers' fp32 forward.
 configs[3]'s arithmetic on one GPU (10M chunks sharded 8-way -> 8 shards of 1.25M rows, the
 all-gathered batch of 512 queries, i.e. exactly one rank's scan shape at N = 8):
   * per-shard tiled scans (dense_gemm_scan_w4_kernel, the default tiled form) at k = 5 and k = 40, merged over the 8
@@ -122,35 +122,42 @@ def test_configs2_hybrid_1m_matches_oracle(corpus_1m, oracle_mod):
 
 
 def test_configs2_rerank_full_depth_within_1e3(corpus_1m, gpu):
-    """Cross-encoder over the retrieved top-20 of 2 queries: 40 (query, chunk) pairs of 256
+    """Cross-encoder over the retrieved top-20 of all 16 queries: 320 (query, chunk) pairs of 256
     tokens (<s> q16 </s></s> d236 </s>, bench.py's pair layout) through all 12 layers (fp16 GEMMs /
-    attention) against transformers' fp32 forward of the same seeded weights."""
+    attention, the graphed forward) against transformers' fp32 forward of the same seeded weights
+    (round 5: 16 queries, was 2)."""
     from audio_rag_amd.reranking.xlmr import CrossEncoderXLMR, build_reranker
     from audio_rag_amd.retrieval.device import DenseIndex
     from audio_rag_amd.synthetic import VOCAB, doc_tokens
 
     c = corpus_1m
-    cand = DenseIndex(c["rows"]).topk(c["q"][:2].contiguous(), 20).ids  # [2, 20] ordinals
+    nq = c["q"].shape[0]
+    cand = DenseIndex(c["rows"]).topk(c["q"], 20).ids  # [nq, 20] ordinals
     g = torch.Generator(device=gpu).manual_seed(4)
-    q_tok = torch.randint(4, VOCAB, (2, 16), generator=g, device=gpu, dtype=torch.int32)
+    q_tok = torch.randint(4, VOCAB, (nq, 16), generator=g, device=gpu, dtype=torch.int32)
     docs = doc_tokens(cand, 236)
-    eos = torch.full((2, 20, 1), 2, dtype=torch.int32, device=gpu)
-    bos = torch.zeros((2, 20, 1), dtype=torch.int32, device=gpu)
-    pairs = torch.cat([bos, q_tok[:, None, :].expand(2, 20, 16), eos, eos, docs, eos],
-                      dim=2).reshape(40, 256).contiguous()
+    eos = torch.full((nq, 20, 1), 2, dtype=torch.int32, device=gpu)
+    bos = torch.zeros((nq, 20, 1), dtype=torch.int32, device=gpu)
+    pairs = torch.cat([bos, q_tok[:, None, :].expand(nq, 20, 16), eos, eos, docs, eos],
+                      dim=2).reshape(nq * 20, 256).contiguous()
     mask = torch.ones_like(pairs)
     model = build_reranker(seed=5)
     enc = CrossEncoderXLMR(model, gpu)
     enc.to_dtype(torch.float16)
     got = enc.forward(pairs, mask).cpu().numpy().astype(np.float64)
+    want = []
     with torch.no_grad():
-        logits = model(input_ids=pairs.long().cpu(), attention_mask=mask.long().cpu()).logits
-    want = torch.sigmoid(logits.double()).view(-1).numpy()
+        for b in range(0, nq * 20, 40):
+            ids = pairs[b:b + 40].long().cpu()
+            want.append(torch.sigmoid(model(input_ids=ids, attention_mask=torch.ones_like(ids)
+                                            ).logits.double()).view(-1).numpy())
+    want = np.concatenate(want)
     err = np.abs(got - want).max()
-    print(f"configs[2] rerank 40 pairs x 256 tokens, 12 layers: max |score error| = {err:.2e}")
+    print(f"configs[2] rerank {nq * 20} pairs x 256 tokens, 12 layers: "
+          f"max |score error| = {err:.2e}")
     assert err < 1e-3
     # the reranked order the pipeline would return (stable sort, reranking/bge.py:134)
-    for qq in range(2):
+    for qq in range(nq):
         o_got = np.argsort(-got[qq * 20:(qq + 1) * 20], kind="stable")[:5]
         o_want = np.argsort(-want[qq * 20:(qq + 1) * 20], kind="stable")[:5]
         gap = np.sort(want[qq * 20:(qq + 1) * 20])[::-1]
