@@ -301,5 +301,8 @@ def test_bge_m3_full_depth_matches_fp32(gpu):
             got = lex[0]
             clear = [t for t, w in ref_lex.items() if w > 0.05]
             assert all(t in got for t in clear), name
+            # (the seeded stand-in's sparse head leaves no positive weight on these texts, so
+            # this check is empty here; tests/test_lexical_weights_gpu.py compares 34 nonzero
+            # weights through a re-biased head)
             np.testing.assert_allclose([got[t] for t in clear], [ref_lex[t] for t in clear],
                                        rtol=5e-2, atol=5e-3)
