@@ -369,7 +369,12 @@ class HybridGraph:
                           (self.qi, self.qx, self.qv), limit, rrf_k)
 
         # warm-up on a side stream, then capture under inference mode (as _QueryGraph and the
-        # reranker's graphs do: the CUDA generator's graph state is shared by every capture)
+        # reranker's graphs do: the CUDA generator's graph state is shared by every capture).
+        # The warm-up batch is one-hot dense queries with empty sparse parts: all-zero queries
+        # tie every row at cosine 0, so their top-k cannot be certified and the warm-up ran the
+        # dense collect pass over the whole shard (~0.16 s per call at 1M rows, r05z trace)
+        rows = torch.arange(self.batch, device=dev)
+        self.q[rows, rows % self.dim] = 1.0
         with torch.inference_mode():
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
