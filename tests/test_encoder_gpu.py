@@ -416,3 +416,20 @@ def test_bge_m3_query_graph_equals_eager(gpu):
                                    rtol=5e-3, atol=1e-3)
     assert len(e._graphs) == 2  # one captured graph per length bucket used
 
+
+
+def test_attention_f16_many_items_ragged(gpu):
+    """Many sequences (840 (sequence, head) workgroups, more than the CUs) with a different ragged
+    mask each (incl. a single live key and an all-live row), against fp32 eager attention."""
+    g = torch.Generator().manual_seed(321)
+    n, L, H, dh = 70, 200, 12, 64  # 840 items
+    qkv = (torch.randn(n, L, 3 * H * dh, generator=g) * 1.5).half()
+    lens = torch.randint(1, L + 1, (n,), generator=g)
+    lens[0], lens[1] = L, 1
+    mask = (torch.arange(L)[None, :] < lens[:, None]).to(torch.int32)
+    ref = _attention_ref(qkv, mask, H, dh)
+    Q, M = qkv.to(gpu).contiguous(), mask.to(gpu)
+    out = torch.empty(n, L, H * dh, dtype=torch.float16, device=gpu)
+    _call("armi_enc_attention_f16", Q.data_ptr(), M.data_ptr(), out.data_ptr(), n, L, H, dh,
+          1 / math.sqrt(dh))
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=1e-3, atol=3e-3)
