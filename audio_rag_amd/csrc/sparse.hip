@@ -14,10 +14,11 @@
 // Search, one pass per 64 queries:
 //   pass_terms: the 64 queries are dealt to 16 waves, 4 each (slot 4w + i), and every slot gets
 //           the ascending list of its query's terms as (staging row offset, weight).
-//   scan:   workgroup = one row range, wave = 4 queries, lane = two adjacent rows of a 128-row
+//   scan:   workgroup = one row range, wave = 4 queries, lane = four adjacent rows of a 256-row
 //           tile. Each distinct term of the pass is staged once per tile: its holder wave loads
-//           the next 64 (or 128) postings (lane-reversed), keeps the prefix inside the tile and
-//           scatters the values into the term's 128-entry row image in LDS. Then every wave
+//           the next 128 postings (lane-reversed; more while the tile holds more), keeps the
+//           prefix inside the tile and scatters the values into the term's 256-entry row image
+//           in LDS (a dense-value column: one 16-B load per lane of the tile's value bits). Then every wave
 //           walks each of its queries' terms in ascending term order and adds fl32(w * v) into
 //           that query's fp32 accumulators of the lane's two rows (packed multiply, packed add).
 //           Ascending term order per (row, query) is the Qdrant summation order; nothing else
@@ -50,15 +51,19 @@ constexpr int kMaxTerms = 256;          // query terms per query (BGE-M3 queries
 constexpr int kLongTerm = 256;          // postings from which a term gets a range-start table
 constexpr int kPad = 128;               // sentinel slots past the last list (two 64-posting loads)
 constexpr int kBatch = 4;  // terms whose LDS reads are in flight together (8: no gain, r04ak)
-constexpr int kTile = 128;              // rows per scan step: two adjacent rows per lane
+constexpr int kTile = 256;              // rows per scan step: four adjacent rows per lane
 constexpr int kQStride = kMaxTerms + 2 * kBatch;  // list entries per query slot (+ padding)
 constexpr int kMaxRanges = 256;
 constexpr int kMaxU = kQB * kMaxTerms;  // distinct terms of one pass, at most
-constexpr int kU = 128;                 // terms per staging segment
+constexpr int kU = 64;                  // terms per staging segment
 constexpr int kHold = kU / kWaves;      // terms of a segment staged by one wave
 constexpr int kRegSegs = 64 / kHold;    // segments whose cursors stay in registers
-// two staging buffers, the all-zero row and the 64-entry scratch row of out-of-tile scatters
-constexpr size_t kScanLds = (size_t)(2 * kU + 1) * kTile * 4 + 64 * 4;
+// segment boundaries 64 .. kMaxU / kU of each query slot (the first 64 stay in registers)
+constexpr int kSegTab = kMaxU / kU - 64 + 1;
+// two staging buffers, the all-zero row, the 64-entry scratch row of out-of-tile scatters and
+// the segment-boundary table (uint16 [kWaves][kQW][kSegTab])
+constexpr size_t kScanLdsStage = (size_t)(2 * kU + 1) * kTile * 4 + 64 * 4;
+constexpr size_t kScanLds = kScanLdsStage + (size_t)kWaves * kQW * kSegTab * 2;
 constexpr size_t kPrepLds = (size_t)kMaxU * 8;         // pass pairs: keys + weights, 128 KB
 constexpr int kBitmapVocab = 1 << 18;   // vocabularies up to which a pass numbers its terms by bitmap
 constexpr int kBmWords = kBitmapVocab / 32;
@@ -568,14 +573,16 @@ __device__ __forceinline__ int2 range_cursor(int32_t t, int g, int64_t lo, int n
   return make_int2(c, post[c].x);
 }
 
-// Workgroup = one row range; steps = (128-row tile, segment of kU pass terms). Staging: term
+// Workgroup = one row range; steps = (256-row tile, segment of kU = 64 pass terms). Staging: term
 // u_local of the segment is held by wave u_local & 15 (lane slot u_local >> 4), which keeps its
-// cursor, loads the term's next 64 postings (lane-reversed: posting c+p in lane 63-p) and, when
-// the tile can hold more, the 64 after them, keeps the prefix inside the tile and scatters
-// ~bits(value) to buf[u_local][row - tile start] in LDS (0 = no posting). Compute: lane l owns
-// rows 2l and 2l+1 of the tile; wave w walks each of its 4 queries' terms of the segment in
-// ascending u, reads the row pair buf[u_local][2l..2l+1] and adds fl32(w * v) into the query's
-// pair of fp32 accumulators (one packed multiply, one packed add). Staging of step s+1 is issued
+// cursor, loads the term's next 128 postings (lane-reversed: postings c + 2 (63 - l) and + 1 in
+// lane l; a further 128 at a time while all of them fall inside the tile), keeps the prefix inside
+// the tile and scatters the value bits to buf[u_local][row - tile start] in LDS (0 = no posting).
+// Compute: lane l owns rows 4l .. 4l + 3 of the tile; wave w walks each of its 4 queries' terms of
+// the segment in ascending u, reads the four rows buf[u_local][4l .. 4l + 3] (one ds_read_b128)
+// and adds fl32(w * v) into the query's four fp32 accumulators (two packed multiplies, two packed
+// adds). Round 5: 256-row tiles of 64-term segments (was 128 rows x 128 terms, two rows per
+// lane): the per-term list entry, address add and LDS read serve four rows instead of two. Staging of step s+1 is issued
 // before, and written after, the compute of step s (double-buffered LDS, one barrier per step).
 // kCollect = false: per-range candidate lists; kCollect = true: every row scoring >= thr.
 template <bool kCollect>
@@ -653,13 +660,14 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     l1r[i] = kEndRow;
     l2r[i] = kEndRow;
   }
-  f2 acc[kQW];
-  uint32_t hx[kQW], hy[kQW];  // OR of the staged value bits seen per row: != 0 <=> a shared term
+  f2 acc[kQW], acc2[kQW];  // rows 4 lane, + 1 (acc) and + 2, + 3 (acc2)
+  uint32_t hm[kQW][4];  // per row: OR of the staged value bits seen, != 0 <=> a shared term
 #pragma unroll
   for (int i = 0; i < kQW; ++i) {
     acc[i] = f2{0.f, 0.f};
-    hx[i] = 0u;
-    hy[i] = 0u;
+    acc2[i] = f2{0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) hm[i][h] = 0u;
   }
 
   // staged postings of the held terms: lane l holds postings c + 2 (63 - l) (.x row, .y value
@@ -691,12 +699,10 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       if ((amask >> k) & 1u) {
         const int cx = rl_i(cv.x, base + k);  // uniform
         if (cx < 0) {
-          // dense column: the tile's value bits, rows tlo + 2 lane and + 1 in .x / .y (zero past
-          // the store). A 16-B load straight into sp[k] (.z / .w unused): an 8-B load into part
-          // of it would need a copy, i.e. a wait for the load here instead of in finish (round 5:
-          // measured in the ISA, a vmcnt(0) before the load that drains every staged load)
+          // dense column: the tile's value bits, rows tlo + 4 lane .. + 3 (zero past the store):
+          // one whole 16-B load per lane
           sp[k] = *reinterpret_cast<const p4*>(dense_val + (size_t)(-cx - 1) * dense_stride + tlo +
-                                               2 * lane);
+                                               4 * lane);
         } else {
           sp[k] = *reinterpret_cast<const p4*>(post + cx + rev2);
         }
@@ -724,27 +730,39 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     for (int k = 0; k < kHold; ++k) {
       uint32_t* row = buf + (k * kWaves + wave) * kTile;
       if ((amask & dmask) >> k & 1u) {  // dense column: the whole row image, no clear, no cursor
-        reinterpret_cast<uint2*>(row)[lane] = make_uint2((uint32_t)sp[k].x, (uint32_t)sp[k].y);
+        reinterpret_cast<p4*>(row)[lane] = sp[k];
         continue;
       }
-      if ((dm >> k) & 1u) reinterpret_cast<uint2*>(row)[lane] = make_uint2(0u, 0u);
+      if ((dm >> k) & 1u) reinterpret_cast<p4*>(row)[lane] = p4{0, 0, 0, 0};
       if ((amask >> k) & 1u) {
-        const uint64_t be = __ballot(sp[k].x < thi), bo = __ballot(sp[k].z < thi);
-        const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
-        const int no = bo == ~0ull ? 64 : __builtin_clzll(~bo);
-        const int n = min(2 * ne, 2 * no + 1);  // postings inside the tile
-        // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
-        uint32_t* d0 = rev2 < n ? row + (sp[k].x - tlo) : trash;
-        uint32_t* d1 = rev2 + 1 < n ? row + (sp[k].z - tlo) : trash;
-        *d0 = (uint32_t)sp[k].y;
-        *d1 = (uint32_t)sp[k].w;
-        // the next posting's row, or a lower bound of it
-        const int nl = (63 - (n >> 1)) & 63;
-        const int32_t re = rl_i(sp[k].x, nl), ro = rl_i(sp[k].z, nl);
-        const int32_t nr = n < kTile ? ((n & 1) ? ro : re) : thi;
-        const bool me = lane == base + k;
-        scv.x = me ? scv.x + n : scv.x;
-        scv.y = me ? nr : scv.y;
+        // a 256-row tile can hold more than the 128 postings of one load: the rest are loaded
+        // here, 128 at a time (rare for a term in < 1/8 of the rows), until the list leaves the
+        // tile
+        p4 v = sp[k];
+        int adv = 0;  // postings consumed before v
+        while (true) {  // wave-uniform trip count
+          const uint64_t be = __ballot(v.x < thi), bo = __ballot(v.z < thi);
+          const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
+          const int no = bo == ~0ull ? 64 : __builtin_clzll(~bo);
+          const int n = min(2 * ne, 2 * no + 1);  // postings of v inside the tile
+          // values are stored with 0.0 as -0.0 (index build), so a posting is never the 0 marker
+          uint32_t* d0 = rev2 < n ? row + (v.x - tlo) : trash;
+          uint32_t* d1 = rev2 + 1 < n ? row + (v.z - tlo) : trash;
+          *d0 = (uint32_t)v.y;
+          *d1 = (uint32_t)v.w;
+          if (n < 128) {
+            // the next posting's row (lane 63 - n / 2 holds positions n & ~1 and n | 1)
+            const int nl = 63 - (n >> 1);
+            const int32_t re = rl_i(v.x, nl), ro = rl_i(v.z, nl);
+            const bool me = lane == base + k;
+            scv.x = me ? scv.x + adv + n : scv.x;
+            scv.y = me ? ((n & 1) ? ro : re) : scv.y;
+            break;
+          }
+          adv += 128;
+          const int cx = rl_i(scv.x, base + k) + adv;  // uniform
+          v = *reinterpret_cast<const p4*>(post + cx + rev2);
+        }
       }
     }
     if (seg < kRegSegs) {
@@ -754,10 +772,12 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       if (lane < kHold && u < nU) gcur[u] = scv;
     }
   };
-  // qf[i] (lane s) / qf2[i] (lane s - 64): first entry of query slot i's list whose term lies in
-  // segment s or later (a pass has at most kMaxU / kU = 128 segments)
-  static_assert(kMaxU / kU <= 128, "two lane slots per segment boundary");
-  int qn[kQW], qf[kQW], qf2[kQW];
+  // qf[i] (lane s): first entry of query slot i's list whose term lies in segment s or later;
+  // segments 64 .. kMaxU / kU in the LDS table segtab (a pass has at most 256 segments)
+  uint16_t* const segtab = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(sbuf) +
+                                                       kScanLdsStage) +
+                           (size_t)wave * kQW * kSegTab;
+  int qn[kQW], qf[kQW];
 #pragma unroll
   for (int i = 0; i < kQW; ++i) {
     const int slot = wave * kQW + i;
@@ -777,31 +797,41 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
       return a0;
     };
     qf[i] = lane <= nSeg ? lower_seg(lane) : qn[i];
-    qf2[i] = lane + 64 <= nSeg ? lower_seg(lane + 64) : qn[i];
+    for (int sg = 64 + lane; sg < nSeg; sg += 64)  // (only waves' own entries: no barrier needed)
+      segtab[i * kSegTab + sg - 64] = (uint16_t)lower_seg(sg);
   }
   auto first_of = [&](int i, int sg) {  // sg is wave-uniform
-    return sg >= nSeg ? qn[i] : (sg < 64 ? rl_i(qf[i], sg) : rl_i(qf2[i], sg - 64));
+    return sg >= nSeg ? qn[i]
+                      : (sg < 64 ? rl_i(qf[i], sg)
+                                 : __builtin_amdgcn_readfirstlane((int)segtab[i * kSegTab + sg - 64]));
   };
   auto compute = [&](int seg, int par) {
-    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)par * kU * kTile) + lane * 8;
+    const char* buf = reinterpret_cast<const char*>(sbuf + (size_t)par * kU * kTile) + lane * 16;
     const int zoff = (2 - par) * kU * kTile * 4;  // the all-zero row, relative to buf
     // staged rows hold the posting's value bits (a zero value as -0.0), 0 = no posting; a row
     // without a posting adds fl32(w * 0) = +-0, which leaves an fp32 sum unchanged. Batches of
     // 4 entries; entries past the segment's end (the next segment's, or the zero padding after
     // the list: finite weights) read the all-zero row, so they add +-0 as well.
-    auto batch = [&](const QTerm* tm, int tail, f2& a, uint32_t& x, uint32_t& y) {
-      uint2 rv[kBatch];
+    auto math = [&](const QTerm* tm, const uint4* rv, int i) {
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k)
-        rv[k] = *reinterpret_cast<const uint2*>(buf + (k < tail ? tm[k].off : zoff));
-#pragma unroll
-      for (int k = 0; k < kBatch; ++k)
-        a = a + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
+      for (int k = 0; k < kBatch; ++k) {
+        acc[i] = acc[i] + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
+        acc2[i] = acc2[i] + f2{tm[k].w, tm[k].w} * f2{__uint_as_float(rv[k].z), __uint_as_float(rv[k].w)};
+      }
 #pragma unroll
       for (int k = 0; k < kBatch; k += 2) {
-        x = or3(x, rv[k].x, rv[k + 1].x);
-        y = or3(y, rv[k].y, rv[k + 1].y);
+        hm[i][0] = or3(hm[i][0], rv[k].x, rv[k + 1].x);
+        hm[i][1] = or3(hm[i][1], rv[k].y, rv[k + 1].y);
+        hm[i][2] = or3(hm[i][2], rv[k].z, rv[k + 1].z);
+        hm[i][3] = or3(hm[i][3], rv[k].w, rv[k + 1].w);
       }
+    };
+    auto batch = [&](const QTerm* tm, int tail, int i) {
+      uint4 rv[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k)
+        rv[k] = *reinterpret_cast<const uint4*>(buf + (k < tail ? tm[k].off : zoff));
+      math(tm, rv, i);
     };
     // The next batch's entries (one scalar load) are requested right after this batch's LDS
     // reads, so the two latencies overlap: the loop waits once per batch for both (scalar loads
@@ -823,37 +853,27 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
         QTerm nxt[kBatch];  // requested first: in flight with this batch's LDS reads
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) nxt[k] = L[j + kBatch + k];
-        uint2 rv[kBatch];
+        uint4 rv[kBatch];
 #pragma unroll
-        for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint2*>(buf + cur[k].off);
-        f2& a = acc[i];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k)
-          a = a + f2{cur[k].w, cur[k].w} * f2{__uint_as_float(rv[k].x), __uint_as_float(rv[k].y)};
-#pragma unroll
-        for (int k = 0; k < kBatch; k += 2) {
-          hx[i] = or3(hx[i], rv[k].x, rv[k + 1].x);
-          hy[i] = or3(hy[i], rv[k].y, rv[k + 1].y);
-        }
+        for (int k = 0; k < kBatch; ++k) rv[k] = *reinterpret_cast<const uint4*>(buf + cur[k].off);
+        math(cur, rv, i);
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) cur[k] = nxt[k];
       }
-      if (j < j1) batch(cur, j1 - j, acc[i], hx[i], hy[i]);  // cur = entries j .. j + 3
+      if (j < j1) batch(cur, j1 - j, i);  // cur = entries j .. j + 3
     }
   };
-  auto candidates = [&](int tile, uint64_t m0, uint64_t m1) {
+  auto candidates = [&](int tile, uint64_t mw) {
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kTile);
     const int32_t thi = tile_hi(tile);
-    const int32_t r0 = tlo + 2 * lane;
-    const uint64_t mw = lane < 32 ? m0 : m1;
-    const bool ok0 = ((mw >> ((2 * lane) & 63)) & 1ull) && r0 < thi;
-    const bool ok1 = ((mw >> ((2 * lane + 1) & 63)) & 1ull) && r0 + 1 < thi;
+    const int32_t r0 = tlo + 4 * lane;
+    const uint32_t mb = (uint32_t)(mw >> ((4 * lane) & 63)) & 0xfu;  // the lane's four rows
 #pragma unroll
     for (int i = 0; i < kQW; ++i) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {  // the lane's two rows, ascending
-        const bool cand = h == 0 ? (ok0 && hx[i] != 0u) : (ok1 && hy[i] != 0u);
-        const float sc = h == 0 ? acc[i].x : acc[i].y;
+      for (int h = 0; h < 4; ++h) {  // the lane's four rows, ascending
+        const bool cand = ((mb >> h) & 1u) && r0 + h < thi && hm[i][h] != 0u;
+        const float sc = h == 0 ? acc[i].x : h == 1 ? acc[i].y : h == 2 ? acc2[i].x : acc2[i].y;
         const int32_t r = r0 + h;
         if constexpr (kCollect) {
           const int q = qw[i];
@@ -880,8 +900,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   };
 
   // the all-zero row after the two staging buffers (read by the padding entries of a batch)
-  if (threadIdx.x < kTile / 2)
-    reinterpret_cast<uint2*>(sbuf + (size_t)2 * kU * kTile)[threadIdx.x] = make_uint2(0u, 0u);
+  if (threadIdx.x < kTile / 4)
+    reinterpret_cast<uint4*>(sbuf + (size_t)2 * kU * kTile)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
   const int S = n_tiles * nSeg;
   unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long t_a = 0, t_b = 0;
@@ -904,13 +924,13 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     const int par = s & 1;
     const bool last_seg = seg == nSeg - 1;
     const int tile1 = last_seg ? tile + 1 : tile, seg1 = last_seg ? 0 : seg + 1;  // step s + 1
-    // loaded now, used after this step's compute; lo is a multiple of 64, so the tile's rows
-    // are the bits of words tlo / 64 and tlo / 64 + 1
-    uint64_t m0 = ~0ull, m1 = ~0ull;
+    // loaded now, used after this step's compute; lo is a multiple of 64, so the lane's four
+    // rows tlo + 4 lane .. + 3 are bits of word tlo / 64 + lane / 16
+    uint64_t mw = ~0ull;
     if (row_mask && last_seg) {
       const int64_t tlo = lo + (int64_t)tile * kTile;
-      m0 = row_mask[tlo >> 6];
-      m1 = tlo + 64 < hi ? row_mask[(tlo >> 6) + 1] : 0ull;
+      const int64_t w0 = tlo + 64 * (lane >> 4);
+      mw = w0 < hi ? row_mask[w0 >> 6] : 0ull;
     }
     ARMI_PROF_T(t_a);
     if (s + 1 < S) issue(tile1, seg1);
@@ -921,14 +941,15 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #pragma unroll
         for (int i = 0; i < kQW; ++i) {
           acc[i] = f2{0.f, 0.f};
-          hx[i] = 0u;
-          hy[i] = 0u;
+          acc2[i] = f2{0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) hm[i][h] = 0u;
         }
       }
       if (!(dbg & 1)) compute(seg, par);
       ARMI_PROF_T(t_a);
       ARMI_PROF_ADD(1, t_b, t_a);
-      if (last_seg) candidates(tile, m0, m1);
+      if (last_seg) candidates(tile, mw);
       ARMI_PROF_T(t_b);
       ARMI_PROF_ADD(2, t_a, t_b);
     }
