@@ -172,7 +172,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
             raise ArmiUnavailable(f"{p}: ABI version {lib.armi_abi_version()} != {ABI_VERSION}")
         want = source_digest()
         got = lib.armi_source_digest().decode()
-        if want is not None and got != want:
+        # ARMI_AB_OTHER_SOURCES=1 (with ARMI_LIB_PATH only): time a build of other sources, e.g.
+        # the previous commit's kernel, beside this tree's on one box (A/B probes; never the
+        # in-tree library, which always has to match csrc/)
+        ab = bool(os.environ.get("ARMI_LIB_PATH")) and os.environ.get("ARMI_AB_OTHER_SOURCES") == "1"
+        if want is not None and got != want and not ab:
             raise ArmiUnavailable(f"{p} was built from other sources (digest {got}, csrc/ is "
                                   f"{want}): rebuild it with `python -m audio_rag_amd.build`")
         _lib = lib
