@@ -299,21 +299,19 @@ def test_sparse_zero_negative_and_denormal_products(gpu, oracle_mod):
           oracle_mod.sparse_topk(indptr, indices, values, qi, qx, qv, 20))
 
 
-def test_sparse_clustered_postings(gpu, oracle_mod):
-    """A posting-list term (below 1/8 of the rows) whose postings fill whole 128-row tiles, so
-    the scan's staged window of 128 postings is entirely inside the tile (its next posting row is
-    only bounded, not read) and the following tiles start from the advanced cursor."""
-    indptr, indices, values = oracle_mod.sparse_corpus(20000, seed=93)
+def _clustered_case(oracle_mod, gpu, n, rows, seed):
+    """The corpus of sparse_corpus(n) with a posting-list term t (below 1/8 of the rows) added to
+    `rows`, and 64 queries that all carry t: (device index, csr, query csr)."""
+    indptr, indices, values = oracle_mod.sparse_corpus(n, seed=seed)
     t = 249_999  # not in the Zipf corpus's head
-    rows = np.r_[0:300, 5000:5090, 19_900:20000]
-    add = np.zeros(20000, dtype=bool)
+    add = np.zeros(n, dtype=bool)
     add[rows] = True
     new_ptr = np.zeros_like(indptr)
     np.cumsum(np.diff(indptr) + add, out=new_ptr[1:])
     ni = np.empty(new_ptr[-1], np.int32)
     nv = np.empty(new_ptr[-1], np.float32)
-    rng = np.random.default_rng(94)
-    for r in range(20000):
+    rng = np.random.default_rng(seed + 1)
+    for r in range(n):
         a, b = indptr[r], indptr[r + 1]
         c = new_ptr[r]
         ids, vals = indices[a:b], values[a:b]
@@ -326,7 +324,7 @@ def test_sparse_clustered_postings(gpu, oracle_mod):
         ni[c:c + len(ids)] = ids
         nv[c:c + len(ids)] = vals
     csr = (new_ptr, ni, nv)
-    qi, qx, qv = oracle_mod.sparse_queries(64, seed=95)
+    qi, qx, qv = oracle_mod.sparse_queries(64, seed=seed + 2)
     # every query also carries t (kept ascending)
     xs, vs = [], []
     for b in range(64):
@@ -340,6 +338,23 @@ def test_sparse_clustered_postings(gpu, oracle_mod):
     qv2 = np.concatenate(vs).astype(np.float32)
     qi2 = np.zeros(65, np.int32)
     np.cumsum([len(x) for x in xs], out=qi2[1:])
-    idx = _sparse_index(csr, gpu)
+    return _sparse_index(csr, gpu), csr, (qi2, qx2, qv2)
+
+
+def test_sparse_clustered_postings(gpu, oracle_mod):
+    """A posting-list term (below 1/8 of the rows) whose postings fill whole tiles, so the scan's
+    staged window of 128 postings is entirely inside the tile (its next posting row is only
+    bounded, not read) and the following tiles start from the advanced cursor."""
+    idx, csr, q = _clustered_case(oracle_mod, gpu, 20000, np.r_[0:300, 5000:5090, 19_900:20000], 93)
     for k in (5, 40):
-        _same(_run(idx, (qi2, qx2, qv2), k, gpu), oracle_mod.sparse_topk(*csr, qi2, qx2, qv2, k))
+        _same(_run(idx, q, k, gpu), oracle_mod.sparse_topk(*csr, *q, k))
+
+
+def test_sparse_clustered_postings_beyond_one_load(gpu, oracle_mod):
+    """200k rows (832-row ranges, so whole 256-row tiles): a posting-list term with runs of 300
+    and 700 contiguous rows, i.e. more postings inside one tile than one 128-posting load holds
+    (the scan reloads 128 at a time, round 5), plus runs across range and tile edges."""
+    rows = np.r_[0:300, 800:870, 50_000:50_700, 123_456:123_700, 199_700:200_000]
+    idx, csr, q = _clustered_case(oracle_mod, gpu, 200_000, rows, 193)
+    for k in (5, 40):
+        _same(_run(idx, q, k, gpu), oracle_mod.sparse_topk(*csr, *q, k))
