@@ -967,42 +967,44 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
 #endif
   if constexpr (!kCollect) {
     if (has_q) {
-      // per query: top 16 of the 128 lane entries (sort both list levels, bitonic split of their
-      // heads); the kQW queries' sorts run together so their shuffle chains overlap
-      float ka[kQW], kb[kQW], ck[kQW], bq[kQW];
-      int32_t ra[kQW], rb[kQW], cr[kQW];
+      // per query: top 16 of the 128 lane entries. Sorting the lanes' best entries (l1) leaves
+      // the 16 best in lanes 0 .. 15; a second entry (l2) ranks below its own lane's l1, so only
+      // the l2 of those 16 lanes can reach the top 16: lanes 16 .. 31 take them (the lane that
+      // owns a row r is ((r - lo) mod kTile) / 4), and one more sort of those 32 gives the top 16.
+      // The bound is the 17th best key: max(the 17th l1, the 17th of the 32) (round 5; was two
+      // full sorts of l1 and l2, a bitonic split of their heads and a third sort).
+      float ka[kQW], ck[kQW], bq[kQW];
+      int32_t ra[kQW], cr[kQW];
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
         ka[i] = l1s[i];
         ra[i] = l1r[i];
-        kb[i] = l2s[i];
-        rb[i] = l2r[i];
       }
       armi::wave_sort_approx_desc_n<kQW>(ka, ra);
-      armi::wave_sort_approx_desc_n<kQW>(kb, rb);
+      const int e = lane & 15;
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
-        const float kbr = __shfl(kb[i], (15 - lane) & 63);
-        const int32_t rbr = __shfl(rb[i], (15 - lane) & 63);
-        const float kb16 = __shfl(kb[i], 16);
-        float lose = kNegInf;
-        ck[i] = kNegInf;
-        cr[i] = kEndRow;
-        if (lane < 16) {
-          const bool take_a = armi::approx_better(ka[i], ra[i], kbr, rbr);
-          ck[i] = take_a ? ka[i] : kbr;
-          cr[i] = take_a ? ra[i] : rbr;
-          lose = take_a ? kbr : ka[i];
-        } else if (lane == 16) {
-          lose = fmaxf(ka[i], kb16);
-        }
-        bq[i] = fmaxf(disc[i], lose);
+        const float ke = __shfl(ka[i], e);
+        const int32_t re = __shfl(ra[i], e);
+        const int src = ke == kNegInf ? 0 : (int)(((int64_t)re - lo) & (kTile - 1)) >> 2;
+        const float pk = __shfl(l2s[i], src);
+        const int32_t pr = __shfl(l2r[i], src);
+        const bool part = lane >= 16 && lane < 32 && ke != kNegInf;
+        ck[i] = lane < 16 ? ka[i] : (part ? pk : kNegInf);
+        cr[i] = lane < 16 ? ra[i] : (part ? pr : kEndRow);
+        const float lose16 = __shfl(ka[i], 16);
+        bq[i] = fmaxf(disc[i], lane == 0 ? lose16 : kNegInf);
+      }
+      armi::wave_sort_approx_desc_n<kQW>(ck, cr);
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) {
+        const float lose2 = __shfl(ck[i], 16);
+        bq[i] = fmaxf(bq[i], lane == 0 ? lose2 : kNegInf);
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
         for (int i = 0; i < kQW; ++i) bq[i] = fmaxf(bq[i], armi::xor_stride(bq[i], o));
-      armi::wave_sort_approx_desc_n<kQW>(ck, cr);
 #pragma unroll
       for (int i = 0; i < kQW; ++i) {
         const int q = qw[i];
