@@ -128,5 +128,14 @@ def load_tokenizer(path: Path | None):
 
 
 def tokenizer_for(name: str | None):
-    """The tokenizer of the checkpoint `name` resolves to on disk, else None."""
-    return load_tokenizer(resolve_local(name))
+    """The tokenizer of the checkpoint `name` resolves to on disk, else None (no checkpoint: the
+    encoders keep their seeded stand-ins and the stand-in tokenizer). A checkpoint whose weights
+    are on disk without tokenizer.json raises: its load() would run the real weights on the
+    stand-in tokenizer's ids and return wrong vectors without any error."""
+    path = resolve_local(name)
+    tok = load_tokenizer(path)
+    if tok is None and path is not None and (
+            (path / "model.safetensors").exists() or (path / "pytorch_model.bin").exists()):
+        raise FileNotFoundError(f"{path}: checkpoint weights without tokenizer.json (convert the "
+                                "sentencepiece model to tokenizer.json next to the weights)")
+    return tok

@@ -133,6 +133,11 @@ class BGEM3Embedder(BaseEmbedder):
         except Exception as e:
             raise EmbeddingError(f"Failed to load embedding model: {e}")
         self._fast = None
+        # XLMREncoderF16 rebinds the model's query / key / value weights as views of its fused
+        # Q|K|V tensor (one GEMM instead of three): the model must not be moved, cast or given a
+        # new state dict in place afterwards (the two would silently stop sharing weights), so
+        # the model and the encoder live and die together (unload() drops both; a new load()
+        # rebuilds both from the same tensors)
         if self.query_kernels == "armi" and self._device.type == "cuda":
             from audio_rag_amd.embeddings.xlmr_f16 import XLMREncoderF16
 

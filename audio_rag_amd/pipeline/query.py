@@ -222,9 +222,13 @@ class QueryPipeline:
             # and the others with their sparse vector: one device batch per such group
             has_lex = [bool(x) for x in lex] if lex is not None else [False] * len(query_texts)
             per_query: list = [None] * len(query_texts)
+            # a sharded retriever's search_batch is a collective (one all-gather per call): every
+            # rank must make the same number of calls whatever its own queries are, so both groups
+            # are searched even when one is empty (search_batch takes an empty batch)
+            collective = getattr(retriever, "_world", 1) > 1
             for want in (True, False):
                 rows = [i for i, h in enumerate(has_lex) if h == want]
-                if not rows:
+                if not rows and not collective:
                     continue
                 sel = torch.tensor(rows, dtype=torch.long, device=dense.device)
                 batch = QueryBatch(dense=dense.index_select(0, sel).contiguous())
@@ -233,9 +237,13 @@ class QueryPipeline:
                     indptr = np.zeros(len(parts) + 1, dtype=np.int32)
                     np.cumsum([len(p[0]) for p in parts], out=indptr[1:])
                     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(retriever.device)
+                    # one unused entry keeps the term arrays non-empty (an empty group, or queries
+                    # whose terms were all dropped): the C ABI refuses null arrays
                     batch = QueryBatch(dense=batch.dense, sparse_indptr=t(indptr),
-                                       sparse_indices=t(np.concatenate([p[0] for p in parts])),
-                                       sparse_values=t(np.concatenate([p[1] for p in parts])))
+                                       sparse_indices=t(np.concatenate([p[0] for p in parts] +
+                                                                       [np.zeros(1, np.int32)])),
+                                       sparse_values=t(np.concatenate([p[1] for p in parts] +
+                                                                      [np.zeros(1, np.float32)])))
                 out, mode = retriever.search_batch(batch, k, resolved, filter_metadata, search_type)
                 thr = None  # search()'s score_threshold rule (qdrant.py:331: legacy dense only)
                 if mode == "legacy_dense" and self.config.retrieval.score_threshold > 0:

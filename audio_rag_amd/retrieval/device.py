@@ -405,10 +405,18 @@ class HybridGraph:
                 buf[o_qv:end].view(torch.float32)[:n])
 
     def _check(self, queries, q_indptr, q_indices, q_values) -> int:
+        """Shape checks of a batch. The per-query limit of max_terms (armi_sparse_topk scores a
+        longer query's first 256 terms only and flags it) is checked here for a host indptr; a
+        device indptr is not read back (that would synchronise every step): callers keep each
+        query within max_terms, as query_sparse_arrays does for the pipeline."""
         n = int(q_indices.numel())
         if (tuple(queries.shape) != (self.batch, self.dim) or int(q_indptr.numel()) != self.batch + 1
                 or n > self.batch * self.max_terms or int(q_values.numel()) != n):
             raise ValueError("HybridGraph: batch shape differs from the captured one")
+        if not q_indptr.is_cuda and self.batch > 0:
+            lens = q_indptr[1:].to(torch.int64) - q_indptr[:-1].to(torch.int64)
+            if int(lens.max()) > self.max_terms or int(lens.min()) < 0:
+                raise ValueError(f"HybridGraph: a query has more than {self.max_terms} terms")
         return n
 
     def pack(self, queries: torch.Tensor, q_indptr: torch.Tensor, q_indices: torch.Tensor,

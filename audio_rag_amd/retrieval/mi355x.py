@@ -165,6 +165,7 @@ class MI355XRetriever(BaseRetriever):
         self._collections: dict[str, ChunkCollection] = {}
         self._hybrid: ConcurrentHybrid | None = None
         self._graphs_ok = True  # cleared when a capture is refused (search() then runs eagerly)
+        self.last_sharded = None  # the ShardedSearch of the last collective call (diagnostics)
         # num_gpus > 1: the corpus is sharded by ordinal over the ranks of the default process
         # group (one process per GPU, launched by torchrun, torch.distributed initialised and
         # the process's GPU selected before the retriever is built): see _search_sharded
@@ -352,6 +353,7 @@ class MI355XRetriever(BaseRetriever):
                            if coll.hybrid else None,
                            rrf=lambda a, b, k: rrf_fuse(a, b, k, rrf_k=self.config.rrf_k),
                            merge_packed=merge_shards_packed)
+        self.last_sharded = sh
         csr = (queries.sparse_indptr, queries.sparse_indices, queries.sparse_values)
         # the ranks agree on top_k and on collection + filter through the call's header (a
         # mismatch raises on every rank); batch sizes and branches may differ

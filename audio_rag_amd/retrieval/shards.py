@@ -158,6 +158,11 @@ class ShardedSearch:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self._side: torch.cuda.Stream | None = None
+        # search(): gathered query rows that are real queries (None: all of them); the rest pad
+        # a smaller batch to the largest one and are never scanned (_dense_local)
+        self._live: torch.Tensor | None = None
+        self.scanned_queries = 0  # dense queries this rank's last local scan searched
+        self.last_dense_flags: torch.Tensor | None = None  # ARMI_FLAG_* of those queries
 
     # ------------------------------------------------------------------ collectives
 
@@ -220,7 +225,7 @@ class ShardedSearch:
     def dense(self, q_local: torch.Tensor, k: int) -> TopK:
         nb = int(q_local.shape[0])
         all_q, _ = self._gather_queries(q_local)
-        return self._exchange([self.local_dense(all_q, k)], k, nb)[0]
+        return self._exchange([self._dense_local(all_q, k)], k, nb)[0]
 
     def sparse(self, q_local_csr: tuple[torch.Tensor, torch.Tensor, torch.Tensor], k: int) -> TopK:
         """q_local_csr: (indptr int32 [nb+1], indices int32, values float32) of this rank."""
@@ -273,6 +278,19 @@ class ShardedSearch:
         nb_max = int(h[:, 0].max())
         if nb_max == 0:
             return _head(None, 0, k, dev)
+        nbs = h[:, 0].tolist()
+        self._live = None
+        if any(n != nb_max for n in nbs):
+            self._live = torch.cat([torch.arange(g * nb_max, g * nb_max + n, dtype=torch.int64)
+                                    for g, n in enumerate(nbs)]).to(dev)
+        try:
+            return self._search_padded(q_local, q_local_csr, code, codes, need_sparse, nb, nb_max,
+                                       k, dev)
+        finally:
+            self._live = None
+
+    def _search_padded(self, q_local, q_local_csr, code: int, codes: set, need_sparse: bool,
+                       nb: int, nb_max: int, k: int, dev) -> TopK:
         q_pad = _pad_rows(q_local, nb_max)
         csr = None
         if need_sparse:
@@ -294,9 +312,29 @@ class ShardedSearch:
                    else self.rrf(d, s, k))
         return _head(out, nb, k) if nb != nb_max else out
 
+    def _dense_local(self, all_q: torch.Tensor, k: int) -> TopK:
+        """The local dense scan of the gathered batch. Inside search() with ranks of different
+        batch sizes only the real queries are scanned: a padding row (a copy of the rank's first
+        query, or for an empty rank no query at all) has no owner, and an empty rank's padding
+        used to be a zero vector, which ties every row at cosine 0, cannot be certified and sent
+        every rank through the full-shard collect pass. Padding rows get empty lists."""
+        live = self._live
+        if live is None:
+            self.scanned_queries = int(all_q.shape[0])
+            t = self.local_dense(all_q, k)
+            self.last_dense_flags = t.flags
+            return t
+        self.scanned_queries = int(live.numel())
+        n = int(all_q.shape[0])
+        if live.device != all_q.device:
+            live = live.to(all_q.device)
+        t = self.local_dense(all_q.index_select(0, live).contiguous(), k)
+        self.last_dense_flags = t.flags
+        return _scatter_rows(t, live, n, k)
+
     def _local_pair(self, all_q, all_csr, k: int) -> tuple[TopK, TopK]:
         if not all_q.is_cuda:
-            return self.local_dense(all_q, k), self.local_sparse(all_csr, k)
+            return self._dense_local(all_q, k), self.local_sparse(all_csr, k)
         if self._side is None:
             self._side = torch.cuda.Stream(device=all_q.device)
         main = torch.cuda.current_stream()
@@ -305,7 +343,7 @@ class ShardedSearch:
             t.record_stream(self._side)
         with torch.cuda.stream(self._side):
             s = self.local_sparse(all_csr, k)
-        d = self.local_dense(all_q, k)
+        d = self._dense_local(all_q, k)
         main.wait_stream(self._side)
         for t in s.tensors():
             t.record_stream(main)
@@ -325,9 +363,26 @@ def _head(t: TopK | None, n: int, k: int, dev=None) -> TopK:
                 count=t.count[:n].clamp(max=k).to(torch.int32))
 
 
+def _scatter_rows(t: TopK, rows: torch.Tensor, n: int, k: int) -> TopK:
+    """Lists of the selected gathered rows -> lists of all n rows (the others empty: count 0)."""
+    dev = t.ids.device
+    out = TopK(scores=torch.full((n, k), float("-inf"), dtype=torch.float32, device=dev),
+               ids=torch.full((n, k), -1, dtype=torch.int64, device=dev),
+               rank=torch.full((n, k), float("-inf"), dtype=torch.float64, device=dev),
+               count=torch.zeros(n, dtype=torch.int32, device=dev))
+    out.scores.index_copy_(0, rows, t.scores.to(torch.float32))
+    out.ids.index_copy_(0, rows, t.ids)
+    out.rank.index_copy_(0, rows, t.rank.to(torch.float64))
+    out.count.index_copy_(0, rows, t.count.to(torch.int32))
+    if t.flags is not None:
+        out.flags = torch.zeros(n, dtype=torch.int32, device=dev)
+        out.flags.index_copy_(0, rows, t.flags.to(torch.int32))
+    return out
+
+
 def _pad_rows(q: torch.Tensor, n: int) -> torch.Tensor:
-    """q [nb, dim] -> [n, dim]: padding rows copy row 0 (zeros for an empty batch), so padded
-    queries cost what a real one does; their answers are sliced away."""
+    """q [nb, dim] -> [n, dim]: padding rows copy row 0 (zeros for an empty batch). The dense
+    scan of search() skips them (ShardedSearch._dense_local); their answers are sliced away."""
     nb = int(q.shape[0])
     if nb == n:
         return q

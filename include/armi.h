@@ -333,8 +333,10 @@ int armi_enc_embed(const int32_t* ids, const float* word, const float* pos, cons
                    int width, int pad_id, int vocab, int n_pos, float eps, hipStream_t stream);
 /* The same over fp16 tables (the fp16 model's own word / position / type embeddings, no fp32
  * copy: BGE-M3's word table is 0.5 GB in fp16), writing the fp16 activations the fp16 forwards
- * feed their first GEMM: out [n_seq][L][width] fp16, each value the round-to-nearest-even of
- * what armi_enc_embed computes in fp32 from the same (fp16-exact) table values. */
+ * feed their first GEMM: out [n_seq][L][width] fp16, the round-to-nearest-even of a LayerNorm
+ * computed in fp32 from the same (fp16-exact) table values. Equal to armi_enc_embed's output up
+ * to the fp32 rounding of the LayerNorm statistics, not bitwise: the width % 256 == 0 path
+ * (one workgroup per 32-token chunk) sums a row's components in a different order. */
 int armi_enc_embed_f16(const int32_t* ids, const uint16_t* word, const uint16_t* pos,
                        const uint16_t* type0, const float* gamma, const float* beta, uint16_t* out,
                        int n_seq, int L, int width, int pad_id, int vocab, int n_pos, float eps,

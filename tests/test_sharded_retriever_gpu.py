@@ -92,6 +92,23 @@ def _worker(rank, world, port, out_dir):
         out[name + "_sc"] = [[r.score for r in rs] for rs in res]
         out[name + "_ids"] = np.array([x + [-1] * (K - len(x)) for x in out[name + "_ids"]])
         out[name + "_sc"] = np.array([x + [0.0] * (K - len(x)) for x in out[name + "_sc"]])
+    # an empty rank (no queries this call) beside ranks that search hybrid: its padding rows are
+    # never scanned, so every scanned dense query is certified (a zero-vector padding query
+    # used to tie every row and send each rank through the full-shard collect pass)
+    qb = batch if rank % 2 else type(batch)(dense=batch.dense[:0], sparse_indptr=batch.sparse_indptr[:1],
+                                           sparse_indices=batch.sparse_indices,
+                                           sparse_values=batch.sparse_values)
+    tk, mode = ret.search_batch(qb, K, None, None, "hybrid")
+    res = ret.materialize_batch(tk, mode, coll.name)
+    out["mixC_n"] = np.array(len(res))
+    out["mixC_ids"] = np.array([[int(r.chunk.text.split()[1]) for r in rs] + [-1] * (K - len(rs))
+                                for rs in res]).reshape(len(res), K)
+    out["mixC_sc"] = np.array([[r.score for r in rs] + [0.0] * (K - len(rs))
+                               for rs in res]).reshape(len(res), K)
+    sh = ret.last_sharded
+    out["mixC_scanned"] = np.array(sh.scanned_queries)
+    fl = sh.last_dense_flags.cpu().numpy()
+    out["mixC_certified"] = np.array(int(np.all((fl & 1) == 1) and np.all((fl & 2) == 0)))
     # a top_k disagreement raises RetrievalError on every rank instead of hanging
     from audio_rag_amd.core.exceptions import RetrievalError
 
@@ -179,6 +196,12 @@ def test_sharded_retriever_plugin_equals_global(tmp_path, oracle_mod, world):
                     ids, sc = want(mode, None, r * B + q)
                 assert list(z[name + "_ids"][q, :len(ids)]) == [int(x) for x in ids], (r, name, q)
                 assert [float(x) for x in z[name + "_sc"][q, :len(sc)]] == [float(x) for x in sc]
+        assert int(z["mixC_scanned"]) == B * (world // 2) and int(z["mixC_certified"]) == 1, r
+        assert int(z["mixC_n"]) == (B if r % 2 else 0), r
+        for q in range(int(z["mixC_n"])):
+            ids, sc = want("hybrid", None, r * B + q)
+            assert list(z["mixC_ids"][q, :len(ids)]) == [int(x) for x in ids], (r, "mixC", q)
+            assert [float(x) for x in z["mixC_sc"][q, :len(sc)]] == [float(x) for x in sc]
         ids, _ = want("hybrid", None, r * B)
         assert list(z["single_ids"]) == [int(x) for x in ids]
         # rank-local rerank of its own slice vs transformers fp32 (bge.py:119-123)

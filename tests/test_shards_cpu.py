@@ -191,6 +191,7 @@ def _mixed_worker(rank, world, port, out_dir):
             q_csr = (torch.from_numpy(ip), torch.from_numpy(qx[a:b] if b > a else qx[:1]),
                      torch.from_numpy(qv[a:b] if b > a else qv[:1]))
         t = ss.search(q_mine, q_csr, mode, K, digest=7)
+        out[f"c{case}_scanned"] = ss.scanned_queries
         out[f"c{case}_ids"] = t.ids.numpy()
         out[f"c{case}_sc"] = t.rank.numpy()
         out[f"c{case}_cnt"] = t.count.numpy()
@@ -214,6 +215,7 @@ MIXED_CASES = [
     [("sparse", 2, False), ("hybrid", B, True)],
     [("dense", B, False), ("sparse", B - 1, False)],
     [("hybrid", 0, False), ("hybrid", 3, False)],
+    [("dense", 0, False), ("hybrid", B, False)],
 ]
 
 
@@ -247,6 +249,12 @@ def test_two_rank_mixed_branches_and_sizes(tmp_path, oracle_mod):
     for r in range(world):
         z = np.load(tmp_path / f"mixed{r}.npz")
         assert int(z["raised"]) == 2, r
+        for case, plan in enumerate(MIXED_CASES):
+            # only real queries reach the local dense scan: an empty rank's batch is padding,
+            # never scanned (a zero-vector padding query cannot be certified: full collect pass)
+            nbs = [plan[g % len(plan)][1] for g in range(world)]
+            want_scanned = sum(nbs) if len(set(nbs)) > 1 else world * nbs[0]
+            assert int(z[f"c{case}_scanned"]) == want_scanned, (r, case)
         gd = o.dense_topk(rows, q_all[:2], K)
         np.testing.assert_array_equal(z["after_ids"], gd.ids)
         for case, plan in enumerate(MIXED_CASES):
