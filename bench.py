@@ -687,10 +687,11 @@ def main() -> None:
 
 
 def secondary_configs(args) -> dict:
-    """BASELINE configs[1] and configs[2], and north_star's 10k / 10M ends of the size sweep,
-    measured beside the headline (the driver runs only the default bench line): each is a child
-    bench.py run on the same GPU, its JSON line attached under "configs1" / "configs2" /
-    "chunks_10k" / "chunks_10M" (value, ms_per_step, p50, rooflines)."""
+    """BASELINE configs[1] and configs[2], north_star's 10k / 10M ends of the size sweep,
+    configs[2]'s retrieval alone ("hybrid"), the single-stream AudioRAG.query() pipeline and
+    configs[3]'s per-rank call, measured beside the headline (the driver runs only the default
+    bench line): each is a child bench.py run on the same GPU, its JSON line attached under its
+    key (value, ms_per_step, p50, rooflines)."""
     import subprocess
 
     # configs1 / configs2 carry their own cpu_baseline (dense at 100k; the reference's hybrid +
@@ -707,14 +708,29 @@ def secondary_configs(args) -> dict:
                        "--latency-iters", "10"],
         "chunks_10M": ["--chunks", "10000000", "--steps", "20", "--warmup", "3",
                        "--latency-iters", "3"],
+        # configs[2]'s retrieval alone (dense + sparse prefetch 40 each, RRF 20; no rerank), with
+        # the sparse stage's roofline and the reference's hybrid CPU path beside it
+        "hybrid": ["--workload", "hybrid", "--chunks", str(args.chunks), "--steps", "100",
+                   "--warmup", "10", "--latency-iters", "10", *cpu],
+        # AudioRAG.query() one query at a time over the 1M-chunk hybrid store, per-stage p50s
+        "pipeline": ["--workload", "pipeline", "--chunks", str(args.chunks), "--queries", "100"],
+        # configs[3]'s per-rank call on one GPU: 10M chunks / 8 ranks = 1.25M rows x the 8 x 64
+        # all-gathered queries, top-5 (collectives excluded: per-rank work, not a scaling number)
+        "configs3_rank": ["--chunks", "1250000", "--batch", "512", "--steps", "20", "--warmup",
+                          "3", "--latency-iters", "3"],
     }
     out = {}
     for key, extra in runs.items():
         cmd = [sys.executable, str(ROOT / "bench.py"), "--no-extras", *extra]
-        if key not in ("configs1", "configs2"):
+        if key not in ("configs1", "configs2", "hybrid"):
             cmd.append("--no-cpu-baseline")
         try:
-            res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            t_child = time.perf_counter()
+            # the child's stderr passes through (progress on long runs); stdout is its JSON line
+            res = subprocess.run(cmd, stdout=subprocess.PIPE, text=True,
+                                 timeout=480 if key == "pipeline" else 300)
+            print(f"[bench] {key}: rc {res.returncode} in {time.perf_counter() - t_child:.0f} s",
+                  file=sys.stderr, flush=True)
             line = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else ""
             d = json.loads(line) if res.returncode == 0 and line.startswith("{") else None
         except (subprocess.TimeoutExpired, json.JSONDecodeError):
@@ -723,11 +739,18 @@ def secondary_configs(args) -> dict:
             out[key] = {"error": "child bench run failed", "cmd": " ".join(cmd[1:])}
             continue
         keep = ("value", "unit", "ms_per_step", "steps", "p50_ms", "p50_single_query_ms",
+                "p95_ms", "p99_ms", "stage_p50_ms", "reference_published_p50_ms",
                 "certified_frac", "config", "roofline", "roofline_scan", "roofline_sparse",
-                "rerank_share_of_step", "dtype", "cpu_baseline")
+                "sparse_stage", "rerank_share_of_step", "dtype", "cpu_baseline")
         out[key] = {kk: d[kk] for kk in keep if kk in d}
         if key in ("configs1", "configs2"):
             out[key]["baseline_config"] = {"configs1": 1, "configs2": 2}[key]
+        if key == "configs3_rank":
+            out[key]["baseline_config"] = 3
+            out[key]["note"] = ("per-rank work of configs[3] measured on one GPU: one rank's "
+                                "1.25M-row shard of 10M chunks and the 8 x 64 queries an 8-GPU "
+                                "step all-gathers, top-5; collectives excluded, so this is not a "
+                                "scaling measurement (the driver's SCALE run is)")
     return out
 
 
