@@ -21,7 +21,8 @@ HEADER = Path(__file__).resolve().parents[1] / "include" / "armi.h"
 ARMI_OK = 0
 ARMI_FLAG_CERTIFIED = 1
 ARMI_FLAG_FALLBACK = 2
-TIMING_DENSE_SCAN, TIMING_SPARSE_SCAN, TIMING_ENCODER_GEMM = 0, 1, 2
+ARMI_FLAG_FILTERED = 4
+TIMING_DENSE_SCAN, TIMING_SPARSE_SCAN, TIMING_ENCODER_GEMM, TIMING_SPARSE_STAGE = 0, 1, 2, 3
 SCAN_FP16, SCAN_INT8_FILTER, SCAN_TILED_FP16, SCAN_TILED_INT8 = 0, 1, 2, 3  # armi_dense_scan_form
 ABI_VERSION = 2
 
@@ -84,6 +85,7 @@ SIGNATURES: dict[str, tuple] = {
                                          c_int64, ctypes.POINTER(c_void_p), c_void_p]),
     "armi_sparse_index_destroy": (c_int, [c_void_p]),
     "armi_sparse_workspace_bytes": (c_size_t, [c_void_p, c_int, c_int]),
+    "armi_sparse_index_set_filter": (c_int, [c_void_p, c_int, c_void_p]),
     "armi_sparse_topk": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "armi_rrf_fuse": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

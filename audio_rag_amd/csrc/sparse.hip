@@ -597,7 +597,8 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
     float* __restrict__ cand_key, int32_t* __restrict__ cand_row, float* __restrict__ cand_bound,
     const float* __restrict__ thr, int* __restrict__ coll_count, float* __restrict__ coll_key,
     int32_t* __restrict__ coll_row, int dbg, const int32_t* __restrict__ dense_of,
-    const uint32_t* __restrict__ dense_val, int64_t dense_stride) {
+    const uint32_t* __restrict__ dense_val, int64_t dense_stride,
+    const uint32_t* __restrict__ done_flags) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];  // [2][kU][kTile]
 #ifdef ARMI_SPARSE_PROFILE
   const unsigned long long t_entry = wall_clock64();
@@ -608,7 +609,20 @@ __global__ __launch_bounds__(kScanThreads) void sparse_scan_kernel(
   int qw[kQW];  // this wave's queries (-1: none)
 #pragma unroll
   for (int i = 0; i < kQW; ++i) qw[i] = qof[wave * kQW + i];
-  const bool has_q = qw[0] >= 0;
+  if constexpr (!kCollect) {
+    // queries the MFMA filter already answered (done_flags: the pass's flags) are dropped; with
+    // none left the whole grid exits here (the flags are the same for every workgroup)
+    if (done_flags) {
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < kQW; ++i) {
+        if (qw[i] >= 0 && (done_flags[qw[i]] & ARMI_FLAG_CERTIFIED)) qw[i] = -1;
+        any |= qw[i] >= 0;
+      }
+      if (!__syncthreads_or(any)) return;  // workgroup-uniform
+    }
+  }
+  const bool has_q = qw[0] >= 0 || qw[1] >= 0 || qw[2] >= 0 || qw[3] >= 0;
   float tq[kQW];
   if constexpr (kCollect) {
     bool any = false;
@@ -1068,6 +1082,7 @@ __global__ __launch_bounds__(256) void sparse_merge_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = armi::wave_id();
+  if (flags[ql] & ARMI_FLAG_CERTIFIED) return;  // answered by the MFMA filter (kth = +inf)
   const int pool = n_wg * kKW;
   float kk[kSmPer];
   int32_t rw[kSmPer];
@@ -1415,6 +1430,8 @@ __global__ __launch_bounds__(256) void sparse_collect_merge_kernel(
   }
 }
 
+#include "sparse_filter.h"
+
 struct Workspace {
   int32_t* uterm;
   int32_t* n_terms;
@@ -1430,6 +1447,9 @@ struct Workspace {
   int* coll_count;  // [2 * kQB]: collect counts, then the helpers' done counters
   float* coll_key;
   int32_t* coll_row;
+  uint16_t* fB;     // MFMA filter: the pass's B slices [kFMaxSeg][kQB][kFK] fp16
+  float* fscale;    // its key scale
+  int32_t* felig;   // [kQB] queries the filter may answer
   size_t bytes;
 };
 
@@ -1451,6 +1471,9 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   w.coll_count = cv.take<int>(2 * kQB);
   w.coll_key = cv.take<float>((size_t)kQB * kCollectCap);
   w.coll_row = cv.take<int32_t>((size_t)kQB * kCollectCap);
+  w.fB = cv.take<uint16_t>((size_t)kFMaxSeg * kFBSlice);
+  w.fscale = cv.take<float>(1);
+  w.felig = cv.take<int32_t>(kQB);
   w.bytes = cv.off + 256;
   return w;
 }
@@ -1578,7 +1601,38 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
         skeys, nnz, vocab, idx->dense_stride, idx->dense_val);
     ARMI_LAUNCHED("dense_fill_kernel");
   }
+  // MFMA filter (sparse_filter.h): per-term scales, u8 columns of the dense terms, the CSR rows
+  uint32_t* tmax;
+  unsigned long long* n_neg;
+  ARMI_HIP(tmp.alloc(&tmax, (size_t)vocab + 1));
+  ARMI_HIP(tmp.alloc(&n_neg, 1));
+  ARMI_HIP(hipMemsetAsync(tmax, 0, ((size_t)vocab + 1) * 4, stream));
+  ARMI_HIP(hipMemsetAsync(n_neg, 0, 8, stream));
+  if (nnz > 0) {
+    term_max_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(indices, values, nnz, vocab, tmax, n_neg);
+    ARMI_LAUNCHED("term_max_kernel");
+  }
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->term_scale), std::max<size_t>(vocab, 1) * 4));
+  term_scale_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(tmax, vocab, idx->term_scale);
+  ARMI_LAUNCHED("term_scale_kernel");
+  idx->dense8_stride = (idx->n_rows + kFT - 1) / kFT * kFT + kFT;  // + the last tile's over-read
+  const size_t u8_bytes = std::max<size_t>((size_t)n_dense * idx->dense8_stride, 16);
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->dense_u8), u8_bytes));
+  ARMI_HIP(hipMemsetAsync(idx->dense_u8, 0, u8_bytes, stream));
+  if (nnz > 0 && n_dense > 0) {
+    dense_u8_fill_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(
+        idx->dense_of, reinterpret_cast<const int2*>(idx->post), skeys, nnz, vocab,
+        idx->term_scale, idx->dense8_stride, idx->dense_u8);
+    ARMI_LAUNCHED("dense_u8_fill_kernel");
+  }
+  unsigned long long negatives = 0;
+  ARMI_HIP(hipMemcpyAsync(&negatives, n_neg, 8, hipMemcpyDeviceToHost, stream));
   ARMI_HIP(hipStreamSynchronize(stream));
+  idx->filter_ok = negatives == 0;
+  idx->filter_on = true;
+  idx->row_ptr = indptr;
+  idx->row_idx = indices;
+  idx->row_val = values;
   return ARMI_OK;
 }
 
@@ -1589,6 +1643,8 @@ void free_index(armi_sparse_index* idx) {
   (void)hipFree(idx->start_tab);
   (void)hipFree(idx->dense_of);
   (void)hipFree(idx->dense_val);
+  (void)hipFree(idx->term_scale);
+  (void)hipFree(idx->dense_u8);
   delete idx;
 }
 
@@ -1741,7 +1797,13 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
   if (int rc = armi::allow_lds(pass_terms_bitmap_kernel, kPrepBmLds)) return rc;
   if (int rc = armi::allow_lds(sparse_scan_kernel<false>, kScanLds)) return rc;
   if (int rc = armi::allow_lds(sparse_scan_kernel<true>, kScanLds)) return rc;
+  if (int rc = armi::allow_lds(sparse_filter_scan_kernel, kFLds)) return rc;
   const int n_help = std::max(1, std::min(kMaxHelp, kCollectCap / k));
+  // the MFMA filter answers what it can certify; kc = the rescored candidates per query
+  const bool filter = idx->filter_ok && idx->filter_on && k <= kFMaxK && idx->n_ranges > 0;
+  const int kc = std::min(kFSel / 2, std::max(k + 32, 2 * k));
+  armi::TimedLaunch stage;
+  if (stage.begin(ARMI_TIMING_SPARSE_STAGE, stream) < 0) return ARMI_ERR_HIP;
   for (int q0 = 0; q0 < n_queries; q0 += kQB) {
     const int nqp = std::min(kQB, n_queries - q0);
     uint32_t* pflags = out_flags + q0;
@@ -1760,13 +1822,35 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
           w.qcount, w.qof, pflags, w.coll_count);
     ARMI_LAUNCHED("pass_terms_kernel");
+    if (filter) {
+      sparse_filter_prep_kernel<<<dim3(1), dim3(1024), 0, stream>>>(
+          w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof, idx->term_scale, 1, w.fB, w.fscale,
+          w.felig);
+      ARMI_LAUNCHED("sparse_filter_prep_kernel");
+      armi::TimedLaunch tf;
+      if (tf.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
+      sparse_filter_scan_kernel<<<dim3(idx->n_ranges), dim3(kFThreads), kFLds, stream>>>(
+          idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab,
+          idx->n_rows, idx->range_rows, idx->n_ranges, row_mask, w.uterm, w.n_terms, idx->dense_of,
+          idx->dense_u8, idx->dense8_stride, idx->term_scale, w.fB, w.fscale, w.cand_key,
+          w.cand_row, w.cand_bound);
+      ARMI_LAUNCHED("sparse_filter_scan_kernel");
+      if (int rc = tf.end()) return rc;
+      sparse_filter_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
+          w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, kc, idx->ordinal_base,
+          w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->row_ptr, idx->row_idx, idx->row_val,
+          out_scores, out_ids, out_count, pflags, w.kth);
+      ARMI_LAUNCHED("sparse_filter_merge_kernel");
+    }
+    // the exact scan: every query when the filter is off, else only the queries it left
+    // (the kernel exits at once when it answered all of them)
     armi::TimedLaunch tl;
-    if (tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
+    if (!filter && tl.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
     sparse_scan_kernel<false><<<dim3(idx->n_ranges), dim3(kScanThreads), kScanLds, stream>>>(
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, w.cand_key, w.cand_row, w.cand_bound, nullptr, nullptr, nullptr, nullptr, dbg,
-        idx->dense_of, idx->dense_val, idx->dense_stride);
+        idx->dense_of, idx->dense_val, idx->dense_stride, filter ? pflags : nullptr);
     ARMI_LAUNCHED("sparse_scan_kernel");
     if (int rc = tl.end()) return rc;
 #ifdef ARMI_SPARSE_PROFILE
@@ -1808,7 +1892,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->n_rows,
         idx->range_rows, idx->n_ranges, row_mask, nqp, w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof,
         w.cursors, nullptr, nullptr, nullptr, w.kth, w.coll_count, w.coll_key, w.coll_row, dbg,
-        idx->dense_of, idx->dense_val, idx->dense_stride);
+        idx->dense_of, idx->dense_val, idx->dense_stride, nullptr);
     ARMI_LAUNCHED("sparse_collect_kernel");
     sparse_collect_merge_kernel<<<dim3(nqp + n_help), dim3(256), kCollectLds, stream>>>(
         w.coll_count, w.coll_key, w.coll_row, w.coll_count + kQB, nqp, q0,
@@ -1818,6 +1902,14 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         pflags);
     ARMI_LAUNCHED("sparse_collect_merge_kernel");
   }
+  if (int rc = stage.end()) return rc;
+  return ARMI_OK;
+}
+
+int armi_sparse_index_set_filter(armi_sparse_index* index, int enable, int* usable) {
+  ARMI_REQUIRE(index != nullptr, "armi_sparse_index_set_filter: index is null");
+  index->filter_on = enable != 0;
+  if (usable) *usable = index->filter_ok ? 1 : 0;
   return ARMI_OK;
 }
 

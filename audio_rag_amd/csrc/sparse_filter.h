@@ -1,0 +1,732 @@
+// Certified MFMA filter of the sparse search (round 6). Included by sparse.hip inside its
+// anonymous namespace: uses its pass layout (QTerm lists per query slot, the pass's ascending
+// distinct terms uterm[u]), range partition, range_cursor, ord_key_f and the candidate-list
+// workspace of the exact scan.
+//
+// Restates the same search as sparse.hip (Qdrant's sparse dot product, qdrant.py:289-312):
+// score(q, d) = fp32 sum, ascending shared index, of fl32(q_i * d_i). The exact scan computes it
+// for every row with one VALU multiply and add per (query, term, row), and three rounds of tuning
+// left it issue-bound at ~0.18 ms per 64-query pass. Here every row instead gets an
+// UPPER BOUND of its score from the matrix cores, and only the best few rows per query are
+// scored exactly:
+//
+//   index build: every value v >= 0 of a term in >= 1/8 of the rows (a dense column) is stored as
+//     the u8 level a = ceil(v / s_t), s_t = RU(max_t / 255), so a * s_t >= v exactly (1 B per row
+//     and term, half of the fp16 bytes and a quarter of the fp32 columns the exact scan reads);
+//     posting terms (df < rows / 8) get their levels from the same rule while they are staged.
+//   per pass (prep): B[u][q] = RU16(w_qu * s_u * 2^e) >= w * s * 2^e, one fp16 per (term, query),
+//     e chosen per pass to keep B well inside fp16's range (never subnormal: clamped to 2^-14).
+//   scan: rows in 1024-row tiles, the pass's terms in 16-term steps. Each step stages the u8
+//     column tiles (one 16-B load per lane, prefetched four steps ahead in registers; a posting
+//     term's next 128 postings, scattered) into a [16 term][1024 row] fp16 LDS image, and
+//     v_mfma_f32_32x32x16_f16 multiplies it (A operand by ds_read_b64_tr_b16: the image is
+//     term-major, the operand wants 8 terms of one row per lane) with the step's B slice. key =
+//     acc * scale_up >= the row's exact fp32 score: every product a * B >= w * v, and the fp32
+//     roundings of both the reference's sum and the MFMA accumulation are covered by
+//     scale_up = 2^-e (1 + (nU + 600) 2^-22) (at most 2 (256 + 2 nU) roundings of 2^-23 each).
+//     Per lane x query a 3-deep list of (key, row) plus the largest key it dropped; per
+//     workgroup and query the best 16 entries and a bound on everything else.
+//   merge (per query): the pool's entries from the kc-th largest list maximum up are rescored
+//     exactly from the caller's CSR rows (the products of the shared terms, added in ascending
+//     term order: the oracle's and the exact scan's arithmetic); the query is CERTIFIED when its
+//     k-th exact score exceeds every bound of a row not rescored (keys never under-state a
+//     score), and then answered. Queries that cannot be certified (ties at the boundary, fewer
+//     than k sharing rows, negative weights) keep their flags and take the exact scan, which
+//     skips certified queries and exits at once when none is left.
+//
+// Limits: an index with a negative value, a pass of more than 512 distinct terms or k > 128
+// does not use the filter (the exact scan answers), and neither does a query with a negative or
+// non-finite weight.
+
+constexpr int kFT = 1024;                      // rows per filter tile
+constexpr int kFK = 16;                        // terms per step (one MFMA k-step)
+constexpr int kFWaves = 8;
+constexpr int kFThreads = kFWaves * 64;
+constexpr int kFDepth = 4;                     // steps in flight (register ring)
+constexpr int kFMaxSeg = 32;                   // a held term per lane pair: 32 steps of 16 terms
+constexpr int kFMaxU = kFMaxSeg * kFK;         // distinct terms of a filtered pass, at most 512
+constexpr int kFImgStride = kFT * 2 + 64;      // bytes per term row of the image (+64: the
+                                               // transposed reads of a half-wave hit 64 banks)
+constexpr int kFImgBytes = kFK * kFImgStride;
+constexpr int kFBRow = 48;                     // LDS bytes per query of a B slice (32 + 16 pad)
+constexpr int kFBBytes = kQB * kFBRow;
+constexpr int kFBSlice = kQB * kFK;            // halves per B slice in the workspace [q][16]
+constexpr int kFList = 3;                      // lane list depth
+constexpr int kFLanes = 2 * kFWaves;           // lane lists per query and workgroup
+constexpr int kFPool = kFLanes * kFList;       // their entries (48)
+constexpr size_t kFLds = (size_t)2 * kFImgBytes + 2 * kFBBytes + 256;
+constexpr int kFSel = 1024;                    // rescored candidates per query, at most
+constexpr int kFVal = 8192;                    // (row, term) value slots of one rescore chunk
+constexpr int kFMaxK = 128;
+constexpr int32_t kFNone = (int32_t)0x80000000;  // held-term cursor of "no term"
+static_assert(kQB * kFPool * 8 + kQB * kFLanes * 4 <= 2 * kFImgBytes, "merge overlays the images");
+static_assert(kFMaxSeg * 2 <= 64, "one lane per held term");
+
+__host__ __device__ inline int filter_segments(int n_u) {
+  const int s = (n_u + kFK - 1) / kFK;
+  return s > kFDepth - 1 ? s : kFDepth - 1;  // a term's next tile issues after its last finish
+}
+
+typedef _Float16 fhalf2 __attribute__((ext_vector_type(2)));
+typedef _Float16 fhalf8 __attribute__((ext_vector_type(8)));
+typedef float ff32x16 __attribute__((ext_vector_type(16)));
+typedef short fs4 __attribute__((ext_vector_type(4)));
+typedef uint32_t fu32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t fu32x2 __attribute__((ext_vector_type(2)));
+typedef int32_t fp4 __attribute__((ext_vector_type(4), aligned(8)));
+
+// Quantisation level of a value: the least integer a with a * s >= v (a in [0, 255] since
+// 255 s >= the term's largest value; 0 for v = 0 or -0.0). The fixup makes the bound exact
+// whatever the rounding of the division (the product is exact in fp64).
+__host__ __device__ inline float u8_level(float v, float s) {
+  if (!(v > 0.f) || !(s > 0.f)) return 0.f;
+  float a = ceilf(v / s);
+  if ((double)a * (double)s < (double)v) a += 1.f;
+  return a > 255.f ? 255.f : a;
+}
+
+// 4 bytes -> 4 fp16 (exact): byte b as fp16 bits 0x64bb = 1024 + b, minus 1024.
+__device__ __forceinline__ fu32x2 u8x4_f16(uint32_t x) {
+  const fhalf2 l = __builtin_bit_cast(fhalf2, __builtin_amdgcn_perm(0x64646464u, x, 0x04010400u));
+  const fhalf2 h = __builtin_bit_cast(fhalf2, __builtin_amdgcn_perm(0x64646464u, x, 0x04030402u));
+  const fhalf2 o = {(_Float16)1024.0f, (_Float16)1024.0f};
+  return fu32x2{__builtin_bit_cast(uint32_t, l - o), __builtin_bit_cast(uint32_t, h - o)};
+}
+
+// Smallest fp16 >= p (p >= 0; +inf above the fp16 range), never subnormal (>= 2^-14 for p > 0):
+// the MFMA operand of a weight * scale product.
+__device__ __forceinline__ uint16_t ru_half(double p) {
+  if (!(p > 0.0)) return 0;
+  float f = (float)p;
+  if ((double)f < p) f = __uint_as_float(__float_as_uint(f) + 1u);
+  uint16_t b = __builtin_bit_cast(uint16_t, (_Float16)f);
+  if ((float)__builtin_bit_cast(_Float16, b) < f) b = (uint16_t)(b + 1);
+  return b < 0x0400 ? (uint16_t)0x0400 : b;
+}
+
+// ---------------------------------------------------------------------------- index build
+
+// tmax[t] = bit pattern of the largest value of term t (values >= 0 order as their bits;
+// -0.0 counts as 0), n_neg = values < 0.
+__global__ void term_max_kernel(const int32_t* __restrict__ indices, const float* __restrict__ values,
+                                int64_t nnz, int32_t vocab, uint32_t* __restrict__ tmax,
+                                unsigned long long* __restrict__ n_neg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool neg = false;
+  if (i < nnz) {
+    const float v = values[i];
+    const int32_t t = indices[i];
+    neg = v < 0.f;
+    if (!neg && v > 0.f && t >= 0 && t < vocab) atomicMax(&tmax[t], __float_as_uint(v));
+  }
+  const unsigned long long m = __ballot(neg);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_neg, (unsigned long long)__popcll(m));
+}
+
+// s_t = the least fp32 >= max_t / 255 with 255 s_t >= max_t (checked in fp64)
+__global__ void term_scale_kernel(const uint32_t* __restrict__ tmax, int32_t vocab,
+                                  float* __restrict__ scale) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= vocab) return;
+  const float m = __uint_as_float(tmax[t]);
+  float s = m / 255.f;
+  while (255.0 * (double)s < (double)m) s = __uint_as_float(__float_as_uint(s) + 1u);
+  scale[t] = m > 0.f ? s : 0.f;
+}
+
+// u8 level of every posting of a dense term into its column (sorted entry i: see dense_fill)
+__global__ void dense_u8_fill_kernel(const int32_t* __restrict__ dense_of,
+                                     const int2* __restrict__ post,
+                                     const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
+                                     const float* __restrict__ scale, int64_t stride,
+                                     uint8_t* __restrict__ dense_u8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const uint32_t t = skeys[i];
+  if (t >= (uint32_t)vocab) return;
+  const int32_t d = dense_of[t];
+  if (d < 0) return;
+  const int2 pv = post[i + t];
+  dense_u8[(size_t)d * stride + pv.x] = (uint8_t)u8_level(__int_as_float(pv.y), scale[t]);
+}
+
+// ---------------------------------------------------------------------------- per pass
+
+// One block: the pass's B slices fB[seg][q][16] (fp16 bits), scale_up, and per query whether
+// the filter may answer it (felig). A query is eligible when the index allows the filter, the
+// pass has at most 512 distinct terms and every weight of the query is finite and >= 0.
+__global__ __launch_bounds__(1024) void sparse_filter_prep_kernel(
+    const int32_t* __restrict__ uterm, const int32_t* __restrict__ n_terms,
+    const QTerm* __restrict__ ql, const int32_t* __restrict__ qu,
+    const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
+    const float* __restrict__ term_scale, int filter_ok, uint16_t* __restrict__ fB,
+    float* __restrict__ fscale, int32_t* __restrict__ felig) {
+  __shared__ double wmax[16];
+  __shared__ int elig_s[kQB];
+  __shared__ int e_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
+  const int nU = *n_terms;
+  const bool pass_ok = filter_ok && nU <= kFMaxU;
+  const int nSeg = filter_segments(nU);
+  if (pass_ok) {
+    uint4* b4 = reinterpret_cast<uint4*>(fB);
+    for (int i = tid; i < nSeg * kFBSlice / 8; i += 1024) b4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  double mx = 0.0;
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    const int slot = wave * kQW + i;
+    const int q = qof[slot];
+    const int n = q >= 0 ? qcount[slot] : 0;
+    bool bad = false;
+    double m = 0.0;
+    for (int j = lane; j < n; j += 64) {
+      const float w = ql[slot * kQStride + j].w;
+      const float s = term_scale[uterm[qu[slot * kQStride + j]]];
+      bad |= !(w >= 0.f) || !isfinite(w);  // NaN fails w >= 0
+      m = fmax(m, (double)w * (double)s);
+    }
+    const bool ok = pass_ok && q >= 0 && __ballot(bad) == 0ull;
+    if (ok) mx = fmax(mx, m);
+    if (lane == 0 && q >= 0) elig_s[q] = ok ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  if (lane == 0) wmax[wave] = mx;
+  __syncthreads();
+  if (tid == 0) {
+    double m = 0.0;
+    for (int w = 0; w < 16; ++w) m = fmax(m, wmax[w]);
+    int x = 0;
+    if (m > 0.0) (void)frexp(m, &x);  // m < 2^x
+    int e = 14 - x;                   // every B < 2^14
+    e = e < -100 ? -100 : (e > 110 ? 110 : e);
+    e_s = e;
+    const double d = ldexp(1.0 + (double)(nU + 600) * 0x1p-22, -e);
+    float f = (float)d;
+    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
+    *fscale = f;
+  }
+  __syncthreads();
+  if (tid < kQB) felig[tid] = 0;
+  __syncthreads();
+  const int e = e_s;
+#pragma unroll
+  for (int i = 0; i < kQW; ++i) {
+    const int slot = wave * kQW + i;
+    const int q = qof[slot];
+    if (q < 0 || !elig_s[q]) continue;  // wave-uniform
+    if (lane == 0) felig[q] = 1;
+    const int n = qcount[slot];
+    for (int j = lane; j < n; j += 64) {
+      const int u = qu[slot * kQStride + j];
+      const float w = ql[slot * kQStride + j].w;
+      const float s = term_scale[uterm[u]];
+      fB[(size_t)(u / kFK) * kFBSlice + q * kFK + (u % kFK)] =
+          ru_half(ldexp((double)w * (double)s, e));
+    }
+  }
+}
+
+// The filter scan: one 512-thread workgroup per row range (the exact scan's ranges), steps =
+// (1024-row tile, 16 terms). Wave w stages terms 16 seg + 2 w + j (j = 0, 1) of every step:
+// its held terms' cursors sit in lane 2 seg + j of creg (x: posting cursor, or -(d + 1) for
+// dense column d, or kFNone; y: row of the cursor's posting) and their scales in sreg. The
+// MFMAs: wave w owns row blocks 4 w .. 4 w + 3 (32 rows each) x both 32-query halves.
+__global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
+    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
+    const int32_t* __restrict__ long_of, const int32_t* __restrict__ start_tab, int64_t n_rows,
+    int64_t range_rows, int n_ranges, const uint64_t* __restrict__ row_mask,
+    const int32_t* __restrict__ uterm, const int32_t* __restrict__ n_terms,
+    const int32_t* __restrict__ dense_of, const uint8_t* __restrict__ dense_u8, int64_t stride8,
+    const float* __restrict__ term_scale, const uint16_t* __restrict__ fB,
+    const float* __restrict__ fscale, float* __restrict__ cand_key,
+    int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  const int g = blockIdx.x;
+  const int wave = armi::wave_id();
+  const int lane = threadIdx.x & 63;
+  const int nU = *n_terms;
+  if (nU == 0 || nU > kFMaxU) return;  // workgroup-uniform: the merge / exact scan answer
+  const int nSeg = filter_segments(nU);
+  const int64_t lo = (int64_t)g * range_rows;
+  const int64_t hi = min(lo + range_rows, n_rows);
+  const int n_tiles = hi > lo ? (int)((hi - lo + kFT - 1) / kFT) : 0;
+  const int S = n_tiles * nSeg;
+  const float scale = *fscale;
+  unsigned char* const bimg = fsm + 2 * kFImgBytes;                  // [2][kQB][kFBRow]
+  unsigned char* const trash = fsm + 2 * kFImgBytes + 2 * kFBBytes;  // scatter sink
+
+  int2 creg = make_int2(kFNone, 0);
+  float sreg = 0.f;
+  {
+    const int sg = lane >> 1, u = sg * kFK + 2 * wave + (lane & 1);
+    if (sg < nSeg && u < nU) {
+      const int32_t t = uterm[u];
+      const int32_t d = dense_of[t];
+      sreg = term_scale[t];
+      creg = d >= 0 ? make_int2(-(d + 1), 0)
+                    : range_cursor(t, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
+    }
+  }
+  const int rev2 = 2 * (63 - lane);
+  fp4 ring[kFDepth][2];
+  uint32_t ringb[kFDepth];
+  auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * kFT, hi); };
+  // step s's loads into ring slot `slot`: every lane issues the same three loads per step
+  // (steps past the end and absent terms read a fixed in-bounds address), so the waits the
+  // compiler counts stay exact
+  auto issue = [&](int s, int slot) {
+    const bool live = s < S;
+    const int tile = live ? s / nSeg : 0;
+    const int seg = live ? s - tile * nSeg : 0;
+    const int64_t tlo = lo + (int64_t)tile * kFT;
+    const int32_t thi = tile_hi(tile);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = 2 * seg + j;
+      const int cx = rl_i(creg.x, c), cy = rl_i(creg.y, c);
+      const fp4* src = reinterpret_cast<const fp4*>(post + rev2);
+      if (live && cx != kFNone) {
+        if (cx < 0)
+          src = reinterpret_cast<const fp4*>(dense_u8 + (size_t)(-cx - 1) * stride8 + tlo + 16 * lane);
+        else if (cy < thi)
+          src = reinterpret_cast<const fp4*>(post + cx + rev2);
+      }
+      ring[slot][j] = *src;
+    }
+    ringb[slot] = reinterpret_cast<const uint32_t*>(fB)[(size_t)seg * (kFBSlice / 2) + 64 * wave + lane];
+  };
+  // step s from ring slot `slot` into LDS buffer par: the held terms' rows of the image (u8
+  // levels as fp16; a posting term's row cleared and its in-tile postings scattered; an absent
+  // term's row zero) and the wave's 256 B of the B slice
+  auto finish = [&](int s, int slot, int par) {
+    if (s >= S) return;  // uniform
+    const int tile = s / nSeg, seg = s - tile * nSeg;
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * kFT);
+    const int32_t thi = tile_hi(tile);
+    unsigned char* img = fsm + par * kFImgBytes;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = 2 * seg + j;
+      const int cx = rl_i(creg.x, c), cy = rl_i(creg.y, c);
+      unsigned char* rowp = img + (2 * wave + j) * kFImgStride;
+      fu32x4* dst = reinterpret_cast<fu32x4*>(rowp + 32 * lane);
+      if (cx != kFNone && cx < 0) {
+        const fp4 v = ring[slot][j];
+        const fu32x2 a = u8x4_f16((uint32_t)v.x), b = u8x4_f16((uint32_t)v.y);
+        const fu32x2 cc = u8x4_f16((uint32_t)v.z), dd = u8x4_f16((uint32_t)v.w);
+        dst[0] = fu32x4{a.x, a.y, b.x, b.y};
+        dst[1] = fu32x4{cc.x, cc.y, dd.x, dd.y};
+        continue;
+      }
+      dst[0] = fu32x4{0u, 0u, 0u, 0u};
+      dst[1] = fu32x4{0u, 0u, 0u, 0u};
+      if (cx == kFNone || cy >= thi) continue;  // no posting of the term in this tile
+      const float sc = rl_f(sreg, c);
+      fp4 v = ring[slot][j];
+      int adv = 0;  // postings consumed before v
+      while (true) {  // wave-uniform trip count
+        const uint64_t be = __ballot(v.x < thi), bo = __ballot(v.z < thi);
+        const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
+        const int no = bo == ~0ull ? 64 : __builtin_clzll(~bo);
+        const int n = min(2 * ne, 2 * no + 1);  // postings of v inside the tile
+        const _Float16 a0 = (_Float16)u8_level(__int_as_float(v.y), sc);
+        const _Float16 a1 = (_Float16)u8_level(__int_as_float(v.w), sc);
+        unsigned char* d0 = rev2 < n ? rowp + 2 * (v.x - tlo) : trash + 2 * lane;
+        unsigned char* d1 = rev2 + 1 < n ? rowp + 2 * (v.z - tlo) : trash + 2 * lane;
+        *reinterpret_cast<_Float16*>(d0) = a0;
+        *reinterpret_cast<_Float16*>(d1) = a1;
+        if (n < 128) {
+          const int nl = 63 - (n >> 1);
+          const int32_t re = rl_i(v.x, nl), ro = rl_i(v.z, nl);
+          if (lane == c) {
+            creg.x = cx + adv + n;
+            creg.y = (n & 1) ? ro : re;
+          }
+          break;
+        }
+        adv += 128;
+        v = *reinterpret_cast<const fp4*>(post + cx + adv + rev2);
+      }
+    }
+    const int bi = 64 * wave + lane;  // dword of the slice: query bi / 8, dword bi % 8
+    *reinterpret_cast<uint32_t*>(bimg + par * kFBBytes + (bi >> 3) * kFBRow + 4 * (bi & 7)) =
+        ringb[slot];
+  };
+
+  ff32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    acc[i][0] = ff32x16{};
+    acc[i][1] = ff32x16{};
+  }
+  // transposed-read addresses of the A operand (T10): lane 4 q + p of each 16-lane group
+  // supplies term row kb + q (+ 4 for the second read), data rows rb + 4 p .. + 3
+  const int li = lane & 15;
+  const int a_off = (8 * (lane >> 5) + (li >> 2)) * kFImgStride + 2 * (16 * ((lane >> 4) & 1) + 4 * (li & 3));
+  const int b_off = (lane & 31) * kFBRow + 16 * (lane >> 5);
+  auto compute = [&](int par) {
+    const unsigned char* img = fsm + par * kFImgBytes;
+    const unsigned char* bb = bimg + par * kFBBytes;
+    const fu32x4 b0 = *reinterpret_cast<const fu32x4*>(bb + b_off);
+    const fu32x4 b1 = *reinterpret_cast<const fu32x4*>(bb + 32 * kFBRow + b_off);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned char* p = img + a_off + 2 * 32 * (4 * wave + i);
+      typedef __attribute__((address_space(3))) fs4 lds_fs4;
+      const fs4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_fs4*)(p));
+      const fs4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_fs4*)(p + 4 * kFImgStride));
+      const fu32x2 l2 = __builtin_bit_cast(fu32x2, lo4), h2 = __builtin_bit_cast(fu32x2, hi4);
+      const fhalf8 a = __builtin_bit_cast(fhalf8, fu32x4{l2.x, l2.y, h2.x, h2.y});
+      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(fhalf8, b0), acc[i][0], 0, 0, 0);
+      acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(fhalf8, b1), acc[i][1], 0, 0, 0);
+    }
+  };
+
+  // per lane and query half: a 3-deep (key, row) list and the best key it dropped
+  float ls[2][kFList], disc[2];
+  int32_t lr[2][kFList];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    disc[h] = kNegInf;
+#pragma unroll
+    for (int e = 0; e < kFList; ++e) {
+      ls[h][e] = kNegInf;
+      lr[h][e] = kEndRow;
+    }
+  }
+  auto insert = [&](int h, float x, int32_t r) {
+#pragma unroll
+    for (int e = 0; e < kFList; ++e) {
+      const bool c = x > ls[h][e];
+      const float ts = c ? x : ls[h][e];
+      const int32_t tr = c ? r : lr[h][e];
+      x = c ? ls[h][e] : x;
+      r = c ? lr[h][e] : r;
+      ls[h][e] = ts;
+      lr[h][e] = tr;
+    }
+    disc[h] = fmaxf(disc[h], x);
+  };
+  // the tile's keys into the lane lists; accumulators cleared. Row of register v of block i:
+  // 32 (4 w + i) + 8 (v / 4) + 4 (lane / 32) + v % 4 (the 32x32 MFMA output layout)
+  auto epilogue = [&](int tile) {
+    const int32_t tlo = (int32_t)(lo + (int64_t)tile * kFT);
+    const int32_t thi = tile_hi(tile);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t rb = tlo + 32 * (4 * wave + i);
+      uint32_t mb = 0xffffffffu;
+      if (row_mask) {
+        const uint64_t w64 = rb < thi ? row_mask[rb >> 6] : 0ull;
+        mb = (uint32_t)(w64 >> (rb & 32));
+      }
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int off = 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        const int32_t r = rb + off;
+        const bool ok = r < thi && ((mb >> off) & 1u);
+        insert(0, ok ? acc[i][0][v] * scale : kNegInf, r);
+        insert(1, ok ? acc[i][1][v] * scale : kNegInf, r);
+      }
+      acc[i][0] = ff32x16{};
+      acc[i][1] = ff32x16{};
+    }
+  };
+
+  // prologue: the first kFDepth - 1 steps in flight, step 0 staged
+#pragma unroll
+  for (int p = 0; p < kFDepth - 1; ++p) issue(p, p);
+  finish(0, 0, 0);
+  __syncthreads();
+  // step s: issue s + 3 (ring slot (s + 3) % 4), multiply image s % 2, epilogue at a tile's last
+  // step, stage s + 1 (slot (s + 1) % 4) into the other image, one barrier
+  for (int s0 = 0; s0 < S; s0 += kFDepth) {
+#pragma unroll
+    for (int d = 0; d < kFDepth; ++d) {
+      const int s = s0 + d;
+      if (s < S) {  // uniform
+        issue(s + kFDepth - 1, (d + kFDepth - 1) % kFDepth);
+        compute(d & 1);
+        const int tile = s / nSeg;
+        if (s - tile * nSeg == nSeg - 1) epilogue(tile);
+        finish(s + 1, (d + 1) % kFDepth, (d + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+
+  // workgroup merge: per query the 48 lane-list entries and 16 dropped bounds through LDS (over
+  // the images), then one wave per 8 queries keeps the best 16 and the bound of the rest
+  float* mkey = reinterpret_cast<float*>(fsm);                        // [kQB][kFPool]
+  int32_t* mrow = reinterpret_cast<int32_t*>(fsm + kQB * kFPool * 4);  // [kQB][kFPool]
+  float* mdisc = reinterpret_cast<float*>(fsm + kQB * kFPool * 8);     // [kQB][kFLanes]
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = 32 * h + (lane & 31);
+    const int base = q * kFPool + 2 * kFList * wave + kFList * (lane >> 5);
+#pragma unroll
+    for (int e = 0; e < kFList; ++e) {
+      mkey[base + e] = ls[h][e];
+      mrow[base + e] = lr[h][e];
+    }
+    mdisc[q * kFLanes + 2 * wave + (lane >> 5)] = disc[h];
+  }
+  __syncthreads();
+  float key[8], bq[8];
+  int32_t row[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int q = 8 * wave + n;
+    key[n] = lane < kFPool ? mkey[q * kFPool + lane] : kNegInf;
+    row[n] = lane < kFPool ? mrow[q * kFPool + lane] : kEndRow;
+    bq[n] = lane < kFLanes ? mdisc[q * kFLanes + lane] : kNegInf;
+  }
+  armi::wave_sort_approx_desc_n<8>(key, row);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) bq[n] = fmaxf(bq[n], lane == kKW ? key[n] : kNegInf);
+  armi::wave_max_all_n<8>(bq);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const size_t base = (size_t)g * kQB + 8 * wave + n;
+    if (lane < kKW) {
+      cand_key[base * kKW + lane] = key[n];
+      cand_row[base * kKW + lane] = row[n];
+    }
+    if (lane == 0) cand_bound[base] = bq[n];
+  }
+}
+
+// Per query of the pass: the kc best keys' rows (and every pool entry tied with the kc-th list
+// maximum) rescored exactly from the caller's CSR, sorted (score desc, row asc); certified when
+// the k-th exact score exceeds the bound of every row left out. Certified queries are answered
+// and flagged (CERTIFIED | FILTERED) with kth = +inf, so the exact scan and its collect pass
+// skip them; the others are left to the exact scan.
+__global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
+    const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
+    const float* __restrict__ cand_bound, int n_wg, int q_first, int k, int kc,
+    int64_t ordinal_base, const int32_t* __restrict__ felig, const int32_t* __restrict__ uterm,
+    const QTerm* __restrict__ qlist, const int32_t* __restrict__ qu,
+    const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ row_idx,
+    const float* __restrict__ row_val, float* __restrict__ out_scores,
+    int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags,
+    float* __restrict__ kth_out) {
+  __shared__ float skey[kFSel];
+  __shared__ int32_t srow[kFSel];
+  __shared__ float vals[kFVal];
+  __shared__ int32_t rst[kFSel];
+  __shared__ int32_t rln[kFSel];
+  __shared__ int32_t roff[kFSel + 1];
+  __shared__ int32_t tterm[kMaxTerms];
+  __shared__ float tw[kMaxTerms];
+  __shared__ uint32_t umax[256];
+  __shared__ float red[8];
+  __shared__ int32_t wsum[4];
+  __shared__ float t0s;
+  __shared__ int sh[4];  // [0] selected, [1] slot, [2] members
+  const int ql = blockIdx.x;
+  const int qg = q_first + ql;
+  const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
+  if (!felig[ql]) return;  // uniform: the exact scan answers
+  if (tid == 0) {
+    sh[0] = 0;
+    sh[2] = 0;
+  }
+  if (tid < kQB && qof[tid] == ql) sh[1] = tid;
+  __syncthreads();
+  const int slot = sh[1];
+  const int nt = qcount[slot];
+  auto answer = [&](int count) {  // skey / srow sorted, count valid entries
+    if (wave != 0) return;
+    for (int c = lane; c < k; c += 64) {
+      const size_t o = (size_t)qg * k + c;
+      out_scores[o] = c < count ? skey[c] : kNegInf;
+      out_ids[o] = c < count ? ordinal_base + srow[c] : -1;
+    }
+    if (lane == 0) {
+      out_count[qg] = count;
+      flags[ql] |= ARMI_FLAG_CERTIFIED | ARMI_FLAG_FILTERED;
+      kth_out[ql] = std::numeric_limits<float>::infinity();
+    }
+  };
+  if (nt == 0) {  // no terms: no row shares an index (every pool key is a stand-in)
+    answer(0);
+    return;
+  }
+  // the pool (16 sorted entries per range list), its list bounds and maxima
+  const int pool = n_wg * kKW;
+  float kk[kSmPer];
+  int32_t rw[kSmPer];
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    const int e = tid + 256 * j;
+    const size_t src = ((size_t)(e / kKW) * kQB + ql) * kKW + (e % kKW);
+    kk[j] = e < pool ? cand_key[src] : kNegInf;
+    rw[j] = e < pool ? cand_row[src] : 0;
+  }
+  float b = tid < n_wg ? cand_bound[(size_t)tid * kQB + ql] : kNegInf;
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    const int e = tid + 256 * j;
+    if (e < pool && e % kKW == 0) umax[e / kKW] = ord_key_f(kk[j]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
+  if (lane == 0) red[wave] = b;
+  __syncthreads();
+  if (wave == 0) {  // t0 = kc-th largest list maximum (one-wave radix select)
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gg = lane + 64 * i;
+      u[i] = gg < n_wg ? umax[gg] : ord_key_f(kNegInf);
+    }
+    float t0 = kNegInf;
+    if (n_wg >= kc) {
+      uint32_t prefix = 0;
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = prefix | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(u[i] >= cand));
+        if (cnt >= kc) prefix = cand;
+      }
+      t0 = from_ord_key_f(prefix);
+    }
+    if (lane == 0) t0s = t0;
+  }
+  __syncthreads();
+  const float t0 = t0s;
+  float dmax = kNegInf;
+#pragma unroll
+  for (int j = 0; j < kSmPer; ++j) {
+    if (kk[j] == kNegInf) continue;
+    if (kk[j] >= t0) {
+      const int s = atomicAdd(&sh[0], 1);
+      if (s < kFSel) srow[s] = rw[j];
+    } else {
+      dmax = fmaxf(dmax, kk[j]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
+  if (lane == 0) red[4 + wave] = dmax;
+  for (int j = tid; j < nt; j += 256) {
+    tterm[j] = uterm[qu[slot * kQStride + j]];
+    tw[j] = qlist[slot * kQStride + j].w;
+  }
+  __syncthreads();
+  const int n_sel = sh[0];
+  if (n_sel > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
+  float bound = red[0];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
+
+  // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
+  const int chunk = max(1, kFVal / nt);
+  for (int c0 = 0; c0 < n_sel; c0 += chunk) {
+    const int nr = min(chunk, n_sel - c0);
+    for (int i = tid; i < nr * nt; i += 256) vals[i] = __uint_as_float(0xffffffffu);
+    for (int i = tid; i < nr; i += 256) {
+      const int32_t r = srow[c0 + i];
+      const int64_t a = row_ptr[r];
+      rst[i] = (int32_t)a;
+      rln[i] = (int32_t)(row_ptr[r + 1] - a);
+    }
+    __syncthreads();
+    {  // roff = exclusive prefix of rln (4 entries per thread)
+      int loc[4], tsum = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * tid + u;
+        loc[u] = i < nr ? rln[i] : 0;
+        tsum += loc[u];
+      }
+      int x = tsum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      if (lane == 63) wsum[wave] = x;
+      __syncthreads();
+      int before = x - tsum;
+      for (int w = 0; w < wave; ++w) before += wsum[w];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * tid + u;
+        if (i < nr) roff[i] = before;
+        before += loc[u];
+      }
+      if (tid == 0) roff[nr] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      __syncthreads();
+    }
+    const int E = roff[nr];
+    for (int e0 = tid; e0 < E; e0 += 256 * 4) {
+      int ri[4], pos[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u;
+        int a = 0, n = nr;  // last row whose entries start at or before e
+        while (n > 1) {
+          const int h = n >> 1;
+          if (roff[a + h] <= e) a += h;
+          n -= h;
+        }
+        ri[u] = a;
+        pos[u] = e < E ? rst[a] + (e - roff[a]) : -1;
+      }
+      int32_t ix[4];
+      float vx[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ix[u] = pos[u] >= 0 ? row_idx[pos[u]] : -1;
+        vx[u] = pos[u] >= 0 ? row_val[pos[u]] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pos[u] < 0) continue;
+        int a = 0, n = nt;  // first query term >= ix
+        while (n > 0) {
+          const int h = n >> 1;
+          if (tterm[a + h] < ix[u]) {
+            a += h + 1;
+            n -= h + 1;
+          } else {
+            n = h;
+          }
+        }
+        if (a < nt && tterm[a] == ix[u]) vals[ri[u] * nt + a] = vx[u];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nr; i += 256) {
+      float s = 0.f;
+      bool hit = false;
+      for (int p = 0; p < nt; ++p) {
+        const float v = vals[i * nt + p];
+        if (__float_as_uint(v) != 0xffffffffu) {
+          s = __fadd_rn(s, __fmul_rn(tw[p], v));  // the reference's order and rounding
+          hit = true;
+        }
+      }
+      skey[c0 + i] = hit ? s : kNegInf;
+    }
+    __syncthreads();
+  }
+  const int n2 = armi::pow2_at_least(max(max(n_sel, k), 2));
+  for (int e = n_sel + tid; e < n2; e += 256) {
+    skey[e] = kNegInf;
+    srow[e] = kEndRow;
+  }
+  int mem = 0;
+  for (int e = tid; e < n_sel; e += 256) mem += skey[e] != kNegInf;
+  if (mem) atomicAdd(&sh[2], mem);
+  armi::lds_sort_approx_desc(skey, srow, n2);
+  const int members = sh[2];
+  const bool certified = members >= k ? skey[k - 1] > bound : bound == kNegInf;
+  if (certified) answer(min(members, k));
+}

@@ -215,6 +215,14 @@ class SparseIndex:
     def workspace_bytes(self, n_queries: int, k: int) -> int:
         return int(query("armi_sparse_workspace_bytes", self._handle, n_queries, k))
 
+    def set_filter(self, enable: bool) -> bool:
+        """Turns armi_sparse_topk's MFMA filter on / off (on by default; off = the exact scan
+        alone, the same results); returns whether the index can use it (every value >= 0)."""
+        usable = ctypes.c_int()
+        torch.cuda.current_stream(self.device).synchronize()
+        call("armi_sparse_index_set_filter", self._handle, int(bool(enable)), ctypes.byref(usable))
+        return bool(usable.value)
+
     def topk(self, q_indptr: torch.Tensor, q_indices: torch.Tensor, q_values: torch.Tensor, k: int,
              row_mask: torch.Tensor | None = None, workspace: torch.Tensor | None = None) -> TopK:
         """Sparse dot top-k for a query CSR (q_indptr int32 [B+1], ascending q_indices int32,

@@ -60,6 +60,8 @@ extern "C" {
 /* flags written per query by the top-k entry points */
 #define ARMI_FLAG_CERTIFIED 1u /* fast path proved its top-k equal to the exact ranking */
 #define ARMI_FLAG_FALLBACK 2u  /* fast path could not prove it; exact scan produced the answer */
+#define ARMI_FLAG_FILTERED 4u  /* sparse: answered by the MFMA filter + exact rescore (with
+                                * ARMI_FLAG_CERTIFIED) instead of the exact scan */
 
 const char* armi_last_error(void);
 int armi_abi_version(void);
@@ -169,13 +171,16 @@ int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
  * launch of a timed kernel is bracketed by a HIP event pair on the stream it is launched on.
  * _read synchronises on the recorded events of one slot, returns the summed kernel time and the
  * launch count, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
- * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (sparse_scan_kernel of armi_sparse_topk),
- * ARMI_TIMING_ENCODER_GEMM (the cross-encoder GEMMs of armi_enc_linear_f16).
+ * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (the dominant scan of armi_sparse_topk: the MFMA
+ * filter scan when the filter runs, else sparse_scan_kernel), ARMI_TIMING_ENCODER_GEMM (the
+ * cross-encoder GEMMs of armi_enc_linear_f16), ARMI_TIMING_SPARSE_STAGE (a whole
+ * armi_sparse_topk call).
  * armi_scan_timing_read = armi_kernel_timing_read(ARMI_TIMING_DENSE_SCAN, ...). */
 #define ARMI_TIMING_DENSE_SCAN 0
 #define ARMI_TIMING_SPARSE_SCAN 1
 #define ARMI_TIMING_ENCODER_GEMM 2
-#define ARMI_TIMING_SLOTS 3
+#define ARMI_TIMING_SPARSE_STAGE 3  /* the whole armi_sparse_topk call (every pass, every kernel) */
+#define ARMI_TIMING_SLOTS 4
 int armi_scan_timing_enable(int enable);
 int armi_scan_timing_read(double* total_ms, int64_t* launches);
 int armi_kernel_timing_read(int slot, double* total_ms, int64_t* launches);
@@ -261,7 +266,8 @@ int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, const int3
 typedef struct armi_sparse_index armi_sparse_index;
 
 /* CSR corpus: indptr [n_rows+1] int64, indices [nnz] int32 (strictly ascending per row),
- * values [nnz] float. Caller-owned, must outlive the index. */
+ * values [nnz] float. Caller-owned, must outlive the index (the filter's exact rescore reads
+ * the rows). */
 int armi_sparse_index_create(int device, const int64_t* indptr, const int32_t* indices,
                              const float* values, int64_t n_rows, int64_t nnz, int32_t vocab,
                              int64_t ordinal_base, armi_sparse_index** out, hipStream_t stream);
@@ -276,12 +282,22 @@ size_t armi_sparse_workspace_bytes(const armi_sparse_index* index, int n_queries
  * term-at-a-time rescoring of the shard by helper workgroups: exact either way). score = sum
  * over shared indices, ascending index order, of fl32(q*d) accumulated in fp32 (mul and add
  * rounded separately). Only rows that share at least one index with the query are results.
- * Ranking (score desc, ordinal asc). */
+ * Ranking (score desc, ordinal asc).
+ * When every value of the index is >= 0 and k <= 128, a pass of at most 512 distinct terms is
+ * first answered by the MFMA filter (upper bounds of every row's score from u8 levels on the
+ * matrix cores, exact rescore of the best candidates from the CSR rows, certificate): such
+ * queries get ARMI_FLAG_CERTIFIED | ARMI_FLAG_FILTERED; the exact scan answers the rest. The
+ * results are the same either way. */
 int armi_sparse_topk(const armi_sparse_index* index, const int32_t* q_indptr,
                      const int32_t* q_indices, const float* q_values, int n_queries, int k,
                      const uint64_t* row_mask, float* out_scores, int64_t* out_ids,
                      int32_t* out_count, uint32_t* out_flags, void* workspace,
                      size_t workspace_bytes, hipStream_t stream);
+
+/* Enables (1) or disables (0) the MFMA filter of armi_sparse_topk on this index (default on:
+ * the exact scan alone when off); usable (host, nullable) = 1 when the index can use the filter
+ * (every value >= 0), else 0. No search may be in flight on the index. */
+int armi_sparse_index_set_filter(armi_sparse_index* index, int enable, int* usable);
 
 /* Query-term exchange of the sharded hybrid step (retrieval/shards.py; no reference
  * counterpart, the reference queries one Qdrant replica). _pack: CSR -> fixed slots (count
