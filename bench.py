@@ -439,7 +439,7 @@ def main() -> None:
         step(i)
     barrier()
     _armi.call("armi_scan_timing_enable", 1)
-    for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN):
+    for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN, _armi.TIMING_SPARSE_STAGE):
         _armi.call("armi_kernel_timing_read", slot, _armi.ctypes.byref(_armi.ctypes.c_double()),
                    _armi.ctypes.byref(_armi.ctypes.c_int64()))
     barrier()
@@ -624,34 +624,50 @@ def main() -> None:
         }
         result["rerank_share_of_step"] = (rr_ms * 1e-3) / elapsed
     if sindex is not None and world == 1:
-        # sparse scan roofline: algorithmic bytes of a 64-query pass = sum over the pass's
-        # distinct terms of what the scan must read for them: 8 B (row int32 + value fp32) per
-        # posting, or 4 B per row for a term in >= 1/8 of the rows (the index's dense columns)
+        # sparse roofline of the dominant sparse kernel. With the MFMA filter (every query of a
+        # pass answered by it: ARMI_FLAG_FILTERED) that is sparse_filter_scan_kernel, whose
+        # algorithmic bytes per 64-query pass are the u8 levels of the pass's dense-column terms
+        # (1 B per row and term, df >= rows/8) + 8 B (row int32 + value fp32) per posting of its
+        # other terms; the exact scan reads 4 B per row of a dense-column term instead.
         sp_ms, sp_n = _armi.ctypes.c_double(), _armi.ctypes.c_int64()
         _armi.call("armi_kernel_timing_read", _armi.TIMING_SPARSE_SCAN, _armi.ctypes.byref(sp_ms),
                    _armi.ctypes.byref(sp_n))
+        st_ms, st_n = _armi.ctypes.c_double(), _armi.ctypes.c_int64()
+        _armi.call("armi_kernel_timing_read", _armi.TIMING_SPARSE_STAGE, _armi.ctypes.byref(st_ms),
+                   _armi.ctypes.byref(st_n))
+        fl = torch.cat([sindex.topk(*qs, pre_k, workspace=sws).flags for qs in q_sparse])
+        filtered = float(((fl & _armi.ARMI_FLAG_FILTERED) != 0).float().mean())
         post = torch.bincount(csr[1].long(), minlength=VOCAB)
+        col_bytes = 1 if filtered == 1.0 else 4
+
         def term_bytes(df: torch.Tensor) -> float:
             dense = df * 8 >= n
-            return float(torch.where(dense, torch.full_like(df, 4 * n), 8 * df).sum())
+            return float(torch.where(dense, torch.full_like(df, col_bytes * n), 8 * df).sum())
 
         pass_bytes = [term_bytes(post[torch.unique(qs[1].long())]) for qs in q_sparse]
         alg = sum(pass_bytes[i % n_q_batches] for i in range(args.steps)) / max(args.steps, 1)
+        sp_kernel = "sparse_filter_scan_kernel" if filtered == 1.0 else "sparse_scan_kernel<false>"
         if sp_n.value:
             sp_avg = sp_ms.value / sp_n.value
-            sp_traffic, sp_src = read_traffic(f"sparse_scan_{args.corpus}_n{n}_q{batch}",
-                                              "sparse_scan_kernel<false>")
+            sp_traffic, sp_src = read_traffic(f"sparse_scan_{args.corpus}_n{n}_q{batch}", sp_kernel)
             result["roofline_sparse"] = {
-                "bound": "hbm", "kernel": "sparse_scan_kernel<false>", "achieved": alg / (sp_avg * 1e-3) / 1e9,
+                "bound": "hbm", "kernel": sp_kernel, "achieved": alg / (sp_avg * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": alg / (sp_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": sp_traffic,
                 "traffic_source": sp_src,
                 "traffic_over_algorithmic": sp_traffic / alg if sp_traffic else None,
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": sp_avg,
                 "launches_timed": sp_n.value,
-                "note": "algorithmic bytes = sum over the distinct terms of the 64-query pass of "
-                        "8 B per posting (4 B per row for dense-column terms, df >= rows/8); the "
-                        "kernel is instruction/latency-bound (DESIGN §3)"}
+                "note": ("algorithmic bytes = sum over the distinct terms of the 64-query pass of "
+                         f"{col_bytes} B per row for a dense-column term (df >= rows/8) and 8 B "
+                         "per posting of the others")}
+        if st_n.value:
+            result["sparse_stage"] = {
+                "avg_call_ms": st_ms.value / st_n.value, "calls_timed": st_n.value,
+                "filtered_frac": filtered,
+                "note": "one armi_sparse_topk call of 64 queries (pass_terms, filter prep / scan / "
+                        "merge, the exact scan's early exit and its merge / collect launches), "
+                        "HIP events around the call on its stream"}
     if scan_timing_note:
         result["scan_timing"] = scan_timing_note
     result["cpu_baseline"] = None
