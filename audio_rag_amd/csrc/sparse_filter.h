@@ -48,18 +48,18 @@ constexpr int kFMaxU = kFMaxSeg * kFK;         // distinct terms of a filtered p
 constexpr int kFImgStride = kFT * 2 + 64;      // bytes per term row of the image (+64: the
                                                // transposed reads of a half-wave hit 64 banks)
 constexpr int kFImgBytes = kFK * kFImgStride;
-constexpr int kFBRow = 48;                     // LDS bytes per query of a B slice (32 + 16 pad)
-constexpr int kFBBytes = kQB * kFBRow;
-constexpr int kFBSlice = kQB * kFK;            // halves per B slice in the workspace [q][16]
+constexpr int kFBBytes = kQB * kFK * 2;        // one B slice [q][16] fp16 (2 KB), in the
+constexpr int kFBSlice = kQB * kFK;            // workspace and, for every step, in LDS
 constexpr int kFList = 3;                      // lane list depth
 constexpr int kFLanes = 2 * kFWaves;           // lane lists per query and workgroup
 constexpr int kFPool = kFLanes * kFList;       // their entries (48)
-constexpr size_t kFLds = (size_t)2 * kFImgBytes + 2 * kFBBytes + 256;
+constexpr size_t kFLds = (size_t)2 * kFImgBytes + (size_t)kFMaxSeg * kFBBytes + 256;
 constexpr int kFSel = 1024;                    // rescored candidates per query, at most
 constexpr int kFVal = 8192;                    // (row, term) value slots of one rescore chunk
 constexpr int kFMaxK = 128;
 constexpr int32_t kFNone = (int32_t)0x80000000;  // held-term cursor of "no term"
 static_assert(kQB * kFPool * 8 + kQB * kFLanes * 4 <= 2 * kFImgBytes, "merge overlays the images");
+static_assert(2 * kFImgBytes + kFMaxSeg * kFBBytes + 256 <= 160 * 1024, "LDS of the filter scan");
 static_assert(kFMaxSeg * 2 <= 64, "one lane per held term");
 
 __host__ __device__ inline int filter_segments(int n_u) {
@@ -74,6 +74,16 @@ typedef short fs4 __attribute__((ext_vector_type(4)));
 typedef uint32_t fu32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t fu32x2 __attribute__((ext_vector_type(2)));
 typedef int32_t fp4 __attribute__((ext_vector_type(4), aligned(8)));
+
+// A posting window loaded and waited for inside one asm block: the rare continuation loads of
+// a tile that holds more than 128 postings of a term. As a plain load the compiler's wait-count
+// pass cannot tell whether it ran, and waited vmcnt(0) for it at the top of every step, i.e. for
+// the whole prefetch ring (the scan then ran one memory round trip per step).
+__device__ __forceinline__ fp4 load_window_sync(const int2* p) {
+  fp4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
 
 // Quantisation level of a value: the least integer a with a * s >= v (a in [0, 255] since
 // 255 s >= the term's largest value; 0 for v = 0 or -0.0). The fixup makes the bound exact
@@ -254,8 +264,15 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   const int n_tiles = hi > lo ? (int)((hi - lo + kFT - 1) / kFT) : 0;
   const int S = n_tiles * nSeg;
   const float scale = *fscale;
-  unsigned char* const bimg = fsm + 2 * kFImgBytes;                  // [2][kQB][kFBRow]
-  unsigned char* const trash = fsm + 2 * kFImgBytes + 2 * kFBBytes;  // scatter sink
+  // the pass's B slices, all of them for the whole scan: [seg][q][16] fp16, the two 16-B halves
+  // of query q's row swapped when q & 8 (conflict-free 16-lane ds_read_b128 groups)
+  unsigned char* const bimg = fsm + 2 * kFImgBytes;
+  unsigned char* const trash = bimg + (size_t)kFMaxSeg * kFBBytes;  // scatter sink
+  for (int i = threadIdx.x; i < nSeg * (kFBBytes / 16); i += kFThreads) {
+    const int q = (i >> 1) & (kQB - 1), h = i & 1;
+    *reinterpret_cast<uint4*>(bimg + (i >> 1) * 32 + 16 * (h ^ ((q >> 3) & 1))) =
+        reinterpret_cast<const uint4*>(fB)[i];
+  }
 
   int2 creg = make_int2(kFNone, 0);
   float sreg = 0.f;
@@ -271,11 +288,10 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   }
   const int rev2 = 2 * (63 - lane);
   fp4 ring[kFDepth][2];
-  uint32_t ringb[kFDepth];
   auto tile_hi = [&](int tile) { return (int32_t)min(lo + (int64_t)(tile + 1) * kFT, hi); };
-  // step s's loads into ring slot `slot`: every lane issues the same three loads per step
-  // (steps past the end and absent terms read a fixed in-bounds address), so the waits the
-  // compiler counts stay exact
+  // step s's loads into ring slot `slot`: every lane issues the same two loads per step (steps
+  // past the end and absent terms read a fixed in-bounds address), so the waits the compiler
+  // counts stay exact
   auto issue = [&](int s, int slot) {
     const bool live = s < S;
     const int tile = live ? s / nSeg : 0;
@@ -295,12 +311,14 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
       }
       ring[slot][j] = *src;
     }
-    ringb[slot] = reinterpret_cast<const uint32_t*>(fB)[(size_t)seg * (kFBSlice / 2) + 64 * wave + lane];
   };
   // step s from ring slot `slot` into LDS buffer par: the held terms' rows of the image (u8
   // levels as fp16; a posting term's row cleared and its in-tile postings scattered; an absent
-  // term's row zero) and the wave's 256 B of the B slice
+  // term's row zero)
   auto finish = [&](int s, int slot, int par) {
+    // the slot's loads are waited for here, once, on every path (a use inside the branches
+    // below made the compiler's wait counts conservative: a whole step drained per step)
+    asm volatile("" ::"v"(ring[slot][0]), "v"(ring[slot][1]));
     if (s >= S) return;  // uniform
     const int tile = s / nSeg, seg = s - tile * nSeg;
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kFT);
@@ -347,12 +365,9 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
           break;
         }
         adv += 128;
-        v = *reinterpret_cast<const fp4*>(post + cx + adv + rev2);
+        v = load_window_sync(post + cx + adv + rev2);
       }
     }
-    const int bi = 64 * wave + lane;  // dword of the slice: query bi / 8, dword bi % 8
-    *reinterpret_cast<uint32_t*>(bimg + par * kFBBytes + (bi >> 3) * kFBRow + 4 * (bi & 7)) =
-        ringb[slot];
   };
 
   ff32x16 acc[4][2];
@@ -365,12 +380,12 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   // supplies term row kb + q (+ 4 for the second read), data rows rb + 4 p .. + 3
   const int li = lane & 15;
   const int a_off = (8 * (lane >> 5) + (li >> 2)) * kFImgStride + 2 * (16 * ((lane >> 4) & 1) + 4 * (li & 3));
-  const int b_off = (lane & 31) * kFBRow + 16 * (lane >> 5);
-  auto compute = [&](int par) {
+  const int b_off = (lane & 31) * 32 + 16 * ((lane >> 5) ^ ((lane >> 3) & 1));
+  auto compute = [&](int par, int seg) {
     const unsigned char* img = fsm + par * kFImgBytes;
-    const unsigned char* bb = bimg + par * kFBBytes;
+    const unsigned char* bb = bimg + seg * kFBBytes;
     const fu32x4 b0 = *reinterpret_cast<const fu32x4*>(bb + b_off);
-    const fu32x4 b1 = *reinterpret_cast<const fu32x4*>(bb + 32 * kFBRow + b_off);
+    const fu32x4 b1 = *reinterpret_cast<const fu32x4*>(bb + 32 * 32 + b_off);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned char* p = img + a_off + 2 * 32 * (4 * wave + i);
@@ -442,18 +457,22 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   __syncthreads();
   // step s: issue s + 3 (ring slot (s + 3) % 4), multiply image s % 2, epilogue at a tile's last
   // step, stage s + 1 (slot (s + 1) % 4) into the other image, one barrier
+  // (the four steps of a round run whole, past S too: their loads are dummies, their products
+  // unused and their stores skipped, so every path issues the same loads in the same order and
+  // the compiler's wait counts stay exact)
   for (int s0 = 0; s0 < S; s0 += kFDepth) {
 #pragma unroll
     for (int d = 0; d < kFDepth; ++d) {
       const int s = s0 + d;
-      if (s < S) {  // uniform
-        issue(s + kFDepth - 1, (d + kFDepth - 1) % kFDepth);
-        compute(d & 1);
-        const int tile = s / nSeg;
-        if (s - tile * nSeg == nSeg - 1) epilogue(tile);
-        finish(s + 1, (d + 1) % kFDepth, (d + 1) & 1);
-        __syncthreads();
-      }
+      issue(s + kFDepth - 1, (d + kFDepth - 1) % kFDepth);
+      // keep the step's loads at the top: the scheduler otherwise sinks them below this step's
+      // waits, and only one step stays in flight
+      __builtin_amdgcn_sched_barrier(0);
+      const int tile = s / nSeg, seg = s - tile * nSeg;
+      compute(d & 1, seg);
+      if (s < S && seg == nSeg - 1) epilogue(tile);  // uniform
+      finish(s + 1, (d + 1) % kFDepth, (d + 1) & 1);
+      __syncthreads();
     }
   }
 

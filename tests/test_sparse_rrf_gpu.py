@@ -266,7 +266,8 @@ def test_sparse_collect_overflow_is_exact(gpu, oracle_mod):
         for m in (None, mask):
             got = _run(idx, q, k, gpu, mask=m)
             _same(got, oracle_mod.sparse_topk(*csr, *q, k, row_mask=m, ordinal_base=11))
-            assert not (got["flags"] & 4).any(), got["flags"]
+            # the pile and the -inf-threshold queries are never answered by the MFMA filter
+            assert not (got["flags"][:2] & 4).any(), got["flags"]
             # the pile query always needs the overflow path
             assert got["flags"][0] & 2, got["flags"]
             if m is None:
