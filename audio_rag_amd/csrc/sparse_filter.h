@@ -625,7 +625,10 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     if (kk[j] == kNegInf) continue;
     if (kk[j] >= t0) {
       const int s = atomicAdd(&sh[0], 1);
-      if (s < kFSel) srow[s] = rw[j];
+      if (s < kFSel) {
+        skey[s] = kk[j];
+        srow[s] = rw[j];
+      }
     } else {
       dmax = fmaxf(dmax, kk[j]);
     }
@@ -638,11 +641,25 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     tw[j] = qlist[slot * kQStride + j].w;
   }
   __syncthreads();
-  const int n_sel = sh[0];
-  if (n_sel > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
+  const int n_all = sh[0];
+  if (n_all > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
   float bound = red[0];
 #pragma unroll
   for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
+  // t0 is the kc-th largest LIST maximum, so more than kc entries reach it: only the kc best
+  // keys are rescored, the (kc + 1)-th key joins the bound of the rows left out
+  int n_sel = n_all;
+  if (n_all > kc) {
+    const int n2s = armi::pow2_at_least(n_all);
+    for (int e = n_all + tid; e < n2s; e += 256) {
+      skey[e] = kNegInf;
+      srow[e] = kEndRow;
+    }
+    armi::lds_sort_approx_desc(skey, srow, n2s);
+    bound = fmaxf(bound, skey[kc]);
+    n_sel = kc;
+    __syncthreads();  // (skey is rewritten with exact scores below)
+  }
 
   // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
   const int chunk = max(1, kFVal / nt);
@@ -684,10 +701,11 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       __syncthreads();
     }
     const int E = roff[nr];
-    for (int e0 = tid; e0 < E; e0 += 256 * 4) {
-      int ri[4], pos[4];
+    constexpr int kRU = 8;  // entries per thread and round: their loads in flight together
+    for (int e0 = tid; e0 < E; e0 += 256 * kRU) {
+      int ri[kRU], pos[kRU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kRU; ++u) {
         const int e = e0 + 256 * u;
         int a = 0, n = nr;  // last row whose entries start at or before e
         while (n > 1) {
@@ -698,15 +716,15 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
         ri[u] = a;
         pos[u] = e < E ? rst[a] + (e - roff[a]) : -1;
       }
-      int32_t ix[4];
-      float vx[4];
+      int32_t ix[kRU];
+      float vx[kRU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kRU; ++u) {
         ix[u] = pos[u] >= 0 ? row_idx[pos[u]] : -1;
         vx[u] = pos[u] >= 0 ? row_val[pos[u]] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kRU; ++u) {
         if (pos[u] < 0) continue;
         int a = 0, n = nt;  // first query term >= ix
         while (n > 0) {
