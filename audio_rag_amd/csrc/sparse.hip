@@ -217,6 +217,12 @@ struct alignas(8) QTerm {
   int32_t off;
 };
 
+// the MFMA filter's per-pass B slices, run at the end of a pass_terms block (sparse_filter.h)
+__device__ void filter_prep_block(const int32_t* uterm, const int32_t* n_terms, const QTerm* ql,
+                                  const int32_t* qu, const int32_t* qcount, const int32_t* qof,
+                                  const float* term_scale, uint16_t* fB, float* fscale,
+                                  int32_t* felig);
+
 // Wave 0 of a pass_terms block (tid = lane < 64): per-query term counts (first 256 terms;
 // flags[q] = 8 beyond), their exclusive offsets off[0..64], and the query -> slot deal: queries
 // sorted by term count (desc, then index) are dealt to the 16 waves in snake order, so each
@@ -269,7 +275,8 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    int32_t* __restrict__ coll_count) {
+    int32_t* __restrict__ coll_count, const float* __restrict__ term_scale,
+    uint16_t* __restrict__ fB, float* __restrict__ fscale, int32_t* __restrict__ felig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem);               // [kBmWords]
   int32_t* wpre = reinterpret_cast<int32_t*>(smem + kBmWords * 4);  // [kBmWords]
@@ -360,6 +367,10 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     if (lane < kBatch) ql[slot * kQStride + m + lane] = QTerm{0.f, 0};
     if (lane == 0) qcount[slot] = m;
   }
+  if (fB) {  // uniform: the MFMA filter runs on this pass
+    __syncthreads();
+    filter_prep_block(uterm, n_terms, ql, qu, qcount, qof, term_scale, fB, fscale, felig);
+  }
 }
 
 // One block for the pass. Sorts the pass's (term, query) pairs by (term, slot) where query q sits
@@ -372,7 +383,8 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    int32_t* __restrict__ coll_count) {
+    int32_t* __restrict__ coll_count, const float* __restrict__ term_scale,
+    uint16_t* __restrict__ fB, float* __restrict__ fscale, int32_t* __restrict__ felig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
   float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
@@ -516,6 +528,10 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     if (lane < kBatch) ql[(wave * kQW + i) * kQStride + run[i] + lane] = QTerm{0.f, 0};
   if (lane < kQW)
     qcount[wave * kQW + lane] = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
+  if (fB) {  // uniform: the MFMA filter runs on this pass
+    __syncthreads();
+    filter_prep_block(uterm, n_terms, ql, qu, qcount, qof, term_scale, fB, fscale, felig);
+  }
 }
 
 // ------------------------------------------------------------------------- scan
@@ -1813,20 +1829,18 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       ARMI_HIP(hipMemsetAsync(out_ids + (size_t)q0 * k, 0xff, sizeof(int64_t) * nqp * k, stream));
       continue;
     }
+    // (with the filter on, the pass_terms block also writes the filter's B slices)
+    uint16_t* fB = filter ? w.fB : nullptr;
     if (idx->vocab <= kBitmapVocab)
       pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, w.coll_count);
+          w.qcount, w.qof, pflags, w.coll_count, idx->term_scale, fB, w.fscale, w.felig);
     else
       pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, w.coll_count);
+          w.qcount, w.qof, pflags, w.coll_count, idx->term_scale, fB, w.fscale, w.felig);
     ARMI_LAUNCHED("pass_terms_kernel");
     if (filter) {
-      sparse_filter_prep_kernel<<<dim3(1), dim3(1024), 0, stream>>>(
-          w.uterm, w.n_terms, w.ql, w.qu, w.qcount, w.qof, idx->term_scale, 1, w.fB, w.fscale,
-          w.felig);
-      ARMI_LAUNCHED("sparse_filter_prep_kernel");
       armi::TimedLaunch tf;
       if (tf.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
       sparse_filter_scan_kernel<<<dim3(idx->n_ranges), dim3(kFThreads), kFLds, stream>>>(

@@ -162,15 +162,18 @@ __global__ void dense_u8_fill_kernel(const int32_t* __restrict__ dense_of,
 
 // ---------------------------------------------------------------------------- per pass
 
-// One block: the pass's B slices fB[seg][q][16] (fp16 bits), scale_up, and per query whether
-// the filter may answer it (felig). A query is eligible when the index allows the filter, the
-// pass has at most 512 distinct terms and every weight of the query is finite and >= 0.
-__global__ __launch_bounds__(1024) void sparse_filter_prep_kernel(
-    const int32_t* __restrict__ uterm, const int32_t* __restrict__ n_terms,
-    const QTerm* __restrict__ ql, const int32_t* __restrict__ qu,
-    const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
-    const float* __restrict__ term_scale, int filter_ok, uint16_t* __restrict__ fB,
-    float* __restrict__ fscale, int32_t* __restrict__ felig) {
+// The tail of the pass_terms block (1024 threads, after its lists are written and a barrier):
+// the pass's B slices fB[seg][q][16] (fp16 bits), scale_up, and per query whether the filter
+// may answer it (felig). A query is eligible when the pass has at most 512 distinct terms and
+// every weight of the query is finite and >= 0.
+__device__ void filter_prep_block(const int32_t* __restrict__ uterm,
+                                  const int32_t* __restrict__ n_terms,
+                                  const QTerm* __restrict__ ql, const int32_t* __restrict__ qu,
+                                  const int32_t* __restrict__ qcount,
+                                  const int32_t* __restrict__ qof,
+                                  const float* __restrict__ term_scale, uint16_t* __restrict__ fB,
+                                  float* __restrict__ fscale, int32_t* __restrict__ felig) {
+  const int filter_ok = 1;
   __shared__ double wmax[16];
   __shared__ int elig_s[kQB];
   __shared__ int e_s;
