@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--filter", choices=["on", "off"], default="on",
+                    help="armi_sparse_topk's MFMA filter (off: the exact scan alone)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     t0 = time.time()
@@ -27,6 +29,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.time()
     si = SparseIndex(indptr, idx, val, bench.VOCAB)
+    si.set_filter(a.filter == "on")
     torch.cuda.synchronize()
     t2 = time.time()
     print(f"corpus {a.rows} rows nnz {idx.numel()} gen {t1 - t0:.2f}s build {t2 - t1:.3f}s", flush=True)
@@ -44,7 +47,8 @@ def main():
     ms = ev0.elapsed_time(ev1) / a.iters
     fl = r.flags.cpu()
     print(f"batch {a.batch} k {a.k}: {ms:.3f} ms/batch, {a.batch / ms * 1e3:.0f} queries/s, "
-          f"certified {(fl & 1).bool().float().mean().item():.2f}", flush=True)
+          f"certified {(fl & 1).bool().float().mean().item():.2f} "
+          f"filtered {(fl & 4).bool().float().mean().item():.2f} (filter {a.filter})", flush=True)
 
 
 if __name__ == "__main__":
