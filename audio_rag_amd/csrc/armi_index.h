@@ -73,15 +73,17 @@ struct armi_sparse_index {
   int64_t dense_stride = 0;      // words per column (rows rounded up, + one tile of zeros)
   int32_t* dense_of = nullptr;   // [vocab] column of the term, -1
   uint32_t* dense_val = nullptr; // [n_dense][dense_stride]
-  // MFMA filter (round 6): every dense-column term also has a u8 column of quantisation levels
+  // MFMA filter (round 6): every term in >= 1/32 of the rows has a u8 column of quantisation levels
   // a = ceil(v / term_scale[t]) in [0, 255] (a * term_scale >= v exactly; 0 = no posting or a zero
   // value), so a pass streams 1 B per row and term and scores upper bounds on the matrix cores;
   // the candidates are rescored exactly from the caller's CSR rows.
   bool filter_ok = false;        // every value >= 0 (the bound needs non-negative products)
   bool filter_on = true;         // armi_sparse_index_set_filter
   float* term_scale = nullptr;   // [vocab] RU(max value of the term / 255), 0 for empty terms
+  int32_t n_col8 = 0;            // terms with a u8 column: df >= rows / 32
+  int32_t* col8_of = nullptr;    // [vocab] u8 column of the term, -1
   int64_t dense8_stride = 0;     // bytes per u8 column (rows rounded up to a filter tile, + one)
-  uint8_t* dense_u8 = nullptr;   // [n_dense][dense8_stride]
+  uint8_t* dense_u8 = nullptr;   // [n_col8][dense8_stride]
   const int64_t* row_ptr = nullptr;  // the caller's CSR (indptr [n_rows + 1], indices, values)
   const int32_t* row_idx = nullptr;
   const float* row_val = nullptr;

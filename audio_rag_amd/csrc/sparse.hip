@@ -1631,13 +1631,24 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->term_scale), std::max<size_t>(vocab, 1) * 4));
   term_scale_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(tmax, vocab, idx->term_scale);
   ARMI_LAUNCHED("term_scale_kernel");
+  col8_flag_kernel<<<grid_for((int64_t)vocab + 1, 256), 256, 0, stream>>>(idx->term_ptr, vocab,
+                                                                         idx->n_rows, dflag);
+  ARMI_LAUNCHED("col8_flag_kernel");
+  ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(dscan_tmp, dscan_bytes, dflag, dscan, vocab + 1, stream));
+  int32_t n_col8 = 0;
+  ARMI_HIP(hipMemcpyAsync(&n_col8, dscan + vocab, 4, hipMemcpyDeviceToHost, stream));
+  ARMI_HIP(hipStreamSynchronize(stream));
+  idx->n_col8 = n_col8;
+  ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->col8_of), std::max<size_t>(vocab, 1) * 4));
+  dense_of_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(dflag, dscan, vocab, idx->col8_of);
+  ARMI_LAUNCHED("dense_of_kernel");
   idx->dense8_stride = (idx->n_rows + kFT - 1) / kFT * kFT + kFT;  // + the last tile's over-read
-  const size_t u8_bytes = std::max<size_t>((size_t)n_dense * idx->dense8_stride, 16);
+  const size_t u8_bytes = std::max<size_t>((size_t)n_col8 * idx->dense8_stride, 16);
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->dense_u8), u8_bytes));
   ARMI_HIP(hipMemsetAsync(idx->dense_u8, 0, u8_bytes, stream));
-  if (nnz > 0 && n_dense > 0) {
+  if (nnz > 0 && n_col8 > 0) {
     dense_u8_fill_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(
-        idx->dense_of, reinterpret_cast<const int2*>(idx->post), skeys, nnz, vocab,
+        idx->col8_of, reinterpret_cast<const int2*>(idx->post), skeys, nnz, vocab,
         idx->term_scale, idx->dense8_stride, idx->dense_u8);
     ARMI_LAUNCHED("dense_u8_fill_kernel");
   }
@@ -1661,6 +1672,7 @@ void free_index(armi_sparse_index* idx) {
   (void)hipFree(idx->dense_val);
   (void)hipFree(idx->term_scale);
   (void)hipFree(idx->dense_u8);
+  (void)hipFree(idx->col8_of);
   delete idx;
 }
 
@@ -1845,7 +1857,7 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       if (tf.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
       sparse_filter_scan_kernel<<<dim3(idx->n_ranges), dim3(kFThreads), kFLds, stream>>>(
           idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab,
-          idx->n_rows, idx->range_rows, idx->n_ranges, row_mask, w.uterm, w.n_terms, idx->dense_of,
+          idx->n_rows, idx->range_rows, idx->n_ranges, row_mask, w.uterm, w.n_terms, idx->col8_of,
           idx->dense_u8, idx->dense8_stride, idx->term_scale, w.fB, w.fscale, w.cand_key,
           w.cand_row, w.cand_bound);
       ARMI_LAUNCHED("sparse_filter_scan_kernel");

@@ -10,10 +10,10 @@
 // UPPER BOUND of its score from the matrix cores, and only the best few rows per query are
 // scored exactly:
 //
-//   index build: every value v >= 0 of a term in >= 1/8 of the rows (a dense column) is stored as
+//   index build: every value v >= 0 of a term in >= 1/32 of the rows (a u8 column) is stored as
 //     the u8 level a = ceil(v / s_t), s_t = RU(max_t / 255), so a * s_t >= v exactly (1 B per row
 //     and term, half of the fp16 bytes and a quarter of the fp32 columns the exact scan reads);
-//     posting terms (df < rows / 8) get their levels from the same rule while they are staged.
+//     posting terms (df < rows / 32) get their levels from the same rule while they are staged.
 //   per pass (prep): B[u][q] = RU16(w_qu * s_u * 2^e) >= w * s * 2^e, one fp16 per (term, query),
 //     e chosen per pass to keep B well inside fp16's range (never subnormal: clamped to 2^-14).
 //   scan: rows in 1024-row tiles, the pass's terms in 16-term steps. Each step stages the u8
@@ -144,7 +144,22 @@ __global__ void term_scale_kernel(const uint32_t* __restrict__ tmax, int32_t voc
   scale[t] = m > 0.f ? s : 0.f;
 }
 
-// u8 level of every posting of a dense term into its column (sorted entry i: see dense_fill)
+// terms with a u8 column: df >= rows / kCol8Frac (a wider set than the exact scan's fp32
+// columns: a posting term then holds <= ~32 postings per 1024-row tile on average, so a tile
+// almost never needs a second 128-posting window, whose synchronous load stalls the workgroup)
+constexpr int kCol8Frac = 32;
+__global__ void col8_flag_kernel(const int32_t* __restrict__ term_ptr, int32_t vocab,
+                                 int64_t n_rows, int32_t* __restrict__ flag) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < vocab) {
+    const int64_t df = term_ptr[t + 1] - 1 - term_ptr[t];
+    flag[t] = (df > 0 && df * kCol8Frac >= n_rows) ? 1 : 0;
+  } else if (t == vocab) {
+    flag[t] = 0;
+  }
+}
+
+// u8 level of every posting of a u8-column term into its column (sorted entry i: see dense_fill)
 __global__ void dense_u8_fill_kernel(const int32_t* __restrict__ dense_of,
                                      const int2* __restrict__ post,
                                      const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
@@ -251,7 +266,7 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
     const int32_t* __restrict__ long_of, const int32_t* __restrict__ start_tab, int64_t n_rows,
     int64_t range_rows, int n_ranges, const uint64_t* __restrict__ row_mask,
     const int32_t* __restrict__ uterm, const int32_t* __restrict__ n_terms,
-    const int32_t* __restrict__ dense_of, const uint8_t* __restrict__ dense_u8, int64_t stride8,
+    const int32_t* __restrict__ col8_of, const uint8_t* __restrict__ dense_u8, int64_t stride8,
     const float* __restrict__ term_scale, const uint16_t* __restrict__ fB,
     const float* __restrict__ fscale, float* __restrict__ cand_key,
     int32_t* __restrict__ cand_row, float* __restrict__ cand_bound) {
@@ -283,7 +298,7 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
     const int sg = lane >> 1, u = sg * kFK + 2 * wave + (lane & 1);
     if (sg < nSeg && u < nU) {
       const int32_t t = uterm[u];
-      const int32_t d = dense_of[t];
+      const int32_t d = col8_of[t];
       sreg = term_scale[t];
       creg = d >= 0 ? make_int2(-(d + 1), 0)
                     : range_cursor(t, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
@@ -521,11 +536,18 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   }
 }
 
-// Per query of the pass: the kc best keys' rows (and every pool entry tied with the kc-th list
-// maximum) rescored exactly from the caller's CSR, sorted (score desc, row asc); certified when
-// the k-th exact score exceeds the bound of every row left out. Certified queries are answered
-// and flagged (CERTIFIED | FILTERED) with kth = +inf, so the exact scan and its collect pass
-// skip them; the others are left to the exact scan.
+// Per query of the pass, in up to two rounds. Round 1: the kc best keys of the pool (the entries
+// from the kc-th largest list maximum up, ranked by key) are rescored exactly from the caller's
+// CSR rows and ranked (score desc, row asc); certified when the k-th exact score exceeds the bound
+// of every row left out (the lists' bounds, the pool keys below the threshold, the (kc+1)-th key).
+// Round 2 (when round 1 cannot certify): every pool entry whose key reaches round 1's k-th exact
+// score, rescored and ranked again: a row outside it has key < that score <= the true k-th, so
+// only the lists' bounds and the pool keys below it remain. (Round 2 certifies the queries whose
+// scores crowd the top, e.g. two terms present in every row: ~100 rows within the keys' slack of
+// the 40th score.) Certified queries are answered and flagged (CERTIFIED | FILTERED) with
+// kth = +inf, so the exact scan and its collect pass skip them; the others are left to it.
+// Rankings are rank counts (each entry counts the entries better than it: LDS broadcast reads,
+// no barrier per stage) instead of bitonic sorts.
 __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
     const float* __restrict__ cand_bound, int n_wg, int q_first, int k, int kc,
@@ -536,12 +558,13 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     const float* __restrict__ row_val, float* __restrict__ out_scores,
     int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags,
     float* __restrict__ kth_out) {
-  __shared__ float skey[kFSel];
+  __shared__ float skey[kFSel];    // selected entries: key, then the exact score
   __shared__ int32_t srow[kFSel];
-  __shared__ float vals[kFVal];
-  __shared__ int32_t rst[kFSel];
-  __shared__ int32_t rln[kFSel];
-  __shared__ int32_t roff[kFSel + 1];
+  __shared__ float tkey[kFSel];    // ranked copies
+  __shared__ int32_t trow[kFSel];
+  __shared__ float vals[kFVal];    // (row, query term) values of a rescore chunk
+  __shared__ int32_t rst[kFSel];   // a chunk's rows: first CSR entry
+  __shared__ int32_t roff[kFSel + 1];  // ... and the exclusive prefix of their lengths
   __shared__ int32_t tterm[kMaxTerms];
   __shared__ float tw[kMaxTerms];
   __shared__ uint32_t umax[256];
@@ -553,20 +576,16 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   const int qg = q_first + ql;
   const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
   if (!felig[ql]) return;  // uniform: the exact scan answers
-  if (tid == 0) {
-    sh[0] = 0;
-    sh[2] = 0;
-  }
   if (tid < kQB && qof[tid] == ql) sh[1] = tid;
   __syncthreads();
   const int slot = sh[1];
   const int nt = qcount[slot];
-  auto answer = [&](int count) {  // skey / srow sorted, count valid entries
+  auto answer = [&](int count) {  // tkey / trow ranked, count valid entries
     if (wave != 0) return;
     for (int c = lane; c < k; c += 64) {
       const size_t o = (size_t)qg * k + c;
-      out_scores[o] = c < count ? skey[c] : kNegInf;
-      out_ids[o] = c < count ? ordinal_base + srow[c] : -1;
+      out_scores[o] = c < count ? tkey[c] : kNegInf;
+      out_ids[o] = c < count ? ordinal_base + trow[c] : -1;
     }
     if (lane == 0) {
       out_count[qg] = count;
@@ -598,7 +617,12 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) red[wave] = b;
+  for (int j = tid; j < nt; j += 256) {
+    tterm[j] = uterm[qu[slot * kQStride + j]];
+    tw[j] = qlist[slot * kQStride + j].w;
+  }
   __syncthreads();
+  const float list_bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (wave == 0) {  // t0 = kc-th largest list maximum (one-wave radix select)
     uint32_t u[4];
 #pragma unroll
@@ -620,71 +644,82 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     }
     if (lane == 0) t0s = t0;
   }
-  __syncthreads();
-  const float t0 = t0s;
-  float dmax = kNegInf;
-#pragma unroll
-  for (int j = 0; j < kSmPer; ++j) {
-    if (kk[j] == kNegInf) continue;
-    if (kk[j] >= t0) {
-      const int s = atomicAdd(&sh[0], 1);
-      if (s < kFSel) {
-        skey[s] = kk[j];
-        srow[s] = rw[j];
-      }
-    } else {
-      dmax = fmaxf(dmax, kk[j]);
+  // rank of entry i among n entries of (key, row) by (key desc, row asc)
+  auto rank_of = [&](const float* key, const int32_t* row, int n, int i) {
+    const float ki = key[i];
+    const int32_t ri = row[i];
+    int r = 0;
+    for (int j = 0; j < n; ++j) r += armi::approx_better(key[j], row[j], ki, ri) ? 1 : 0;
+    return r;
+  };
+  float thr = kNegInf;
+  for (int round = 0; round < 2; ++round) {
+    __syncthreads();  // (t0s written; the previous round is done with the arrays)
+    if (tid == 0) {
+      sh[0] = 0;
+      sh[2] = 0;
     }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
-  if (lane == 0) red[4 + wave] = dmax;
-  for (int j = tid; j < nt; j += 256) {
-    tterm[j] = uterm[qu[slot * kQStride + j]];
-    tw[j] = qlist[slot * kQStride + j].w;
-  }
-  __syncthreads();
-  const int n_all = sh[0];
-  if (n_all > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
-  float bound = red[0];
-#pragma unroll
-  for (int w = 1; w < 8; ++w) bound = fmaxf(bound, red[w]);
-  // t0 is the kc-th largest LIST maximum, so more than kc entries reach it: only the kc best
-  // keys are rescored, the (kc + 1)-th key joins the bound of the rows left out
-  int n_sel = n_all;
-  if (n_all > kc) {
-    const int n2s = armi::pow2_at_least(n_all);
-    for (int e = n_all + tid; e < n2s; e += 256) {
-      skey[e] = kNegInf;
-      srow[e] = kEndRow;
-    }
-    armi::lds_sort_approx_desc(skey, srow, n2s);
-    bound = fmaxf(bound, skey[kc]);
-    n_sel = kc;
-    __syncthreads();  // (skey is rewritten with exact scores below)
-  }
-
-  // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
-  const int chunk = max(1, kFVal / nt);
-  for (int c0 = 0; c0 < n_sel; c0 += chunk) {
-    const int nr = min(chunk, n_sel - c0);
-    for (int i = tid; i < nr * nt; i += 256) vals[i] = __uint_as_float(0xffffffffu);
-    for (int i = tid; i < nr; i += 256) {
-      const int32_t r = srow[c0 + i];
-      const int64_t a = row_ptr[r];
-      rst[i] = (int32_t)a;
-      rln[i] = (int32_t)(row_ptr[r + 1] - a);
-    }
+    if (round == 0) thr = t0s;
     __syncthreads();
-    {  // roff = exclusive prefix of rln (4 entries per thread)
-      int loc[4], tsum = 0;
+    float dmax = kNegInf;
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) {
+      if (kk[j] == kNegInf) continue;
+      if (kk[j] >= thr) {
+        const int s2 = atomicAdd(&sh[0], 1);
+        if (s2 < kFSel) {
+          skey[s2] = kk[j];
+          srow[s2] = rw[j];
+        }
+      } else {
+        dmax = fmaxf(dmax, kk[j]);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
+    if (lane == 0) red[4 + wave] = dmax;
+    __syncthreads();
+    const int n_all = sh[0];
+    if (n_all > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
+    float bound = fmaxf(list_bound, fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7])));
+    int n_sel = n_all;
+    if (round == 0 && n_all > kc) {
+      // the kc best keys only; the (kc+1)-th joins the bound of the rows left out
+      for (int i = tid; i < n_all; i += 256) {
+        const int r = rank_of(skey, srow, n_all, i);
+        if (r <= kc) {
+          tkey[r] = skey[i];
+          trow[r] = srow[i];
+        }
+      }
+      __syncthreads();
+      bound = fmaxf(bound, tkey[kc]);
+      for (int i = tid; i < kc; i += 256) {
+        skey[i] = tkey[i];
+        srow[i] = trow[i];
+      }
+      n_sel = kc;
+      __syncthreads();
+    }
+    // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
+    const int chunk = max(1, min(kFSel, kFVal / nt));
+    for (int c0 = 0; c0 < n_sel; c0 += chunk) {
+      const int nr = min(chunk, n_sel - c0);
+      for (int i = tid; i < nr * nt; i += 256) vals[i] = __uint_as_float(0xffffffffu);
+      int loc[4], tsum = 0;  // the lengths of rows 4 tid .. 4 tid + 3 of the chunk
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = 4 * tid + u;
-        loc[u] = i < nr ? rln[i] : 0;
+        loc[u] = 0;
+        if (i < nr) {
+          const int32_t r = srow[c0 + i];
+          const int64_t a = row_ptr[r];
+          rst[i] = (int32_t)a;
+          loc[u] = (int32_t)(row_ptr[r + 1] - a);
+        }
         tsum += loc[u];
       }
-      int x = tsum;
+      int x = tsum;  // roff = exclusive prefix of the lengths
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const int y = __shfl_up(x, d);
@@ -702,71 +737,79 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       }
       if (tid == 0) roff[nr] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
       __syncthreads();
-    }
-    const int E = roff[nr];
-    constexpr int kRU = 8;  // entries per thread and round: their loads in flight together
-    for (int e0 = tid; e0 < E; e0 += 256 * kRU) {
-      int ri[kRU], pos[kRU];
+      const int E = roff[nr];
+      constexpr int kRU = 8;  // entries per thread and round: their loads in flight together
+      for (int e0 = tid; e0 < E; e0 += 256 * kRU) {
+        int ri[kRU], pos[kRU];
 #pragma unroll
-      for (int u = 0; u < kRU; ++u) {
-        const int e = e0 + 256 * u;
-        int a = 0, n = nr;  // last row whose entries start at or before e
-        while (n > 1) {
-          const int h = n >> 1;
-          if (roff[a + h] <= e) a += h;
-          n -= h;
+        for (int u = 0; u < kRU; ++u) {
+          const int e = e0 + 256 * u;
+          int a = 0, n = nr;  // last row whose entries start at or before e
+          while (n > 1) {
+            const int h = n >> 1;
+            if (roff[a + h] <= e) a += h;
+            n -= h;
+          }
+          ri[u] = a;
+          pos[u] = e < E ? rst[a] + (e - roff[a]) : -1;
         }
-        ri[u] = a;
-        pos[u] = e < E ? rst[a] + (e - roff[a]) : -1;
-      }
-      int32_t ix[kRU];
-      float vx[kRU];
+        int32_t ix[kRU];
+        float vx[kRU];
 #pragma unroll
-      for (int u = 0; u < kRU; ++u) {
-        ix[u] = pos[u] >= 0 ? row_idx[pos[u]] : -1;
-        vx[u] = pos[u] >= 0 ? row_val[pos[u]] : 0.f;
-      }
+        for (int u = 0; u < kRU; ++u) {
+          ix[u] = pos[u] >= 0 ? row_idx[pos[u]] : -1;
+          vx[u] = pos[u] >= 0 ? row_val[pos[u]] : 0.f;
+        }
 #pragma unroll
-      for (int u = 0; u < kRU; ++u) {
-        if (pos[u] < 0) continue;
-        int a = 0, n = nt;  // first query term >= ix
-        while (n > 0) {
-          const int h = n >> 1;
-          if (tterm[a + h] < ix[u]) {
-            a += h + 1;
-            n -= h + 1;
-          } else {
-            n = h;
+        for (int u = 0; u < kRU; ++u) {
+          if (pos[u] < 0) continue;
+          int a = 0, n = nt;  // first query term >= ix
+          while (n > 0) {
+            const int h = n >> 1;
+            if (tterm[a + h] < ix[u]) {
+              a += h + 1;
+              n -= h + 1;
+            } else {
+              n = h;
+            }
+          }
+          if (a < nt && tterm[a] == ix[u]) vals[ri[u] * nt + a] = vx[u];
+        }
+      }
+      __syncthreads();
+      for (int i = tid; i < nr; i += 256) {
+        float sc = 0.f;
+        bool hit = false;
+        for (int p = 0; p < nt; ++p) {
+          const float v = vals[i * nt + p];
+          if (__float_as_uint(v) != 0xffffffffu) {
+            sc = __fadd_rn(sc, __fmul_rn(tw[p], v));  // the reference's order and rounding
+            hit = true;
           }
         }
-        if (a < nt && tterm[a] == ix[u]) vals[ri[u] * nt + a] = vx[u];
+        skey[c0 + i] = hit ? sc : kNegInf;
+      }
+      __syncthreads();
+    }
+    // rank the exact scores (score desc, row asc); the best k go to tkey / trow
+    int mem = 0;
+    for (int i = tid; i < n_sel; i += 256) {
+      mem += skey[i] != kNegInf;
+      const int r = rank_of(skey, srow, n_sel, i);
+      if (r < k) {
+        tkey[r] = skey[i];
+        trow[r] = srow[i];
       }
     }
+    if (mem) atomicAdd(&sh[2], mem);
     __syncthreads();
-    for (int i = tid; i < nr; i += 256) {
-      float s = 0.f;
-      bool hit = false;
-      for (int p = 0; p < nt; ++p) {
-        const float v = vals[i * nt + p];
-        if (__float_as_uint(v) != 0xffffffffu) {
-          s = __fadd_rn(s, __fmul_rn(tw[p], v));  // the reference's order and rounding
-          hit = true;
-        }
-      }
-      skey[c0 + i] = hit ? s : kNegInf;
+    const int members = sh[2];
+    const bool certified = members >= k ? tkey[k - 1] > bound : bound == kNegInf;
+    if (certified) {
+      answer(min(members, k));
+      return;
     }
-    __syncthreads();
+    if (members < k) return;  // uniform: no k-th score to widen the rescore with
+    thr = tkey[k - 1];  // round 2: every pool row whose key reaches it
   }
-  const int n2 = armi::pow2_at_least(max(max(n_sel, k), 2));
-  for (int e = n_sel + tid; e < n2; e += 256) {
-    skey[e] = kNegInf;
-    srow[e] = kEndRow;
-  }
-  int mem = 0;
-  for (int e = tid; e < n_sel; e += 256) mem += skey[e] != kNegInf;
-  if (mem) atomicAdd(&sh[2], mem);
-  armi::lds_sort_approx_desc(skey, srow, n2);
-  const int members = sh[2];
-  const bool certified = members >= k ? skey[k - 1] > bound : bound == kNegInf;
-  if (certified) answer(min(members, k));
 }
