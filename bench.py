@@ -638,10 +638,12 @@ def main() -> None:
         fl = torch.cat([sindex.topk(*qs, pre_k, workspace=sws).flags for qs in q_sparse])
         filtered = float(((fl & _armi.ARMI_FLAG_FILTERED) != 0).float().mean())
         post = torch.bincount(csr[1].long(), minlength=VOCAB)
-        col_bytes = 1 if filtered == 1.0 else 4
+        # the filter's u8 columns: terms in >= 1/32 of the rows; the exact scan's fp32 columns:
+        # terms in >= 1/8
+        col_bytes, col_frac = (1, 32) if filtered == 1.0 else (4, 8)
 
         def term_bytes(df: torch.Tensor) -> float:
-            dense = df * 8 >= n
+            dense = df * col_frac >= n
             return float(torch.where(dense, torch.full_like(df, col_bytes * n), 8 * df).sum())
 
         pass_bytes = [term_bytes(post[torch.unique(qs[1].long())]) for qs in q_sparse]
@@ -659,7 +661,7 @@ def main() -> None:
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": sp_avg,
                 "launches_timed": sp_n.value,
                 "note": ("algorithmic bytes = sum over the distinct terms of the 64-query pass of "
-                         f"{col_bytes} B per row for a dense-column term (df >= rows/8) and 8 B "
+                         f"{col_bytes} B per row for a column term (df >= rows/{col_frac}) and 8 B "
                          "per posting of the others")}
         if st_n.value:
             result["sparse_stage"] = {
