@@ -1867,6 +1867,41 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
           w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->row_ptr, idx->row_idx, idx->row_val,
           out_scores, out_ids, out_count, pflags, w.kth);
       ARMI_LAUNCHED("sparse_filter_merge_kernel");
+#ifdef ARMI_SPARSE_PROFILE
+      if (dbg & 8) {
+        std::vector<unsigned long long> hs((size_t)kMaxRanges * kFWaves * 8), hm((size_t)kQB * 8);
+        ARMI_HIP(hipStreamSynchronize(stream));
+        ARMI_HIP(hipMemcpyFromSymbol(hs.data(), HIP_SYMBOL(g_fscan_prof), hs.size() * 8));
+        ARMI_HIP(hipMemcpyFromSymbol(hm.data(), HIP_SYMBOL(g_fmerge_prof), hm.size() * 8));
+        double sum[6] = {0}, mx[6] = {0};
+        int cnt = 0;
+        for (size_t wv = 0; wv < (size_t)idx->n_ranges * kFWaves; ++wv) {
+          ++cnt;
+          for (int i = 0; i < 6; ++i) {
+            sum[i] += (double)hs[wv * 8 + i];
+            mx[i] = std::max(mx[i], (double)hs[wv * 8 + i]);
+          }
+        }
+        fprintf(stderr, "filter scan (us) avg/max per wave: issue %.1f/%.1f compute %.1f/%.1f epilogue "
+                "%.1f/%.1f finish %.1f/%.1f barrier %.1f/%.1f prologue %.1f/%.1f steps %llu\n",
+                sum[0] / cnt / 100, mx[0] / 100, sum[1] / cnt / 100, mx[1] / 100, sum[2] / cnt / 100,
+                mx[2] / 100, sum[3] / cnt / 100, mx[3] / 100, sum[4] / cnt / 100, mx[4] / 100,
+                sum[5] / cnt / 100, mx[5] / 100, hs[6]);
+        double ms[8] = {0};
+        int r1 = 0, r2 = 0, fail = 0;
+        for (int q = 0; q < nqp; ++q) {
+          for (int i = 1; i < 8; ++i) ms[i] += (double)hm[q * 8 + i];
+          const long long rr = (long long)hm[q * 8];
+          r1 += rr == 1;
+          r2 += rr == 2;
+          fail += rr < 0;
+        }
+        fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f rescore "
+                "%.1f round1 %.1f round2 %.1f end %.1f; rounds 1/2/failed %d/%d/%d\n",
+                ms[1] / nqp / 100, ms[2] / nqp / 100, ms[3] / nqp / 100, ms[4] / nqp / 100,
+                ms[5] / nqp / 100, ms[7] / nqp / 100, r1, r2, fail);
+      }
+#endif
     }
     // the exact scan: every query when the filter is off, else only the queries it left
     // (the kernel exits at once when it answered all of them)

@@ -62,6 +62,17 @@ static_assert(kQB * kFPool * 8 + kQB * kFLanes * 4 <= 2 * kFImgBytes, "merge ove
 static_assert(2 * kFImgBytes + kFMaxSeg * kFBBytes + 256 <= 160 * 1024, "LDS of the filter scan");
 static_assert(kFMaxSeg * 2 <= 64, "one lane per held term");
 
+#ifdef ARMI_SPARSE_PROFILE
+// Profiling build only (ARMI_BUILD_FLAGS=-DARMI_SPARSE_PROFILE, ARMI_SPARSE_DBG=8): 100 MHz stamps
+// per scan wave (issue, compute, epilogue, finish, barrier, prologue, steps) and per merge query
+// (phase ends: pool, selection, rescore, rank, rounds)
+__device__ unsigned long long g_fscan_prof[kMaxRanges * kFWaves * 8];
+__device__ unsigned long long g_fmerge_prof[kQB * 8];
+#define ARMI_FP_T(x) x = wall_clock64()
+#else
+#define ARMI_FP_T(x) (void)0
+#endif
+
 __host__ __device__ inline int filter_segments(int n_u) {
   const int s = (n_u + kFK - 1) / kFK;
   return s > kFDepth - 1 ? s : kFDepth - 1;  // a term's next tile issues after its last finish
@@ -468,11 +479,24 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
     }
   };
 
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, ta = 0, tb = 0;
+  (void)tp;
+  (void)ta;
+  (void)tb;
+  ARMI_FP_T(ta);
   // prologue: the first kFDepth - 1 steps in flight, step 0 staged
 #pragma unroll
   for (int p = 0; p < kFDepth - 1; ++p) issue(p, p);
   finish(0, 0, 0);
   __syncthreads();
+#ifdef ARMI_SPARSE_PROFILE
+  ARMI_FP_T(tb);
+  tp[5] = tb - ta;
+#define ARMI_FP_ADD(i) ARMI_FP_T(tb); tp[i] += tb - ta; ta = tb
+#else
+#define ARMI_FP_ADD(i) (void)0
+#endif
+  ARMI_FP_T(ta);
   // step s: issue s + 3 (ring slot (s + 3) % 4), multiply image s % 2, epilogue at a tile's last
   // step, stage s + 1 (slot (s + 1) % 4) into the other image, one barrier
   // (the four steps of a round run whole, past S too: their loads are dummies, their products
@@ -486,14 +510,27 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
       // keep the step's loads at the top: the scheduler otherwise sinks them below this step's
       // waits, and only one step stays in flight
       __builtin_amdgcn_sched_barrier(0);
+      ARMI_FP_ADD(0);
       const int tile = s / nSeg, seg = s - tile * nSeg;
       compute(d & 1, seg);
+      ARMI_FP_ADD(1);
       if (s < S && seg == nSeg - 1) epilogue(tile);  // uniform
+      ARMI_FP_ADD(2);
       finish(s + 1, (d + 1) % kFDepth, (d + 1) & 1);
+      ARMI_FP_ADD(3);
       __syncthreads();
+      ARMI_FP_ADD(4);
     }
   }
 
+#ifdef ARMI_SPARSE_PROFILE
+  if (lane == 0) {
+    unsigned long long* pr = g_fscan_prof + ((size_t)g * kFWaves + wave) * 8;
+    for (int i = 0; i < 6; ++i) pr[i] = tp[i];
+    pr[6] = S;
+  }
+#endif
+#undef ARMI_FP_ADD
   // workgroup merge: per query the 48 lane-list entries and 16 dropped bounds through LDS (over
   // the images), then one wave per 8 queries keeps the best 16 and the bound of the rest
   float* mkey = reinterpret_cast<float*>(fsm);                        // [kQB][kFPool]
@@ -575,11 +612,25 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   const int ql = blockIdx.x;
   const int qg = q_first + ql;
   const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  (void)ts;
+  ARMI_FP_T(ts[0]);
   if (!felig[ql]) return;  // uniform: the exact scan answers
   if (tid < kQB && qof[tid] == ql) sh[1] = tid;
   __syncthreads();
   const int slot = sh[1];
   const int nt = qcount[slot];
+#ifdef ARMI_SPARSE_PROFILE
+  auto prof_out = [&](int rounds) {
+    if (tid == 0) {
+      ARMI_FP_T(ts[7]);
+      for (int i = 1; i < 8; ++i) g_fmerge_prof[ql * 8 + i] = ts[i] ? ts[i] - ts[0] : 0;
+      g_fmerge_prof[ql * 8] = rounds;
+    }
+  };
+#else
+  auto prof_out = [&](int) {};
+#endif
   auto answer = [&](int count) {  // tkey / trow ranked, count valid entries
     if (wave != 0) return;
     for (int c = lane; c < k; c += 64) {
@@ -622,6 +673,7 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     tw[j] = qlist[slot * kQStride + j].w;
   }
   __syncthreads();
+  ARMI_FP_T(ts[1]);
   const float list_bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (wave == 0) {  // t0 = kc-th largest list maximum (one-wave radix select)
     uint32_t u[4];
@@ -701,6 +753,7 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       n_sel = kc;
       __syncthreads();
     }
+    ARMI_FP_T(ts[2]);
     // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
     const int chunk = max(1, min(kFSel, kFVal / nt));
     for (int c0 = 0; c0 < n_sel; c0 += chunk) {
@@ -791,6 +844,7 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       }
       __syncthreads();
     }
+    ARMI_FP_T(ts[3]);
     // rank the exact scores (score desc, row asc); the best k go to tkey / trow
     int mem = 0;
     for (int i = tid; i < n_sel; i += 256) {
@@ -805,11 +859,16 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     __syncthreads();
     const int members = sh[2];
     const bool certified = members >= k ? tkey[k - 1] > bound : bound == kNegInf;
+    ARMI_FP_T(ts[4 + round]);
     if (certified) {
       answer(min(members, k));
+      prof_out(round + 1);
       return;
     }
-    if (members < k) return;  // uniform: no k-th score to widen the rescore with
+    if (members < k) {  // uniform: no k-th score to widen the rescore with
+      prof_out(-1);
+      return;
+    }
     thr = tkey[k - 1];  // round 2: every pool row whose key reaches it
   }
 }
