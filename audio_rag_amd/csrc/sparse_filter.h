@@ -453,29 +453,80 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
     }
     disc[h] = fmaxf(disc[h], x);
   };
-  // the tile's keys into the lane lists; accumulators cleared. Row of register v of block i:
-  // 32 (4 w + i) + 8 (v / 4) + 4 (lane / 32) + v % 4 (the 32x32 MFMA output layout)
+  // The tile's keys into the lane lists; accumulators cleared. Row of register v of block i:
+  // 32 (4 w + i) + 8 (v / 4) + 4 (lane / 32) + v % 4 (the 32x32 MFMA output layout).
+  // Per lane and query half, a compare-free network keeps the tile's four best raw accumulators
+  // (descending), each carrying its code 16 i + v in the low 6 mantissa bits (v_and_or): per
+  // score one max and three med3 (on the bit patterns), no row arithmetic and no selects (a 3-deep insertion with row
+  // selects cost ~17 VALU per score and was half the kernel's time: 64 M scores per pass). At the
+  // tile's end the best three enter the lane list with their rows, the fourth joins the dropped
+  // bound. A code lowers a key by < 2^-17 relative, so the keys leaving the tile are scaled by
+  // scale * (1 + 2^-16). A row that does not count (past the range, masked out) scores 0, and an
+  // entry whose value is 0 apart from its code never enters a list (its score is <= 0: it
+  // cannot be certified into a top-k, see the merge's bound).
+  const float scale_x = scale * (1.0f + 0x1p-16f);
   auto epilogue = [&](int tile) {
     const int32_t tlo = (int32_t)(lo + (int64_t)tile * kFT);
     const int32_t thi = tile_hi(tile);
+    const bool full = thi - tlo == kFT && !row_mask;  // uniform
+    // (as their bit patterns: every key is >= +0, so the unsigned order is the float order, and
+    // integer max / med3 need no canonicalising copies of bit-built floats)
+    uint32_t top[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) top[h][e] = 0u;
+    auto net = [&](int h, float xf, uint32_t code) {
+      const uint32_t x = (__float_as_uint(xf) & 0xffffffc0u) | code;
+      const uint32_t a = top[h][0], b = top[h][1], c = top[h][2], d = top[h][3];
+      top[h][0] = max(a, x);
+      top[h][1] = max(min(a, b), min(max(a, b), x));  // med3: v_med3_u32
+      top[h][2] = max(min(b, c), min(max(b, c), x));
+      top[h][3] = max(min(c, d), min(max(c, d), x));
+    };
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          net(0, acc[i][0][v], 16 * i + v);
+          net(1, acc[i][1][v], 16 * i + v);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t rb = tlo + 32 * (4 * wave + i);
+        uint32_t mb = 0xffffffffu;
+        if (row_mask) {
+          const uint64_t w64 = rb < thi ? row_mask[rb >> 6] : 0ull;
+          mb = (uint32_t)(w64 >> (rb & 32));
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int off = 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+          const bool ok = rb + off < thi && ((mb >> off) & 1u);
+          net(0, ok ? acc[i][0][v] : 0.f, 16 * i + v);
+          net(1, ok ? acc[i][1][v] : 0.f, 16 * i + v);
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int32_t rb = tlo + 32 * (4 * wave + i);
-      uint32_t mb = 0xffffffffu;
-      if (row_mask) {
-        const uint64_t w64 = rb < thi ? row_mask[rb >> 6] : 0ull;
-        mb = (uint32_t)(w64 >> (rb & 32));
-      }
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int off = 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
-        const int32_t r = rb + off;
-        const bool ok = r < thi && ((mb >> off) & 1u);
-        insert(0, ok ? acc[i][0][v] * scale : kNegInf, r);
-        insert(1, ok ? acc[i][1][v] * scale : kNegInf, r);
-      }
       acc[i][0] = ff32x16{};
       acc[i][1] = ff32x16{};
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const uint32_t bits = top[h][e];
+        const uint32_t code = bits & 63u;
+        const int32_t r = tlo + 32 * (4 * wave + (int)(code >> 4)) + 8 * (int)((code >> 2) & 3) +
+                          4 * (lane >> 5) + (int)(code & 3);
+        insert(h, (bits & ~63u) ? __uint_as_float(bits) * scale_x : kNegInf, r);
+      }
+      const uint32_t b4 = top[h][3];
+      disc[h] = fmaxf(disc[h], (b4 & ~63u) ? __uint_as_float(b4) * scale_x : kNegInf);
     }
   };
 
