@@ -1896,10 +1896,10 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
           r2 += rr == 2;
           fail += rr < 0;
         }
-        fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f rescore "
-                "%.1f round1 %.1f round2 %.1f end %.1f; rounds 1/2/failed %d/%d/%d\n",
-                ms[1] / nqp / 100, ms[2] / nqp / 100, ms[3] / nqp / 100, ms[4] / nqp / 100,
-                ms[5] / nqp / 100, ms[7] / nqp / 100, r1, r2, fail);
+        fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f offsets "
+                "%.1f rescore %.1f round1 %.1f round2 %.1f end %.1f; rounds 1/2/failed %d/%d/%d\n",
+                ms[1] / nqp / 100, ms[2] / nqp / 100, ms[6] / nqp / 100, ms[3] / nqp / 100,
+                ms[4] / nqp / 100, ms[5] / nqp / 100, ms[7] / nqp / 100, r1, r2, fail);
       }
 #endif
     }

@@ -842,6 +842,9 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       if (tid == 0) roff[nr] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
       __syncthreads();
       const int E = roff[nr];
+#ifdef ARMI_SPARSE_PROFILE
+      if (round == 0 && c0 == 0) ARMI_FP_T(ts[6]);
+#endif
       // thread t walks entries [t per, (t + 1) per) of the chunk's rows in order: one binary
       // search for its first row, then the row advances at each boundary it passes; the loads of
       // kRU entries are issued before any is used (a search per entry and 8 loads per round made
