@@ -810,19 +810,23 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     for (int c0 = 0; c0 < n_sel; c0 += chunk) {
       const int nr = min(chunk, n_sel - c0);
       for (int i = tid; i < nr * nt; i += 256) vals[i] = __uint_as_float(0xffffffffu);
+      // each row's CSR extent: one row per thread (as a 4-rows-per-thread loop the compiler
+      // issued the four rows' loads one after the other)
+      for (int i = tid; i < nr; i += 256) {
+        const int32_t r = srow[c0 + i];
+        const int64_t a = row_ptr[r], b2 = row_ptr[r + 1];
+        rst[i] = (int32_t)a;
+        roff[i] = (int32_t)(b2 - a);  // (the length, until the prefix below)
+      }
+      __syncthreads();
       int loc[4], tsum = 0;  // the lengths of rows 4 tid .. 4 tid + 3 of the chunk
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = 4 * tid + u;
-        loc[u] = 0;
-        if (i < nr) {
-          const int32_t r = srow[c0 + i];
-          const int64_t a = row_ptr[r];
-          rst[i] = (int32_t)a;
-          loc[u] = (int32_t)(row_ptr[r + 1] - a);
-        }
+        loc[u] = i < nr ? roff[i] : 0;
         tsum += loc[u];
       }
+      __syncthreads();  // (every length read before roff is overwritten with the prefix)
       int x = tsum;  // roff = exclusive prefix of the lengths
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
