@@ -57,6 +57,7 @@ constexpr size_t kFLds = (size_t)2 * kFImgBytes + (size_t)kFMaxSeg * kFBBytes + 
 constexpr int kFSel = 1024;                    // rescored candidates per query, at most
 constexpr int kFVal = 8192;                    // (row, term) value slots of one rescore chunk
 constexpr int kFMaxK = 128;
+constexpr int kFTermBits = 4096;               // the rescore's query-term filter (bits)
 constexpr int32_t kFNone = (int32_t)0x80000000;  // held-term cursor of "no term"
 static_assert(kQB * kFPool * 8 + kQB * kFLanes * 4 <= 2 * kFImgBytes, "merge overlays the images");
 static_assert(2 * kFImgBytes + kFMaxSeg * kFBBytes + 256 <= 160 * 1024, "LDS of the filter scan");
@@ -655,6 +656,7 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   __shared__ int32_t roff[kFSel + 1];  // ... and the exclusive prefix of their lengths
   __shared__ int32_t tterm[kMaxTerms];
   __shared__ float tw[kMaxTerms];
+  __shared__ uint32_t tbits[kFTermBits / 32];  // bit (t mod kFTermBits) of every query term t
   __shared__ uint32_t umax[256];
   __shared__ float red[8];
   __shared__ int32_t wsum[4];
@@ -719,9 +721,13 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) red[wave] = b;
+  for (int j = tid; j < kFTermBits / 32; j += 256) tbits[j] = 0u;
+  __syncthreads();
   for (int j = tid; j < nt; j += 256) {
-    tterm[j] = uterm[qu[slot * kQStride + j]];
+    const int32_t t = uterm[qu[slot * kQStride + j]];
+    tterm[j] = t;
     tw[j] = qlist[slot * kQStride + j].w;
+    atomicOr(&tbits[(t >> 5) & (kFTermBits / 32 - 1)], 1u << (t & 31));
   }
   __syncthreads();
   ARMI_FP_T(ts[1]);
@@ -888,6 +894,9 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
 #pragma unroll
         for (int u = 0; u < kRU; ++u) {
           if (pos[u] < 0) continue;
+          // one LDS read rejects the row's other terms (~96 per row, ~12 shared at most); a
+          // binary search of the query's terms per entry was a chain of dependent LDS reads
+          if (!((tbits[(ix[u] >> 5) & (kFTermBits / 32 - 1)] >> (ix[u] & 31)) & 1u)) continue;
           int a = 0, n = nt;  // first query term >= ix
           while (n > 0) {
             const int h = n >> 1;
