@@ -1865,7 +1865,8 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       sparse_filter_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
           w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, kc, idx->ordinal_base,
           w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->row_ptr, idx->row_idx, idx->row_val,
-          out_scores, out_ids, out_count, pflags, w.kth);
+          idx->dense_of, idx->dense_val, idx->dense_stride, out_scores, out_ids, out_count, pflags,
+          w.kth);
       ARMI_LAUNCHED("sparse_filter_merge_kernel");
 #ifdef ARMI_SPARSE_PROFILE
       if (dbg & 8) {

@@ -644,7 +644,8 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     const QTerm* __restrict__ qlist, const int32_t* __restrict__ qu,
     const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ row_idx,
-    const float* __restrict__ row_val, float* __restrict__ out_scores,
+    const float* __restrict__ row_val, const int32_t* __restrict__ dense_of,
+    const uint32_t* __restrict__ dense_val, int64_t dense_stride, float* __restrict__ out_scores,
     int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags,
     float* __restrict__ kth_out) {
   __shared__ float skey[kFSel];    // selected entries: key, then the exact score
@@ -656,7 +657,8 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   __shared__ int32_t roff[kFSel + 1];  // ... and the exclusive prefix of their lengths
   __shared__ int32_t tterm[kMaxTerms];
   __shared__ float tw[kMaxTerms];
-  __shared__ uint32_t tbits[kFTermBits / 32];  // bit (t mod kFTermBits) of every query term t
+  __shared__ int32_t tcol[kMaxTerms];  // the term's exact fp32 column (dense_of), or -1
+  __shared__ uint32_t tbits[kFTermBits / 32];  // bit (t mod kFTermBits) of the other terms
   __shared__ uint32_t umax[256];
   __shared__ float red[8];
   __shared__ int32_t wsum[4];
@@ -722,14 +724,21 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) red[wave] = b;
   for (int j = tid; j < kFTermBits / 32; j += 256) tbits[j] = 0u;
+  if (tid == 0) sh[3] = 0;
   __syncthreads();
   for (int j = tid; j < nt; j += 256) {
     const int32_t t = uterm[qu[slot * kQStride + j]];
     tterm[j] = t;
     tw[j] = qlist[slot * kQStride + j].w;
-    atomicOr(&tbits[(t >> 5) & (kFTermBits / 32 - 1)], 1u << (t & 31));
+    const int32_t d = dense_of[t];
+    tcol[j] = d;
+    if (d < 0) {
+      atomicOr(&tbits[(t >> 5) & (kFTermBits / 32 - 1)], 1u << (t & 31));
+      atomicAdd(&sh[3], 1);
+    }
   }
   __syncthreads();
+  const bool rare = sh[3] > 0;  // terms without an fp32 column: their values come from the CSR
   ARMI_FP_T(ts[1]);
   const float list_bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (wave == 0) {  // t0 = kc-th largest list maximum (one-wave radix select)
@@ -815,7 +824,20 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     const int chunk = max(1, min(kFSel, kFVal / nt));
     for (int c0 = 0; c0 < n_sel; c0 += chunk) {
       const int nr = min(chunk, n_sel - c0);
-      for (int i = tid; i < nr * nt; i += 256) vals[i] = __uint_as_float(0xffffffffu);
+      // a term in >= 1/8 of the rows: its value from the exact scan's fp32 column (value bits,
+      // 0 = no posting), one independent load per (row, term) (rows of a few 4-MB columns:
+      // reading the same values from the rows' CSR entries took ~29 us of the merge's 47);
+      // sentinel (NaN bits) = no value yet
+      for (int f = tid; f < nr * nt; f += 256) {
+        const int i = f / nt, j = f - i * nt;
+        const int32_t d = tcol[j];
+        uint32_t bits = 0u;
+        if (d >= 0) bits = dense_val[(size_t)d * dense_stride + srow[c0 + i]];
+        vals[f] = __uint_as_float(bits ? bits : 0xffffffffu);
+      }
+      if (!rare) {  // uniform: every term had a column
+        __syncthreads();
+      } else {
       // each row's CSR extent: one row per thread (as a 4-rows-per-thread loop the compiler
       // issued the four rows' loads one after the other)
       for (int i = tid; i < nr; i += 256) {
@@ -907,10 +929,11 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
               n = h;
             }
           }
-          if (a < nt && tterm[a] == ix[u]) vals[ri[u] * nt + a] = vx[u];
+          if (a < nt && tterm[a] == ix[u] && tcol[a] < 0) vals[ri[u] * nt + a] = vx[u];
         }
       }
       __syncthreads();
+      }  // rare
       for (int i = tid; i < nr; i += 256) {
         float sc = 0.f;
         bool hit = false;
