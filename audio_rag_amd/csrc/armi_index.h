@@ -45,8 +45,8 @@ __host__ __device__ inline int64_t ord_to_img(int64_t i, int64_t T, int64_t perm
 }
 }  // namespace armi
 
-// Sparse store: a device inverted index built at create time from the caller's CSR (which must
-// outlive the index, include/armi.h: the MFMA filter's exact rescore reads its rows). Term t's postings (row, value) sit in [term_ptr[t], term_ptr[t+1]),
+// Sparse store: a device inverted index built at create time from the caller's CSR. Term t's
+// postings (row, value) sit in [term_ptr[t], term_ptr[t+1]),
 // ascending by row, the last slot a sentinel row (INT32_MAX); 64 sentinel slots pad the end.
 // The rows are split into n_ranges contiguous ranges of range_rows rows (a multiple of 64), one
 // scan workgroup each; terms with >= 256 postings carry start_tab[long_of[t]][range] = offset of
@@ -76,7 +76,7 @@ struct armi_sparse_index {
   // MFMA filter (round 6): every term in >= 1/32 of the rows has a u8 column of quantisation levels
   // a = ceil(v / term_scale[t]) in [0, 255] (a * term_scale >= v exactly; 0 = no posting or a zero
   // value), so a pass streams 1 B per row and term and scores upper bounds on the matrix cores;
-  // the candidates are rescored exactly from the caller's CSR rows.
+  // the candidates are rescored exactly from the fp32 columns and the postings.
   bool filter_ok = false;        // every value >= 0 (the bound needs non-negative products)
   bool filter_on = true;         // armi_sparse_index_set_filter
   float* term_scale = nullptr;   // [vocab] RU(max value of the term / 255), 0 for empty terms
@@ -84,9 +84,6 @@ struct armi_sparse_index {
   int32_t* col8_of = nullptr;    // [vocab] u8 column of the term, -1
   int64_t dense8_stride = 0;     // bytes per u8 column (rows rounded up to a filter tile, + one)
   uint8_t* dense_u8 = nullptr;   // [n_col8][dense8_stride]
-  const int64_t* row_ptr = nullptr;  // the caller's CSR (indptr [n_rows + 1], indices, values)
-  const int32_t* row_idx = nullptr;
-  const float* row_val = nullptr;
 };
 
 namespace armi {

@@ -1617,7 +1617,7 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
         skeys, nnz, vocab, idx->dense_stride, idx->dense_val);
     ARMI_LAUNCHED("dense_fill_kernel");
   }
-  // MFMA filter (sparse_filter.h): per-term scales, u8 columns of the dense terms, the CSR rows
+  // MFMA filter (sparse_filter.h): per-term scales, u8 columns of the terms in >= 1/32 of the rows
   uint32_t* tmax;
   unsigned long long* n_neg;
   ARMI_HIP(tmp.alloc(&tmax, (size_t)vocab + 1));
@@ -1657,9 +1657,6 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(hipStreamSynchronize(stream));
   idx->filter_ok = negatives == 0;
   idx->filter_on = true;
-  idx->row_ptr = indptr;
-  idx->row_idx = indices;
-  idx->row_val = values;
   return ARMI_OK;
 }
 
@@ -1864,9 +1861,10 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       if (int rc = tf.end()) return rc;
       sparse_filter_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
           w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, kc, idx->ordinal_base,
-          w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->row_ptr, idx->row_idx, idx->row_val,
-          idx->dense_of, idx->dense_val, idx->dense_stride, out_scores, out_ids, out_count, pflags,
-          w.kth);
+          w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->term_ptr,
+          reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->range_rows,
+          idx->n_ranges, idx->dense_of, idx->dense_val, idx->dense_stride, out_scores, out_ids,
+          out_count, pflags, w.kth);
       ARMI_LAUNCHED("sparse_filter_merge_kernel");
 #ifdef ARMI_SPARSE_PROFILE
       if (dbg & 8) {
@@ -1897,10 +1895,12 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
           r2 += rr == 2;
           fail += rr < 0;
         }
-        fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f offsets "
-                "%.1f rescore %.1f round1 %.1f round2 %.1f end %.1f; rounds 1/2/failed %d/%d/%d\n",
-                ms[1] / nqp / 100, ms[2] / nqp / 100, ms[6] / nqp / 100, ms[3] / nqp / 100,
-                ms[4] / nqp / 100, ms[5] / nqp / 100, ms[7] / nqp / 100, r1, r2, fail);
+        double mx7 = 0;
+        for (int q = 0; q < nqp; ++q) mx7 = std::max(mx7, (double)hm[q * 8 + 7]);
+        fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f rescore "
+                "%.1f round1 %.1f round2 %.1f end %.1f (max %.1f); rounds 1/2/failed %d/%d/%d\n",
+                ms[1] / nqp / 100, ms[2] / nqp / 100, ms[3] / nqp / 100, ms[4] / nqp / 100,
+                ms[5] / nqp / 100, ms[7] / nqp / 100, mx7 / 100, r1, r2, fail);
       }
 #endif
     }

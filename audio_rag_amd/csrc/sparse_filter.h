@@ -27,7 +27,8 @@
 //     Per lane x query a 3-deep list of (key, row) plus the largest key it dropped; per
 //     workgroup and query the best 16 entries and a bound on everything else.
 //   merge (per query): the pool's entries from the kc-th largest list maximum up are rescored
-//     exactly from the caller's CSR rows (the products of the shared terms, added in ascending
+//     exactly (the value of each query term in the row from the term's fp32 column, df >= rows/8,
+//     or its postings; the products of the shared terms added in ascending
 //     term order: the oracle's and the exact scan's arithmetic); the query is CERTIFIED when its
 //     k-th exact score exceeds every bound of a row not rescored (keys never under-state a
 //     score), and then answered. Queries that cannot be certified (ties at the boundary, fewer
@@ -57,7 +58,6 @@ constexpr size_t kFLds = (size_t)2 * kFImgBytes + (size_t)kFMaxSeg * kFBBytes + 
 constexpr int kFSel = 1024;                    // rescored candidates per query, at most
 constexpr int kFVal = 8192;                    // (row, term) value slots of one rescore chunk
 constexpr int kFMaxK = 128;
-constexpr int kFTermBits = 4096;               // the rescore's query-term filter (bits)
 constexpr int32_t kFNone = (int32_t)0x80000000;  // held-term cursor of "no term"
 static_assert(kQB * kFPool * 8 + kQB * kFLanes * 4 <= 2 * kFImgBytes, "merge overlays the images");
 static_assert(2 * kFImgBytes + kFMaxSeg * kFBBytes + 256 <= 160 * 1024, "LDS of the filter scan");
@@ -627,7 +627,8 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
 
 // Per query of the pass, in up to two rounds. Round 1: the kc best keys of the pool (the entries
 // from the kc-th largest list maximum up, ranked by key) are rescored exactly from the caller's
-// CSR rows and ranked (score desc, row asc); certified when the k-th exact score exceeds the bound
+// fp32 columns / postings and ranked (score desc, row asc); certified when the k-th exact score
+// exceeds the bound
 // of every row left out (the lists' bounds, the pool keys below the threshold, the (kc+1)-th key).
 // Round 2 (when round 1 cannot certify): every pool entry whose key reaches round 1's k-th exact
 // score, rescored and ranked again: a row outside it has key < that score <= the true k-th, so
@@ -643,8 +644,9 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     int64_t ordinal_base, const int32_t* __restrict__ felig, const int32_t* __restrict__ uterm,
     const QTerm* __restrict__ qlist, const int32_t* __restrict__ qu,
     const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ row_idx,
-    const float* __restrict__ row_val, const int32_t* __restrict__ dense_of,
+    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
+    const int32_t* __restrict__ long_of, const int32_t* __restrict__ start_tab,
+    int64_t range_rows, int n_ranges, const int32_t* __restrict__ dense_of,
     const uint32_t* __restrict__ dense_val, int64_t dense_stride, float* __restrict__ out_scores,
     int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags,
     float* __restrict__ kth_out) {
@@ -653,15 +655,11 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   __shared__ float tkey[kFSel];    // ranked copies
   __shared__ int32_t trow[kFSel];
   __shared__ float vals[kFVal];    // (row, query term) values of a rescore chunk
-  __shared__ int32_t rst[kFSel];   // a chunk's rows: first CSR entry
-  __shared__ int32_t roff[kFSel + 1];  // ... and the exclusive prefix of their lengths
   __shared__ int32_t tterm[kMaxTerms];
   __shared__ float tw[kMaxTerms];
   __shared__ int32_t tcol[kMaxTerms];  // the term's exact fp32 column (dense_of), or -1
-  __shared__ uint32_t tbits[kFTermBits / 32];  // bit (t mod kFTermBits) of the other terms
   __shared__ uint32_t umax[256];
   __shared__ float red[8];
-  __shared__ int32_t wsum[4];
   __shared__ float t0s;
   __shared__ int sh[4];  // [0] selected, [1] slot, [2] members
   const int ql = blockIdx.x;
@@ -723,7 +721,6 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b = fmaxf(b, armi::xor_stride(b, off));
   if (lane == 0) red[wave] = b;
-  for (int j = tid; j < kFTermBits / 32; j += 256) tbits[j] = 0u;
   if (tid == 0) sh[3] = 0;
   __syncthreads();
   for (int j = tid; j < nt; j += 256) {
@@ -732,13 +729,10 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     tw[j] = qlist[slot * kQStride + j].w;
     const int32_t d = dense_of[t];
     tcol[j] = d;
-    if (d < 0) {
-      atomicOr(&tbits[(t >> 5) & (kFTermBits / 32 - 1)], 1u << (t & 31));
-      atomicAdd(&sh[3], 1);
-    }
+    if (d < 0) atomicAdd(&sh[3], 1);
   }
   __syncthreads();
-  const bool rare = sh[3] > 0;  // terms without an fp32 column: their values come from the CSR
+  const bool rare = sh[3] > 0;  // terms without an fp32 column: values from their postings
   ARMI_FP_T(ts[1]);
   const float list_bound = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (wave == 0) {  // t0 = kc-th largest list maximum (one-wave radix select)
@@ -835,105 +829,41 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
         if (d >= 0) bits = dense_val[(size_t)d * dense_stride + srow[c0 + i]];
         vals[f] = __uint_as_float(bits ? bits : 0xffffffffu);
       }
-      if (!rare) {  // uniform: every term had a column
-        __syncthreads();
-      } else {
-      // each row's CSR extent: one row per thread (as a 4-rows-per-thread loop the compiler
-      // issued the four rows' loads one after the other)
-      for (int i = tid; i < nr; i += 256) {
-        const int32_t r = srow[c0 + i];
-        const int64_t a = row_ptr[r], b2 = row_ptr[r + 1];
-        rst[i] = (int32_t)a;
-        roff[i] = (int32_t)(b2 - a);  // (the length, until the prefix below)
-      }
-      __syncthreads();
-      int loc[4], tsum = 0;  // the lengths of rows 4 tid .. 4 tid + 3 of the chunk
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * tid + u;
-        loc[u] = i < nr ? roff[i] : 0;
-        tsum += loc[u];
-      }
-      __syncthreads();  // (every length read before roff is overwritten with the prefix)
-      int x = tsum;  // roff = exclusive prefix of the lengths
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-      }
-      if (lane == 63) wsum[wave] = x;
-      __syncthreads();
-      int before = x - tsum;
-      for (int w = 0; w < wave; ++w) before += wsum[w];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * tid + u;
-        if (i < nr) roff[i] = before;
-        before += loc[u];
-      }
-      if (tid == 0) roff[nr] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-      __syncthreads();
-      const int E = roff[nr];
-#ifdef ARMI_SPARSE_PROFILE
-      if (round == 0 && c0 == 0) ARMI_FP_T(ts[6]);
-#endif
-      // thread t walks entries [t per, (t + 1) per) of the chunk's rows in order: one binary
-      // search for its first row, then the row advances at each boundary it passes; the loads of
-      // kRU entries are issued before any is used (a search per entry and 8 loads per round made
-      // the rescore ~28 us of the merge's 46)
-      constexpr int kRU = 16;
-      const int per = (E + 255) / 256;
-      const int e_beg = min(E, tid * per), e_end = min(E, e_beg + per);
-      int ra = 0;
-      {
-        int n = nr;  // last row whose entries start at or before e_beg
-        while (n > 1) {
-          const int h = n >> 1;
-          if (roff[ra + h] <= e_beg) ra += h;
-          n -= h;
-        }
-      }
-      for (int e0 = e_beg; e0 < e_end; e0 += kRU) {
-        int ri[kRU], pos[kRU];
-#pragma unroll
-        for (int u = 0; u < kRU; ++u) {
-          const int e = e0 + u;
-          pos[u] = -1;
-          ri[u] = ra;
-          if (e < e_end) {
-            while (roff[ra + 1] <= e) ++ra;  // (skips empty rows; roff[nr] = E > e)
-            ri[u] = ra;
-            pos[u] = rst[ra] + (e - roff[ra]);
+      if (rare) {  // uniform: a term without a column (df < rows / 8)
+        // its value for each selected row from its postings (rows ascending): a binary search
+        // within the row's range (start_tab for a term of >= 256 postings, else the whole list
+        // of < 256), one (row, term) pair per thread; the searches stay inside a few small lists
+        // (the rows' CSR entries, scattered over the whole CSR, took ~29 us per query)
+        __syncthreads();  // (the column loads' vals writes before these)
+        for (int f = tid; f < nr * nt; f += 256) {
+          const int i = f / nt, j = f - i * nt;
+          if (tcol[j] >= 0) continue;
+          const int32_t r = srow[c0 + i];
+          const int32_t t = tterm[j];
+          const int32_t b0 = term_ptr[t];
+          const int32_t l = long_of[t];
+          int32_t a = b0, n = term_ptr[t + 1] - 1 - b0;  // (the sentinel excluded)
+          if (l >= 0) {
+            const int gq = (int)(r / range_rows);
+            a = b0 + start_tab[(size_t)l * n_ranges + gq];
+            const int32_t e = gq + 1 < n_ranges ? b0 + start_tab[(size_t)l * n_ranges + gq + 1]
+                                                : term_ptr[t + 1] - 1;
+            n = e - a;
           }
-        }
-        int32_t ix[kRU];
-        float vx[kRU];
-#pragma unroll
-        for (int u = 0; u < kRU; ++u) {
-          ix[u] = pos[u] >= 0 ? row_idx[pos[u]] : -1;
-          vx[u] = pos[u] >= 0 ? row_val[pos[u]] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < kRU; ++u) {
-          if (pos[u] < 0) continue;
-          // one LDS read rejects the row's other terms (~96 per row, ~12 shared at most); a
-          // binary search of the query's terms per entry was a chain of dependent LDS reads
-          if (!((tbits[(ix[u] >> 5) & (kFTermBits / 32 - 1)] >> (ix[u] & 31)) & 1u)) continue;
-          int a = 0, n = nt;  // first query term >= ix
-          while (n > 0) {
-            const int h = n >> 1;
-            if (tterm[a + h] < ix[u]) {
+          while (n > 0) {  // first posting with row >= r
+            const int32_t h = n >> 1;
+            if (post[a + h].x < r) {
               a += h + 1;
               n -= h + 1;
             } else {
               n = h;
             }
           }
-          if (a < nt && tterm[a] == ix[u] && tcol[a] < 0) vals[ri[u] * nt + a] = vx[u];
+          const int2 pv = post[a];
+          if (pv.x == r) vals[f] = __int_as_float(pv.y);  // (a zero value is stored as -0.0)
         }
       }
       __syncthreads();
-      }  // rare
       for (int i = tid; i < nr; i += 256) {
         float sc = 0.f;
         bool hit = false;

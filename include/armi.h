@@ -266,8 +266,7 @@ int armi_stream_loadgen(armi_stream* server, const uint16_t* queries, const int3
 typedef struct armi_sparse_index armi_sparse_index;
 
 /* CSR corpus: indptr [n_rows+1] int64, indices [nnz] int32 (strictly ascending per row),
- * values [nnz] float. Caller-owned, must outlive the index (the filter's exact rescore reads
- * the rows). */
+ * values [nnz] float. Caller-owned, must outlive the index. */
 int armi_sparse_index_create(int device, const int64_t* indptr, const int32_t* indices,
                              const float* values, int64_t n_rows, int64_t nnz, int32_t vocab,
                              int64_t ordinal_base, armi_sparse_index** out, hipStream_t stream);
@@ -285,7 +284,7 @@ size_t armi_sparse_workspace_bytes(const armi_sparse_index* index, int n_queries
  * Ranking (score desc, ordinal asc).
  * When every value of the index is >= 0 and k <= 128, a pass of at most 512 distinct terms is
  * first answered by the MFMA filter (upper bounds of every row's score from u8 levels on the
- * matrix cores, exact rescore of the best candidates from the CSR rows, certificate): such
+ * matrix cores, exact rescore of the best candidates, certificate): such
  * queries get ARMI_FLAG_CERTIFIED | ARMI_FLAG_FILTERED; the exact scan answers the rest. The
  * results are the same either way. */
 int armi_sparse_topk(const armi_sparse_index* index, const int32_t* q_indptr,
