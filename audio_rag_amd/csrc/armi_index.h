@@ -76,7 +76,7 @@ struct armi_sparse_index {
   // MFMA filter (round 6): every term in >= 1/32 of the rows has a u8 column of quantisation levels
   // a = ceil(v / term_scale[t]) in [0, 255] (a * term_scale >= v exactly; 0 = no posting or a zero
   // value), so a pass streams 1 B per row and term and scores upper bounds on the matrix cores;
-  // the candidates are rescored exactly from the fp32 columns and the postings.
+  // the candidates are rescored exactly from the fp32 columns and the rare-value tables.
   bool filter_ok = false;        // every value >= 0 (the bound needs non-negative products)
   bool filter_on = true;         // armi_sparse_index_set_filter
   float* term_scale = nullptr;   // [vocab] RU(max value of the term / 255), 0 for empty terms
@@ -84,6 +84,9 @@ struct armi_sparse_index {
   int32_t* col8_of = nullptr;    // [vocab] u8 column of the term, -1
   int64_t dense8_stride = 0;     // bytes per u8 column (rows rounded up to a filter tile, + one)
   uint8_t* dense_u8 = nullptr;   // [n_col8][dense8_stride]
+  int2* rare_of = nullptr;       // [vocab] rare-value table {first bucket, mask} or {-1, 0}
+  uint2* rare_tab = nullptr;     // the filter rescore's (row, value bits) tables, 8 per bucket
+  int64_t rare_slots = 0;
 };
 
 namespace armi {

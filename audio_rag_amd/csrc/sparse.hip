@@ -30,6 +30,7 @@
 //           >= the k-th candidate (a lower bound of the true k-th), then sorts them.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -217,11 +218,50 @@ struct alignas(8) QTerm {
   int32_t off;
 };
 
+// What a pass_terms block writes for the MFMA filter (sparse_filter.h); fB == nullptr: filter
+// off. Per query entry j of slot q's list, fs = the term's u8 scale; per query q (not slot), the
+// rescore's term table: fterm = {fp32 column (dense_of) or -1, rare-value table base, its mask,
+// the term}, fw = the weight, fnt = the count.
+struct FilterPrep {
+  const float* term_scale;
+  const int32_t* dense_of;
+  const int2* rare_of;
+  uint16_t* fB;     // the pass's B slices [kFMaxSeg][kQB][kFK] fp16
+  float* fscale;    // its key scale
+  int32_t* felig;   // [kQB] queries the filter may answer
+  float* fs;        // [kQB * kQStride] by slot
+  int4* fterm;      // [kQB * kMaxTerms] by query
+  float* fw;        // [kQB * kMaxTerms] by query
+  int32_t* fnt;     // [kQB] by query
+};
+
+// one list entry's filter record (t = its term, w its weight, slot q's entry idx of query qq);
+// returns the term's u8 scale
+__device__ __forceinline__ float filter_entry(const FilterPrep& fp, int slot, int idx, int qq,
+                                              int32_t t, float w) {
+  const float s = fp.term_scale[t];
+  fp.fs[slot * kQStride + idx] = s;
+  const int2 ro = fp.rare_of[t];
+  fp.fterm[qq * kMaxTerms + idx] = make_int4(fp.dense_of[t], ro.x, ro.y, t);
+  fp.fw[qq * kMaxTerms + idx] = w;
+  return s;
+}
+
+// a pass_terms wave's lists as the filter prep reads them: per slot i of the wave its query
+// (-1: none) and list length, and when the list is one 64-entry chunk (regs), entry j's u,
+// weight and scale in lane j
+struct PrepCapture {
+  int q[kQW];
+  int n[kQW];
+  bool regs[kQW];
+  int u[kQW];
+  float w[kQW];
+  float s[kQW];
+};
+
 // the MFMA filter's per-pass B slices, run at the end of a pass_terms block (sparse_filter.h)
-__device__ void filter_prep_block(const int32_t* uterm, const int32_t* n_terms, const QTerm* ql,
-                                  const int32_t* qu, const int32_t* qcount, const int32_t* qof,
-                                  const float* term_scale, uint16_t* fB, float* fscale,
-                                  int32_t* felig);
+__device__ __forceinline__ void filter_prep_block(int nU, const QTerm* ql, const int32_t* qu,
+                                                  const PrepCapture& cap, const FilterPrep& fp);
 
 // Wave 0 of a pass_terms block (tid = lane < 64): per-query term counts (first 256 terms;
 // flags[q] = 8 beyond), their exclusive offsets off[0..64], and the query -> slot deal: queries
@@ -275,8 +315,7 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    int32_t* __restrict__ coll_count, const float* __restrict__ term_scale,
-    uint16_t* __restrict__ fB, float* __restrict__ fscale, int32_t* __restrict__ felig) {
+    int32_t* __restrict__ coll_count, FilterPrep fp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem);               // [kBmWords]
   int32_t* wpre = reinterpret_cast<int32_t*>(smem + kBmWords * 4);  // [kBmWords]
@@ -341,35 +380,57 @@ __global__ __launch_bounds__(1024) void pass_terms_bitmap_kernel(
   }
   __syncthreads();
   // wave w writes the lists of slots 4 w + i
+  PrepCapture cap;
 #pragma unroll
   for (int i = 0; i < kQW; ++i) {
     const int slot = wave * kQW + i;
     const int q = qof[slot];
     int m = 0;
+    cap.u[i] = 0;
+    cap.w[i] = 0.f;
+    cap.s[i] = 0.f;
+    bool full = true;  // every term of the query valid (then entry j of the list = term j)
+    int n = 0;
     if (q >= 0) {
       const int32_t p0 = q_indptr[q];
-      const int n = off[q + 1] - off[q];
+      n = off[q + 1] - off[q];
       for (int c0 = 0; c0 < n; c0 += 64) {
         const int j = c0 + lane;
         const int32_t t = j < n ? q_indices[p0 + j] : -1;
         const bool ok = t >= 0 && t < vocab;
         const unsigned long long mb = __ballot(ok);
+        full &= __popcll(mb) == min(64, n - c0);
         if (ok) {
           const int idx = m + __popcll(mb & ((1ull << lane) - 1ull));
           const int32_t u = wpre[t >> 5] + __popc(bits[t >> 5] & ((1u << (t & 31)) - 1u));
-          ql[slot * kQStride + idx] = QTerm{q_values[p0 + j], (u % kU) * kTile * 4};
+          const float w = q_values[p0 + j];
+          ql[slot * kQStride + idx] = QTerm{w, (u % kU) * kTile * 4};
           qu[slot * kQStride + idx] = u;
+          if (fp.fB && idx < kMaxTerms) {
+            const float s = filter_entry(fp, slot, idx, q, t, w);
+            if (c0 == 0) {
+              cap.u[i] = u;
+              cap.w[i] = w;
+              cap.s[i] = s;
+            }
+          }
         }
         m += __popcll(mb);
       }
     }
+    cap.q[i] = q;
+    cap.n[i] = m;
+    cap.regs[i] = full && n <= 64;
     // a batch of the scan may read up to kBatch - 1 entries past a list: finite weights there
     if (lane < kBatch) ql[slot * kQStride + m + lane] = QTerm{0.f, 0};
     if (lane == 0) qcount[slot] = m;
+    if (fp.fB && lane == 0 && q >= 0) fp.fnt[q] = m;
   }
-  if (fB) {  // uniform: the MFMA filter runs on this pass
+  if (fp.fB) {  // uniform: the MFMA filter runs on this pass
     __syncthreads();
-    filter_prep_block(uterm, n_terms, ql, qu, qcount, qof, term_scale, fB, fscale, felig);
+    int nU = 0;
+    for (int v = 0; v < kScanThreads / 64; ++v) nU += wsum[v];
+    filter_prep_block(nU, ql, qu, cap, fp);
   }
 }
 
@@ -383,8 +444,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
     const float* __restrict__ q_values, int nq, int32_t vocab, int32_t* __restrict__ uterm,
     int32_t* __restrict__ n_terms, QTerm* __restrict__ ql, int32_t* __restrict__ qu,
     int32_t* __restrict__ qcount, int32_t* __restrict__ qof, uint32_t* __restrict__ flags,
-    int32_t* __restrict__ coll_count, const float* __restrict__ term_scale,
-    uint16_t* __restrict__ fB, float* __restrict__ fscale, int32_t* __restrict__ felig) {
+    int32_t* __restrict__ coll_count, FilterPrep fp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);           // [kMaxU]
   float* val = reinterpret_cast<float*>(smem + kMaxU * 4);     // [kMaxU]
@@ -518,6 +578,7 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
         const int32_t u = (int32_t)(k >> 6);
         ql[slot * kQStride + idx] = QTerm{val[e], (u % kU) * kTile * 4};
         qu[slot * kQStride + idx] = u;
+        if (fp.fB) filter_entry(fp, slot, idx, qof[slot], uterm[u], val[e]);
       }
       run[i] += __popcll(mb);
     }
@@ -526,11 +587,23 @@ __global__ __launch_bounds__(1024) void pass_terms_kernel(
 #pragma unroll
   for (int i = 0; i < kQW; ++i)
     if (lane < kBatch) ql[(wave * kQW + i) * kQStride + run[i] + lane] = QTerm{0.f, 0};
-  if (lane < kQW)
-    qcount[wave * kQW + lane] = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
-  if (fB) {  // uniform: the MFMA filter runs on this pass
+  if (lane < kQW) {
+    const int c = lane == 0 ? run[0] : lane == 1 ? run[1] : lane == 2 ? run[2] : run[3];
+    qcount[wave * kQW + lane] = c;
+    const int q = qof[wave * kQW + lane];
+    if (fp.fB && q >= 0) fp.fnt[q] = c;
+  }
+  if (fp.fB) {  // uniform: the MFMA filter runs on this pass (lists read back from memory)
     __syncthreads();
-    filter_prep_block(uterm, n_terms, ql, qu, qcount, qof, term_scale, fB, fscale, felig);
+    PrepCapture cap;
+#pragma unroll
+    for (int i = 0; i < kQW; ++i) {
+      const int slot = wave * kQW + i;
+      cap.q[i] = qof[slot];
+      cap.n[i] = run[i];
+      cap.regs[i] = false;
+    }
+    filter_prep_block(part[1023], ql, qu, cap, fp);
   }
 }
 
@@ -1466,6 +1539,10 @@ struct Workspace {
   uint16_t* fB;     // MFMA filter: the pass's B slices [kFMaxSeg][kQB][kFK] fp16
   float* fscale;    // its key scale
   int32_t* felig;   // [kQB] queries the filter may answer
+  float* fs;        // FilterPrep's per-entry tables
+  int4* fterm;
+  float* fw;
+  int32_t* fnt;
   size_t bytes;
 };
 
@@ -1490,6 +1567,10 @@ Workspace carve(void* base, const armi_sparse_index* idx) {
   w.fB = cv.take<uint16_t>((size_t)kFMaxSeg * kFBSlice);
   w.fscale = cv.take<float>(1);
   w.felig = cv.take<int32_t>(kQB);
+  w.fs = cv.take<float>((size_t)kQB * kQStride);
+  w.fterm = cv.take<int4>((size_t)kQB * kMaxTerms);
+  w.fw = cv.take<float>((size_t)kQB * kMaxTerms);
+  w.fnt = cv.take<int32_t>(kQB);
   w.bytes = cv.off + 256;
   return w;
 }
@@ -1617,6 +1698,47 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
         skeys, nnz, vocab, idx->dense_stride, idx->dense_val);
     ARMI_LAUNCHED("dense_fill_kernel");
   }
+  // the filter rescore's rare-value tables (sparse_filter.h): every posting of a term without an
+  // fp32 column; on an insert that finds both buckets full, again with twice the buckets
+  {
+    int32_t *nb, *nbscan, *fail;
+    ARMI_HIP(tmp.alloc(&nb, (size_t)vocab + 1));
+    ARMI_HIP(tmp.alloc(&nbscan, (size_t)vocab + 1));
+    ARMI_HIP(tmp.alloc(&fail, 1));
+    ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->rare_of), std::max<size_t>(vocab, 1) * 8));
+    for (int div = 4;; div /= 2) {
+      rare_buckets_kernel<<<grid_for((int64_t)vocab + 1, 256), 256, 0, stream>>>(
+          idx->term_ptr, idx->dense_of, vocab, div, nb);
+      ARMI_LAUNCHED("rare_buckets_kernel");
+      ARMI_HIP(hipcub::DeviceScan::ExclusiveSum(dscan_tmp, dscan_bytes, nb, nbscan, vocab + 1, stream));
+      int32_t n_buckets = 0;
+      ARMI_HIP(hipMemcpyAsync(&n_buckets, nbscan + vocab, 4, hipMemcpyDeviceToHost, stream));
+      ARMI_HIP(hipStreamSynchronize(stream));
+      rare_of_kernel<<<grid_for(vocab, 256), 256, 0, stream>>>(nb, nbscan, vocab, idx->rare_of);
+      ARMI_LAUNCHED("rare_of_kernel");
+      if (idx->rare_tab) ARMI_HIP(hipFree(idx->rare_tab));
+      idx->rare_tab = nullptr;
+      const size_t slots = std::max<size_t>((size_t)n_buckets * kRareSlots, 1);
+      ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->rare_tab), slots * 8));
+      ARMI_HIP(hipMemsetAsync(idx->rare_tab, 0xff, slots * 8, stream));
+      ARMI_HIP(hipMemsetAsync(fail, 0, 4, stream));
+      if (nnz > 0 && n_buckets > 0) {
+        int32_t* fill;
+        ARMI_HIP(tmp.alloc(&fill, (size_t)n_buckets));
+        ARMI_HIP(hipMemsetAsync(fill, 0, (size_t)n_buckets * 4, stream));
+        rare_insert_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(
+            idx->rare_of, reinterpret_cast<const int2*>(idx->post), skeys, nnz, vocab, fill,
+            idx->rare_tab, fail);
+        ARMI_LAUNCHED("rare_insert_kernel");
+      }
+      int32_t failed = 0;
+      ARMI_HIP(hipMemcpyAsync(&failed, fail, 4, hipMemcpyDeviceToHost, stream));
+      ARMI_HIP(hipStreamSynchronize(stream));
+      idx->rare_slots = (int64_t)slots;
+      if (failed == 0) break;
+      ARMI_REQUIRE(div > 1, "armi_sparse_index: rare-value tables overflow");
+    }
+  }
   // MFMA filter (sparse_filter.h): per-term scales, u8 columns of the terms in >= 1/32 of the rows
   uint32_t* tmax;
   unsigned long long* n_neg;
@@ -1670,6 +1792,8 @@ void free_index(armi_sparse_index* idx) {
   (void)hipFree(idx->term_scale);
   (void)hipFree(idx->dense_u8);
   (void)hipFree(idx->col8_of);
+  (void)hipFree(idx->rare_of);
+  (void)hipFree(idx->rare_tab);
   delete idx;
 }
 
@@ -1839,15 +1963,16 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       continue;
     }
     // (with the filter on, the pass_terms block also writes the filter's B slices)
-    uint16_t* fB = filter ? w.fB : nullptr;
+    const FilterPrep fp{idx->term_scale, idx->dense_of, idx->rare_of,
+                        filter ? w.fB : nullptr, w.fscale, w.felig, w.fs, w.fterm, w.fw, w.fnt};
     if (idx->vocab <= kBitmapVocab)
       pass_terms_bitmap_kernel<<<dim3(1), dim3(kScanThreads), kPrepBmLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, w.coll_count, idx->term_scale, fB, w.fscale, w.felig);
+          w.qcount, w.qof, pflags, w.coll_count, fp);
     else
       pass_terms_kernel<<<dim3(1), dim3(1024), kPrepLds, stream>>>(
           q_indptr + q0, q_indices, q_values, nqp, idx->vocab, w.uterm, w.n_terms, w.ql, w.qu,
-          w.qcount, w.qof, pflags, w.coll_count, idx->term_scale, fB, w.fscale, w.felig);
+          w.qcount, w.qof, pflags, w.coll_count, fp);
     ARMI_LAUNCHED("pass_terms_kernel");
     if (filter) {
       armi::TimedLaunch tf;
@@ -1861,14 +1986,12 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
       if (int rc = tf.end()) return rc;
       sparse_filter_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
           w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, kc, idx->ordinal_base,
-          w.felig, w.uterm, w.ql, w.qu, w.qcount, w.qof, idx->term_ptr,
-          reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab, idx->range_rows,
-          idx->n_ranges, idx->dense_of, idx->dense_val, idx->dense_stride, out_scores, out_ids,
-          out_count, pflags, w.kth);
+          w.felig, w.fterm, w.fw, w.fnt, idx->rare_tab, idx->dense_val, idx->dense_stride,
+          out_scores, out_ids, out_count, pflags, w.kth);
       ARMI_LAUNCHED("sparse_filter_merge_kernel");
 #ifdef ARMI_SPARSE_PROFILE
       if (dbg & 8) {
-        std::vector<unsigned long long> hs((size_t)kMaxRanges * kFWaves * 8), hm((size_t)kQB * 8);
+        std::vector<unsigned long long> hs((size_t)kMaxRanges * kFWaves * 8), hm((size_t)kQB * 16);
         ARMI_HIP(hipStreamSynchronize(stream));
         ARMI_HIP(hipMemcpyFromSymbol(hs.data(), HIP_SYMBOL(g_fscan_prof), hs.size() * 8));
         ARMI_HIP(hipMemcpyFromSymbol(hm.data(), HIP_SYMBOL(g_fmerge_prof), hm.size() * 8));
@@ -1889,14 +2012,27 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
         double ms[8] = {0};
         int r1 = 0, r2 = 0, fail = 0;
         for (int q = 0; q < nqp; ++q) {
-          for (int i = 1; i < 8; ++i) ms[i] += (double)hm[q * 8 + i];
-          const long long rr = (long long)hm[q * 8];
+          for (int i = 1; i < 8; ++i) ms[i] += (double)hm[q * 16 + i];
+          const long long rr = (long long)hm[q * 16];
           r1 += rr == 1;
           r2 += rr == 2;
           fail += rr < 0;
         }
         double mx7 = 0;
-        for (int q = 0; q < nqp; ++q) mx7 = std::max(mx7, (double)hm[q * 8 + 7]);
+        for (int q = 0; q < nqp; ++q) mx7 = std::max(mx7, (double)hm[q * 16 + 7]);
+        std::vector<int> order(nqp);
+        for (int q = 0; q < nqp; ++q) order[q] = q;
+        std::sort(order.begin(), order.end(),
+                  [&](int a, int b) { return hm[a * 16 + 7] > hm[b * 16 + 7]; });
+        for (int i = 0; i < std::min(nqp, 6); ++i) {
+          const unsigned long long* h = &hm[(size_t)order[i] * 16];
+          fprintf(stderr, "  slow query %d: setup %.1f select %.1f rare-start %.1f rescore %.1f rank "
+                  "%.1f end %.1f terms %llu rare %llu n_all %llu n_sel %llu\n", order[i],
+                  h[1] / 100.0, h[2] / 100.0, h[6] / 100.0, h[3] / 100.0, h[4] / 100.0,
+                  h[7] / 100.0, h[8], h[9], h[10], h[11]);
+          fprintf(stderr, "    radix %.1f selected %.1f ranked %.1f\n", h[12] / 100.0, h[13] / 100.0,
+                  h[14] / 100.0);
+        }
         fprintf(stderr, "filter merge (us, stamps from start) avg: setup %.1f select %.1f rescore "
                 "%.1f round1 %.1f round2 %.1f end %.1f (max %.1f); rounds 1/2/failed %d/%d/%d\n",
                 ms[1] / nqp / 100, ms[2] / nqp / 100, ms[3] / nqp / 100, ms[4] / nqp / 100,

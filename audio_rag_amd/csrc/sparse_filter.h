@@ -68,7 +68,7 @@ static_assert(kFMaxSeg * 2 <= 64, "one lane per held term");
 // per scan wave (issue, compute, epilogue, finish, barrier, prologue, steps) and per merge query
 // (phase ends: pool, selection, rescore, rank, rounds)
 __device__ unsigned long long g_fscan_prof[kMaxRanges * kFWaves * 8];
-__device__ unsigned long long g_fmerge_prof[kQB * 8];
+__device__ unsigned long long g_fmerge_prof[kQB * 16];
 #define ARMI_FP_T(x) x = wall_clock64()
 #else
 #define ARMI_FP_T(x) (void)0
@@ -187,83 +187,193 @@ __global__ void dense_u8_fill_kernel(const int32_t* __restrict__ dense_of,
   dense_u8[(size_t)d * stride + pv.x] = (uint8_t)u8_level(__int_as_float(pv.y), scale[t]);
 }
 
+// The rescore's values of the terms without an fp32 column (df < rows / 8): per term t an
+// open-addressed table of 2^m buckets of 8 (row, value bits) slots (64 B), a row in one of two
+// buckets (two-choice: the emptier at insert), so a lookup is two independent 64-B loads, whatever
+// the term's df (a search of its postings was a chain of ~10 dependent loads, ~25 us a query).
+// Empty slots hold row -1. rare_of[t] = {first bucket, 2^m - 1}, {-1, 0} for no table.
+constexpr int kRareSlots = 8;
+
+__host__ __device__ inline uint32_t rare_hash1(uint32_t row, uint32_t t) {
+  uint32_t h = row * 0x9E3779B1u ^ (t * 0x85EBCA77u + 0x165667B1u);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+
+__host__ __device__ inline uint32_t rare_hash2(uint32_t h1) {
+  uint32_t h = h1 ^ 0x68E31DA4u;
+  h *= 0xB5297A4Du;
+  h ^= h >> 13;
+  h *= 0x1B56C4E9u;
+  h ^= h >> 16;
+  return h;
+}
+
+// buckets of term t: the least power of two >= df / div (div = 4: 2-4 rows per bucket on average)
+__global__ void rare_buckets_kernel(const int32_t* __restrict__ term_ptr,
+                                    const int32_t* __restrict__ dense_of, int32_t vocab, int div,
+                                    int32_t* __restrict__ nb) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > vocab) return;
+  int32_t b = 0;
+  if (t < vocab && dense_of[t] < 0) {
+    const int64_t df = term_ptr[t + 1] - 1 - term_ptr[t];
+    if (df > 0) {
+      b = 1;
+      while ((int64_t)b * div < df) b <<= 1;
+    }
+  }
+  nb[t] = b;
+}
+
+__global__ void rare_of_kernel(const int32_t* __restrict__ nb, const int32_t* __restrict__ scan,
+                               int32_t vocab, int2* __restrict__ rare_of) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= vocab) return;
+  rare_of[t] = nb[t] > 0 ? make_int2(scan[t], nb[t] - 1) : make_int2(-1, 0);
+}
+
+// every posting of a table term into the emptier of its two buckets (sorted entry i: see
+// dense_fill); fail counts postings that found both full (the build retries with more buckets)
+__global__ void rare_insert_kernel(const int2* __restrict__ rare_of, const int2* __restrict__ post,
+                                   const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
+                                   int32_t* __restrict__ fill, uint2* __restrict__ tab,
+                                   int32_t* __restrict__ fail) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const uint32_t t = skeys[i];
+  if (t >= (uint32_t)vocab) return;
+  const int2 ro = rare_of[t];
+  if (ro.x < 0) return;
+  const int2 pv = post[i + t];
+  const uint32_t h1 = rare_hash1((uint32_t)pv.x, t);
+  int64_t b1 = ro.x + (int64_t)(h1 & (uint32_t)ro.y);
+  int64_t b2 = ro.x + (int64_t)(rare_hash2(h1) & (uint32_t)ro.y);
+  if (fill[b2] < fill[b1]) {
+    const int64_t x = b1;
+    b1 = b2;
+    b2 = x;
+  }
+  int64_t b = b1;
+  int s = atomicAdd(&fill[b1], 1);
+  if (s >= kRareSlots) {
+    b = b2;
+    s = atomicAdd(&fill[b2], 1);
+    if (s >= kRareSlots) {
+      atomicAdd(fail, 1);
+      return;
+    }
+  }
+  tab[b * kRareSlots + s] = make_uint2((uint32_t)pv.x, (uint32_t)pv.y);
+}
+
+// the value bits of row r in term table {base, mask} (t the term), 0 when r has no posting (a
+// zero value is stored as -0.0)
+__device__ __forceinline__ uint32_t rare_value(const uint2* __restrict__ tab, int32_t base,
+                                               int32_t mask, uint32_t t, int32_t r) {
+  const uint32_t h1 = rare_hash1((uint32_t)r, t);
+  const uint4* p1 = reinterpret_cast<const uint4*>(tab + (base + (int64_t)(h1 & (uint32_t)mask)) * kRareSlots);
+  const uint4* p2 = reinterpret_cast<const uint4*>(tab + (base + (int64_t)(rare_hash2(h1) & (uint32_t)mask)) * kRareSlots);
+  uint4 v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = p1[i];
+    v[4 + i] = p2[i];
+  }
+  uint32_t bits = 0u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    bits = v[i].x == (uint32_t)r ? v[i].y : bits;
+    bits = v[i].z == (uint32_t)r ? v[i].w : bits;
+  }
+  return bits;
+}
+
 // ---------------------------------------------------------------------------- per pass
 
 // The tail of the pass_terms block (1024 threads, after its lists are written and a barrier):
 // the pass's B slices fB[seg][q][16] (fp16 bits), scale_up, and per query whether the filter
 // may answer it (felig). A query is eligible when the pass has at most 512 distinct terms and
-// every weight of the query is finite and >= 0.
-__device__ void filter_prep_block(const int32_t* __restrict__ uterm,
-                                  const int32_t* __restrict__ n_terms,
-                                  const QTerm* __restrict__ ql, const int32_t* __restrict__ qu,
-                                  const int32_t* __restrict__ qcount,
-                                  const int32_t* __restrict__ qof,
-                                  const float* __restrict__ term_scale, uint16_t* __restrict__ fB,
-                                  float* __restrict__ fscale, int32_t* __restrict__ felig) {
-  const int filter_ok = 1;
+// every weight of the query is finite and >= 0. A slot whose list the pass_terms wave holds in
+// registers (cap.regs: <= 64 entries, entry j in lane j) is read from there, the others from the
+// lists in global memory; one barrier (the pass's largest w * s for the exponent e).
+__device__ __forceinline__ void filter_prep_block(int nU, const QTerm* __restrict__ ql,
+                                                  const int32_t* __restrict__ qu,
+                                                  const PrepCapture& cap, const FilterPrep& fp) {
+  uint16_t* __restrict__ fB = fp.fB;
+  const float* __restrict__ fs = fp.fs;
   __shared__ double wmax[16];
-  __shared__ int elig_s[kQB];
-  __shared__ int e_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
-  const int nU = *n_terms;
-  const bool pass_ok = filter_ok && nU <= kFMaxU;
+  const bool pass_ok = nU <= kFMaxU;
   const int nSeg = filter_segments(nU);
   if (pass_ok) {
     uint4* b4 = reinterpret_cast<uint4*>(fB);
     for (int i = tid; i < nSeg * kFBSlice / 8; i += 1024) b4[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   double mx = 0.0;
+  bool ok[kQW];
 #pragma unroll
   for (int i = 0; i < kQW; ++i) {
     const int slot = wave * kQW + i;
-    const int q = qof[slot];
-    const int n = q >= 0 ? qcount[slot] : 0;
+    const int q = cap.q[i];
+    const int n = q >= 0 ? cap.n[i] : 0;
     bool bad = false;
     double m = 0.0;
-    for (int j = lane; j < n; j += 64) {
-      const float w = ql[slot * kQStride + j].w;
-      const float s = term_scale[uterm[qu[slot * kQStride + j]]];
-      bad |= !(w >= 0.f) || !isfinite(w);  // NaN fails w >= 0
-      m = fmax(m, (double)w * (double)s);
+    if (cap.regs[i]) {  // uniform
+      if (lane < n) {
+        bad = !(cap.w[i] >= 0.f) || !isfinite(cap.w[i]);  // NaN fails w >= 0
+        m = (double)cap.w[i] * (double)cap.s[i];
+      }
+    } else {
+      for (int j = lane; j < n; j += 64) {
+        const float w = ql[slot * kQStride + j].w;
+        const float sc = fs[slot * kQStride + j];
+        bad |= !(w >= 0.f) || !isfinite(w);
+        m = fmax(m, (double)w * (double)sc);
+      }
     }
-    const bool ok = pass_ok && q >= 0 && __ballot(bad) == 0ull;
-    if (ok) mx = fmax(mx, m);
-    if (lane == 0 && q >= 0) elig_s[q] = ok ? 1 : 0;
+    ok[i] = pass_ok && q >= 0 && __ballot(bad) == 0ull;
+    if (ok[i]) mx = fmax(mx, m);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
   if (lane == 0) wmax[wave] = mx;
   __syncthreads();
+  double m = 0.0;
+  for (int w = 0; w < 16; ++w) m = fmax(m, wmax[w]);
+  int x = 0;
+  if (m > 0.0) (void)frexp(m, &x);  // m < 2^x
+  int e = 14 - x;                   // every B < 2^14
+  e = e < -100 ? -100 : (e > 110 ? 110 : e);
   if (tid == 0) {
-    double m = 0.0;
-    for (int w = 0; w < 16; ++w) m = fmax(m, wmax[w]);
-    int x = 0;
-    if (m > 0.0) (void)frexp(m, &x);  // m < 2^x
-    int e = 14 - x;                   // every B < 2^14
-    e = e < -100 ? -100 : (e > 110 ? 110 : e);
-    e_s = e;
     const double d = ldexp(1.0 + (double)(nU + 600) * 0x1p-22, -e);
     float f = (float)d;
     if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
-    *fscale = f;
+    *fp.fscale = f;
   }
-  __syncthreads();
-  if (tid < kQB) felig[tid] = 0;
-  __syncthreads();
-  const int e = e_s;
 #pragma unroll
   for (int i = 0; i < kQW; ++i) {
     const int slot = wave * kQW + i;
-    const int q = qof[slot];
-    if (q < 0 || !elig_s[q]) continue;  // wave-uniform
-    if (lane == 0) felig[q] = 1;
-    const int n = qcount[slot];
-    for (int j = lane; j < n; j += 64) {
-      const int u = qu[slot * kQStride + j];
-      const float w = ql[slot * kQStride + j].w;
-      const float s = term_scale[uterm[u]];
-      fB[(size_t)(u / kFK) * kFBSlice + q * kFK + (u % kFK)] =
-          ru_half(ldexp((double)w * (double)s, e));
+    const int q = cap.q[i];
+    if (q < 0) continue;  // wave-uniform
+    if (lane == 0) fp.felig[q] = ok[i] ? 1 : 0;
+    if (!ok[i]) continue;
+    const int n = cap.n[i];
+    if (cap.regs[i]) {
+      if (lane < n)
+        fB[(size_t)(cap.u[i] / kFK) * kFBSlice + q * kFK + (cap.u[i] % kFK)] =
+            ru_half(ldexp((double)cap.w[i] * (double)cap.s[i], e));
+    } else {
+      for (int j = lane; j < n; j += 64) {
+        const int u = qu[slot * kQStride + j];
+        const float w = ql[slot * kQStride + j].w;
+        const float sc = fs[slot * kQStride + j];
+        fB[(size_t)(u / kFK) * kFBSlice + q * kFK + (u % kFK)] = ru_half(ldexp((double)w * (double)sc, e));
+      }
     }
   }
 }
@@ -636,49 +746,51 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
 // scores crowd the top, e.g. two terms present in every row: ~100 rows within the keys' slack of
 // the 40th score.) Certified queries are answered and flagged (CERTIFIED | FILTERED) with
 // kth = +inf, so the exact scan and its collect pass skip them; the others are left to it.
-// Rankings are rank counts (each entry counts the entries better than it: LDS broadcast reads,
-// no barrier per stage) instead of bitonic sorts.
+// Rankings are rank counts (each entry counts the entries better than it, split over 2 or 4
+// threads when few: 16-B LDS reads, no barrier per stage) instead of bitonic sorts. The query's
+// terms come from the pass_terms block's per-query table (fterm / fw / fnt).
 __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     const float* __restrict__ cand_key, const int32_t* __restrict__ cand_row,
     const float* __restrict__ cand_bound, int n_wg, int q_first, int k, int kc,
-    int64_t ordinal_base, const int32_t* __restrict__ felig, const int32_t* __restrict__ uterm,
-    const QTerm* __restrict__ qlist, const int32_t* __restrict__ qu,
-    const int32_t* __restrict__ qcount, const int32_t* __restrict__ qof,
-    const int32_t* __restrict__ term_ptr, const int2* __restrict__ post,
-    const int32_t* __restrict__ long_of, const int32_t* __restrict__ start_tab,
-    int64_t range_rows, int n_ranges, const int32_t* __restrict__ dense_of,
+    int64_t ordinal_base, const int32_t* __restrict__ felig, const int4* __restrict__ fterm,
+    const float* __restrict__ fw, const int32_t* __restrict__ fnt,
+    const uint2* __restrict__ rare_tab,
     const uint32_t* __restrict__ dense_val, int64_t dense_stride, float* __restrict__ out_scores,
     int64_t* __restrict__ out_ids, int32_t* __restrict__ out_count, uint32_t* __restrict__ flags,
     float* __restrict__ kth_out) {
-  __shared__ float skey[kFSel];    // selected entries: key, then the exact score
-  __shared__ int32_t srow[kFSel];
-  __shared__ float tkey[kFSel];    // ranked copies
-  __shared__ int32_t trow[kFSel];
+  __shared__ __attribute__((aligned(16))) float skey[kFSel];  // selected: key, then exact score
+  __shared__ __attribute__((aligned(16))) int32_t srow[kFSel];
+  __shared__ __attribute__((aligned(16))) float tkey[kFSel];  // ranked copies
+  __shared__ __attribute__((aligned(16))) int32_t trow[kFSel];
   __shared__ float vals[kFVal];    // (row, query term) values of a rescore chunk
-  __shared__ int32_t tterm[kMaxTerms];
+  __shared__ int4 tinfo[kMaxTerms];  // {fp32 column or -1, table base, table mask, term}
   __shared__ float tw[kMaxTerms];
-  __shared__ int32_t tcol[kMaxTerms];  // the term's exact fp32 column (dense_of), or -1
   __shared__ uint32_t umax[256];
   __shared__ float red[8];
   __shared__ float t0s;
-  __shared__ int sh[4];  // [0] selected, [1] slot, [2] members
+  __shared__ int sh[4];  // [0] selected, [2] members, [3] terms without a column
   const int ql = blockIdx.x;
   const int qg = q_first + ql;
   const int tid = threadIdx.x, lane = tid & 63, wave = armi::wave_id();
-  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ts[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int pn_all = 0, pn_sel = 0;
   (void)ts;
+  (void)pn_all;
+  (void)pn_sel;
   ARMI_FP_T(ts[0]);
   if (!felig[ql]) return;  // uniform: the exact scan answers
-  if (tid < kQB && qof[tid] == ql) sh[1] = tid;
-  __syncthreads();
-  const int slot = sh[1];
-  const int nt = qcount[slot];
+  const int nt = fnt[ql];
 #ifdef ARMI_SPARSE_PROFILE
   auto prof_out = [&](int rounds) {
     if (tid == 0) {
       ARMI_FP_T(ts[7]);
-      for (int i = 1; i < 8; ++i) g_fmerge_prof[ql * 8 + i] = ts[i] ? ts[i] - ts[0] : 0;
-      g_fmerge_prof[ql * 8] = rounds;
+      for (int i = 1; i < 8; ++i) g_fmerge_prof[ql * 16 + i] = ts[i] ? ts[i] - ts[0] : 0;
+      g_fmerge_prof[ql * 16] = rounds;
+      g_fmerge_prof[ql * 16 + 8] = nt;
+      g_fmerge_prof[ql * 16 + 9] = sh[3];
+      g_fmerge_prof[ql * 16 + 10] = pn_all;
+      g_fmerge_prof[ql * 16 + 11] = pn_sel;
+      for (int i = 8; i < 11; ++i) g_fmerge_prof[ql * 16 + 4 + i] = ts[i] ? ts[i] - ts[0] : 0;
     }
   };
 #else
@@ -724,12 +836,10 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
   if (tid == 0) sh[3] = 0;
   __syncthreads();
   for (int j = tid; j < nt; j += 256) {
-    const int32_t t = uterm[qu[slot * kQStride + j]];
-    tterm[j] = t;
-    tw[j] = qlist[slot * kQStride + j].w;
-    const int32_t d = dense_of[t];
-    tcol[j] = d;
-    if (d < 0) atomicAdd(&sh[3], 1);
+    const int4 ti = fterm[ql * kMaxTerms + j];
+    tinfo[j] = ti;
+    tw[j] = fw[ql * kMaxTerms + j];
+    if (ti.x < 0) atomicAdd(&sh[3], 1);
   }
   __syncthreads();
   const bool rare = sh[3] > 0;  // terms without an fp32 column: values from their postings
@@ -755,14 +865,35 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       t0 = from_ord_key_f(prefix);
     }
     if (lane == 0) t0s = t0;
+    ARMI_FP_T(ts[8]);
   }
-  // rank of entry i among n entries of (key, row) by (key desc, row asc)
-  auto rank_of = [&](const float* key, const int32_t* row, int n, int i) {
-    const float ki = key[i];
-    const int32_t ri = row[i];
-    int r = 0;
-    for (int j = 0; j < n; ++j) r += armi::approx_better(key[j], row[j], ki, ri) ? 1 : 0;
-    return r;
+  // rank of each of n entries of (key, row) by (key desc, row asc): tpe threads per entry each
+  // count a slice of the others (16-B LDS reads), summed across the tpe lanes; emit(i, rank)
+  auto rank_all = [&](const float* key, const int32_t* row, int n, auto&& emit) {
+    const int lt = n <= 64 ? 2 : (n <= 128 ? 1 : 0);  // log2 tpe
+    const int tpe = 1 << lt;
+    const int per = (((n + tpe - 1) >> lt) + 3) & ~3;
+    for (int f0 = 0; f0 < (n << lt); f0 += 256) {
+      const int f = f0 + tid;
+      const int i = f >> lt, part = f & (tpe - 1);
+      int r = 0;
+      if (i < n) {
+        const float ki = key[i];
+        const int32_t ri = row[i];
+        const int j1 = min(n, (part + 1) * per);
+        for (int j = part * per; j < j1; j += 4) {
+          const float4 k4 = *reinterpret_cast<const float4*>(key + j);
+          const int4 r4 = *reinterpret_cast<const int4*>(row + j);
+          r += armi::approx_better(k4.x, r4.x, ki, ri) ? 1 : 0;
+          r += (j + 1 < j1) & armi::approx_better(k4.y, r4.y, ki, ri) ? 1 : 0;
+          r += (j + 2 < j1) & armi::approx_better(k4.z, r4.z, ki, ri) ? 1 : 0;
+          r += (j + 3 < j1) & armi::approx_better(k4.w, r4.w, ki, ri) ? 1 : 0;
+        }
+      }
+      if (lt >= 1) r += __shfl_xor(r, 1);
+      if (lt >= 2) r += __shfl_xor(r, 2);
+      if (i < n && part == 0) emit(i, r);
+    }
   };
   float thr = kNegInf;
   for (int round = 0; round < 2; ++round) {
@@ -773,37 +904,54 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     }
     if (round == 0) thr = t0s;
     __syncthreads();
+    // the pool entries >= thr into skey / srow: per-thread counts, a wave prefix sum and one LDS
+    // atomic per wave (no per-entry atomic round trips); the others' maximum joins the bound
     float dmax = kNegInf;
+    int c = 0;
 #pragma unroll
     for (int j = 0; j < kSmPer; ++j) {
-      if (kk[j] == kNegInf) continue;
-      if (kk[j] >= thr) {
-        const int s2 = atomicAdd(&sh[0], 1);
-        if (s2 < kFSel) {
-          skey[s2] = kk[j];
-          srow[s2] = rw[j];
+      const bool sel = kk[j] != kNegInf && kk[j] >= thr;
+      c += sel ? 1 : 0;
+      dmax = fmaxf(dmax, sel ? kNegInf : kk[j]);
+    }
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    int wbase = 0;
+    if (lane == 63 && incl > 0) wbase = atomicAdd(&sh[0], incl);
+    int pos = __shfl(wbase, 63) + incl - c;
+    if (c > 0) {
+#pragma unroll
+      for (int j = 0; j < kSmPer; ++j) {
+        if (kk[j] != kNegInf && kk[j] >= thr) {
+          if (pos < kFSel) {
+            skey[pos] = kk[j];
+            srow[pos] = rw[j];
+          }
+          ++pos;
         }
-      } else {
-        dmax = fmaxf(dmax, kk[j]);
       }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dmax = fmaxf(dmax, armi::xor_stride(dmax, off));
     if (lane == 0) red[4 + wave] = dmax;
     __syncthreads();
+    if (round == 0) ARMI_FP_T(ts[9]);
     const int n_all = sh[0];
     if (n_all > kFSel) return;  // uniform: too many ties for the rescore, the exact scan answers
     float bound = fmaxf(list_bound, fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7])));
     int n_sel = n_all;
     if (round == 0 && n_all > kc) {
       // the kc best keys only; the (kc+1)-th joins the bound of the rows left out
-      for (int i = tid; i < n_all; i += 256) {
-        const int r = rank_of(skey, srow, n_all, i);
+      rank_all(skey, srow, n_all, [&](int i, int r) {
         if (r <= kc) {
           tkey[r] = skey[i];
           trow[r] = srow[i];
         }
-      }
+      });
       __syncthreads();
       bound = fmaxf(bound, tkey[kc]);
       for (int i = tid; i < kc; i += 256) {
@@ -812,8 +960,11 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       }
       n_sel = kc;
       __syncthreads();
+      if (round == 0) ARMI_FP_T(ts[10]);
     }
     ARMI_FP_T(ts[2]);
+    pn_all = n_all;
+    pn_sel = n_sel;
     // exact scores of the selected rows, in chunks of rows whose (row, term) slots fit vals
     const int chunk = max(1, min(kFSel, kFVal / nt));
     for (int c0 = 0; c0 < n_sel; c0 += chunk) {
@@ -824,43 +975,22 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
       // sentinel (NaN bits) = no value yet
       for (int f = tid; f < nr * nt; f += 256) {
         const int i = f / nt, j = f - i * nt;
-        const int32_t d = tcol[j];
+        const int32_t d = tinfo[j].x;
         uint32_t bits = 0u;
         if (d >= 0) bits = dense_val[(size_t)d * dense_stride + srow[c0 + i]];
         vals[f] = __uint_as_float(bits ? bits : 0xffffffffu);
       }
       if (rare) {  // uniform: a term without a column (df < rows / 8)
-        // its value for each selected row from its postings (rows ascending): a binary search
-        // within the row's range (start_tab for a term of >= 256 postings, else the whole list
-        // of < 256), one (row, term) pair per thread; the searches stay inside a few small lists
-        // (the rows' CSR entries, scattered over the whole CSR, took ~29 us per query)
+        // its value for each selected row from the term's rare-value table (two independent
+        // 64-B bucket loads), one (row, term) pair per thread
         __syncthreads();  // (the column loads' vals writes before these)
+        ARMI_FP_T(ts[6]);
         for (int f = tid; f < nr * nt; f += 256) {
           const int i = f / nt, j = f - i * nt;
-          if (tcol[j] >= 0) continue;
-          const int32_t r = srow[c0 + i];
-          const int32_t t = tterm[j];
-          const int32_t b0 = term_ptr[t];
-          const int32_t l = long_of[t];
-          int32_t a = b0, n = term_ptr[t + 1] - 1 - b0;  // (the sentinel excluded)
-          if (l >= 0) {
-            const int gq = (int)(r / range_rows);
-            a = b0 + start_tab[(size_t)l * n_ranges + gq];
-            const int32_t e = gq + 1 < n_ranges ? b0 + start_tab[(size_t)l * n_ranges + gq + 1]
-                                                : term_ptr[t + 1] - 1;
-            n = e - a;
-          }
-          while (n > 0) {  // first posting with row >= r
-            const int32_t h = n >> 1;
-            if (post[a + h].x < r) {
-              a += h + 1;
-              n -= h + 1;
-            } else {
-              n = h;
-            }
-          }
-          const int2 pv = post[a];
-          if (pv.x == r) vals[f] = __int_as_float(pv.y);  // (a zero value is stored as -0.0)
+          const int4 ti = tinfo[j];
+          if (ti.x >= 0 || ti.y < 0) continue;  // a column, or no posting at all
+          const uint32_t bits = rare_value(rare_tab, ti.y, ti.z, (uint32_t)ti.w, srow[c0 + i]);
+          if (bits) vals[f] = __uint_as_float(bits);
         }
       }
       __syncthreads();
@@ -881,15 +1011,14 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
     ARMI_FP_T(ts[3]);
     // rank the exact scores (score desc, row asc); the best k go to tkey / trow
     int mem = 0;
-    for (int i = tid; i < n_sel; i += 256) {
-      mem += skey[i] != kNegInf;
-      const int r = rank_of(skey, srow, n_sel, i);
+    for (int i = tid; i < n_sel; i += 256) mem += skey[i] != kNegInf;
+    if (mem) atomicAdd(&sh[2], mem);
+    rank_all(skey, srow, n_sel, [&](int i, int r) {
       if (r < k) {
         tkey[r] = skey[i];
         trow[r] = srow[i];
       }
-    }
-    if (mem) atomicAdd(&sh[2], mem);
+    });
     __syncthreads();
     const int members = sh[2];
     const bool certified = members >= k ? tkey[k - 1] > bound : bound == kNegInf;

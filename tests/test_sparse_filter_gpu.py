@@ -170,3 +170,36 @@ def test_filter_posting_windows_beyond_one_per_tile(gpu, oracle_mod):
         got = _run(idx, (qi, qx, qv), k, gpu)
         _same(got, oracle_mod.sparse_topk(*csr, qi, qx, qv, k))
     assert ((got["flags"] & FILTERED) != 0).sum() >= 1
+
+
+@pytest.mark.parametrize("vocab", [250002, 1 << 20])
+def test_filter_prep_paths(gpu, oracle_mod, vocab):
+    """The filter's per-pass prep reads a query's list from the pass_terms wave's registers when
+    it is one 64-entry chunk of valid terms, else from the lists in memory (longer queries, a
+    term id >= vocab, and every query of the sorted numbering path for vocab > 2^18): all give
+    the oracle's answer, and most of them through the filter."""
+    csr, q = _synthetic(80_000, 48, gpu, seed=51)
+    ip, ix, iv = csr
+    qi, qx, qv = q
+    rng = np.random.default_rng(13)
+    lists = [(qx[qi[b]:qi[b + 1]], qv[qi[b]:qi[b + 1]]) for b in range(qi.size - 1)]
+    for b in range(0, 48, 6):  # 70-110 terms: two 64-entry chunks
+        t = np.unique(np.concatenate([lists[(b + j) % 48][0] for j in range(8)]))[:110]
+        lists[b] = (t, rng.uniform(0.05, 0.35, t.size).astype(np.float32))
+    for b in range(3, 48, 12):  # one term id beyond the vocabulary
+        t, w = lists[b]
+        lists[b] = (np.append(t, vocab + 7).astype(np.int32), np.append(w, 0.3).astype(np.float32))
+    if vocab > 250002:  # an order-preserving move of the upper ids beyond the bitmap's range
+        ix = np.where(ix >= 200000, ix + 300000, ix).astype(np.int32)
+        lists = [(np.where(t >= 200000, t + 300000, t).astype(np.int32), w) for t, w in lists]
+    qi2 = np.zeros(len(lists) + 1, np.int32)
+    qi2[1:] = np.cumsum([t.size for t, _ in lists])
+    qx2 = np.concatenate([t for t, _ in lists]).astype(np.int32)
+    qv2 = np.concatenate([w for _, w in lists]).astype(np.float32)
+    csr2 = (ip, ix, iv)
+    from audio_rag_amd.retrieval.device import SparseIndex
+
+    idx = SparseIndex(*(_t(a, gpu) for a in csr2), vocab, 0)
+    got = _run(idx, (qi2, qx2, qv2), 20, gpu)
+    _same(got, oracle_mod.sparse_topk(*csr2, qi2, qx2, qv2, 20))
+    assert ((got["flags"] & FILTERED) != 0).mean() >= 0.75, got["flags"]
