@@ -665,7 +665,7 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   // unused and their stores skipped, so every path issues the same loads in the same order and
   // the compiler's wait counts stay exact)
   for (int s0 = 0; s0 < S; s0 += kFDepth) {
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int d = 0; d < kFDepth; ++d) {
       const int s = s0 + d;
       issue(s + kFDepth - 1, (d + kFDepth - 1) % kFDepth);
@@ -885,9 +885,9 @@ __global__ __launch_bounds__(256) void sparse_filter_merge_kernel(
           const float4 k4 = *reinterpret_cast<const float4*>(key + j);
           const int4 r4 = *reinterpret_cast<const int4*>(row + j);
           r += armi::approx_better(k4.x, r4.x, ki, ri) ? 1 : 0;
-          r += (j + 1 < j1) & armi::approx_better(k4.y, r4.y, ki, ri) ? 1 : 0;
-          r += (j + 2 < j1) & armi::approx_better(k4.z, r4.z, ki, ri) ? 1 : 0;
-          r += (j + 3 < j1) & armi::approx_better(k4.w, r4.w, ki, ri) ? 1 : 0;
+          r += ((j + 1 < j1) && armi::approx_better(k4.y, r4.y, ki, ri)) ? 1 : 0;
+          r += ((j + 2 < j1) && armi::approx_better(k4.z, r4.z, ki, ri)) ? 1 : 0;
+          r += ((j + 3 < j1) && armi::approx_better(k4.w, r4.w, ki, ri)) ? 1 : 0;
         }
       }
       if (lt >= 1) r += __shfl_xor(r, 1);

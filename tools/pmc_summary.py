@@ -1,24 +1,28 @@
-"""Per-dispatch averages of the PMC counters a rocprofv3 --pmc pass recorded for one kernel."""
+"""Per-kernel averages of rocprofv3 --pmc counter CSVs (sum over a dispatch's instances, averaged
+over dispatches). Usage: pmc_summary.py CSV [CSV ...] (kernels whose name contains 'sparse' or
+'pass_terms')."""
 import collections
 import csv
 import sys
 
 
-def summary(paths, kernel):
-    out = {}
-    for path in paths:
-        agg = collections.defaultdict(float)
-        disp = collections.defaultdict(set)
+def main() -> None:
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    seen = collections.defaultdict(set)
+    for path in sys.argv[1:]:
         for r in csv.DictReader(open(path)):
-            if kernel in r["Kernel_Name"]:
-                agg[r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[r["Counter_Name"]].add(r["Dispatch_Id"])
-        for k, v in agg.items():
-            out[k] = v / max(1, len(disp[k]))
-    return out
+            k = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")
+            k = r["Kernel_Name"].split("::")[-1].split("(")[0] if "::" in r["Kernel_Name"] else k
+            if "sparse" not in k and "pass_terms" not in k:
+                continue
+            per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            seen[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+    for k, cs in per.items():
+        print(k)
+        for c, v in sorted(cs.items()):
+            n = max(len(seen[(k, c)]), 1)
+            print(f"  {c:28s} {v / n:16.1f}")
 
 
 if __name__ == "__main__":
-    kern = sys.argv[1]
-    for k, v in sorted(summary(sys.argv[2:], kern).items()):
-        print(f"{k:28s} {v:16.0f}")
+    main()
