@@ -107,6 +107,18 @@ __host__ __device__ inline float u8_level(float v, float s) {
   return a > 255.f ? 255.f : a;
 }
 
+// The scan's level of a posting value (v >= 0, s > 0, inv ~ 1/s): a valid bound like u8_level
+// (a * s >= v, a <= 255) without a division: ceil(v * inv) is at most one below ceil(v / s)
+// (v / s <= 255, two roundings of 2^-24), and the sign of fma(a, s, -v) (one rounding of the
+// exact a * s - v) says whether a * s >= v; on equality (or an underflowed difference) one level
+// more keeps the bound safe. It may exceed u8_level's level by one; any a with a * s >= v is a
+// valid bound, and 255 s >= v for every value of the term.
+__device__ __forceinline__ float u8_level_fast(float v, float s, float inv) {
+  float a = ceilf(v * inv);
+  a += fmaf(a, s, -v) <= 0.f && v > 0.f ? 1.f : 0.f;
+  return fminf(a, 255.f);
+}
+
 // 4 bytes -> 4 fp16 (exact): byte b as fp16 bits 0x64bb = 1024 + b, minus 1024.
 __device__ __forceinline__ fu32x2 u8x4_f16(uint32_t x) {
   const fhalf2 l = __builtin_bit_cast(fhalf2, __builtin_amdgcn_perm(0x64646464u, x, 0x04010400u));
@@ -415,13 +427,14 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
   }
 
   int2 creg = make_int2(kFNone, 0);
-  float sreg = 0.f;
+  float sreg = 0.f, ireg = 0.f;
   {
     const int sg = lane >> 1, u = sg * kFK + 2 * wave + (lane & 1);
     if (sg < nSeg && u < nU) {
       const int32_t t = uterm[u];
       const int32_t d = col8_of[t];
       sreg = term_scale[t];
+      ireg = sreg > 0.f ? 1.f / sreg : 0.f;
       creg = d >= 0 ? make_int2(-(d + 1), 0)
                     : range_cursor(t, g, lo, n_ranges, term_ptr, long_of, start_tab, post);
     }
@@ -481,7 +494,7 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
       dst[0] = fu32x4{0u, 0u, 0u, 0u};
       dst[1] = fu32x4{0u, 0u, 0u, 0u};
       if (cx == kFNone || cy >= thi) continue;  // no posting of the term in this tile
-      const float sc = rl_f(sreg, c);
+      const float sc = rl_f(sreg, c), isc = rl_f(ireg, c);
       fp4 v = ring[slot][j];
       int adv = 0;  // postings consumed before v
       while (true) {  // wave-uniform trip count
@@ -489,8 +502,8 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
         const int ne = be == ~0ull ? 64 : __builtin_clzll(~be);
         const int no = bo == ~0ull ? 64 : __builtin_clzll(~bo);
         const int n = min(2 * ne, 2 * no + 1);  // postings of v inside the tile
-        const _Float16 a0 = (_Float16)u8_level(__int_as_float(v.y), sc);
-        const _Float16 a1 = (_Float16)u8_level(__int_as_float(v.w), sc);
+        const _Float16 a0 = (_Float16)u8_level_fast(__int_as_float(v.y), sc, isc);
+        const _Float16 a1 = (_Float16)u8_level_fast(__int_as_float(v.w), sc, isc);
         unsigned char* d0 = rev2 < n ? rowp + 2 * (v.x - tlo) : trash + 2 * lane;
         unsigned char* d1 = rev2 + 1 < n ? rowp + 2 * (v.z - tlo) : trash + 2 * lane;
         *reinterpret_cast<_Float16*>(d0) = a0;
@@ -526,6 +539,7 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
     const unsigned char* bb = bimg + seg * kFBBytes;
     const fu32x4 b0 = *reinterpret_cast<const fu32x4*>(bb + b_off);
     const fu32x4 b1 = *reinterpret_cast<const fu32x4*>(bb + 32 * 32 + b_off);
+    fhalf8 a[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned char* p = img + a_off + 2 * 32 * (4 * wave + i);
@@ -533,9 +547,22 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
       const fs4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_fs4*)(p));
       const fs4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_fs4*)(p + 4 * kFImgStride));
       const fu32x2 l2 = __builtin_bit_cast(fu32x2, lo4), h2 = __builtin_bit_cast(fu32x2, hi4);
-      const fhalf8 a = __builtin_bit_cast(fhalf8, fu32x4{l2.x, l2.y, h2.x, h2.y});
-      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(fhalf8, b0), acc[i][0], 0, 0, 0);
-      acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(fhalf8, b1), acc[i][1], 0, 0, 0);
+      a[i] = __builtin_bit_cast(fhalf8, fu32x4{l2.x, l2.y, h2.x, h2.y});
+    }
+    // a tile's first segment starts its sums from the MFMA's zero operand (no 128 register
+    // clears per tile in the epilogue)
+    if (seg == 0) {  // uniform
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], __builtin_bit_cast(fhalf8, b0), ff32x16{}, 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], __builtin_bit_cast(fhalf8, b1), ff32x16{}, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], __builtin_bit_cast(fhalf8, b0), acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], __builtin_bit_cast(fhalf8, b1), acc[i][1], 0, 0, 0);
+      }
     }
   };
 
@@ -620,11 +647,6 @@ __global__ __launch_bounds__(kFThreads) void sparse_filter_scan_kernel(
           net(1, ok ? acc[i][1][v] : 0.f, 16 * i + v);
         }
       }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i][0] = ff32x16{};
-      acc[i][1] = ff32x16{};
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
