@@ -41,6 +41,8 @@ int allow_lds_raw(const void* kernel, size_t bytes) {
 
 struct Timing {
   bool enabled = false;
+  int period = 1;                        // time every period-th launch of a slot
+  int64_t seen[ARMI_TIMING_SLOTS] = {};  // launches of the slot since timing was enabled
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[ARMI_TIMING_SLOTS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> spare;
   std::mutex mu;
@@ -54,6 +56,7 @@ int TimedLaunch::begin(int s, hipStream_t st) {
   Timing& t = timing();
   std::lock_guard<std::mutex> g(t.mu);
   if (!t.enabled || s < 0 || s >= ARMI_TIMING_SLOTS) return 0;
+  if (t.seen[s]++ % t.period != 0) return 0;
   if (t.spare.empty()) {
     hipEvent_t a, b;
     ARMI_HIP(hipEventCreate(&a));
@@ -67,6 +70,36 @@ int TimedLaunch::begin(int s, hipStream_t st) {
   stream = st;
   ARMI_HIP(hipEventRecord(ev[0], stream));
   return 1;
+}
+
+int TimedKernel::begin(int s, hipStream_t stream) {
+  Timing& t = timing();
+  std::lock_guard<std::mutex> g(t.mu);
+  if (!t.enabled || s < 0 || s >= ARMI_TIMING_SLOTS) return 0;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  ARMI_HIP(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) return 0;
+  if (t.seen[s]++ % t.period != 0) return 0;
+  if (t.spare.empty()) {
+    hipEvent_t a, b;
+    ARMI_HIP(hipEventCreate(&a));
+    ARMI_HIP(hipEventCreate(&b));
+    t.spare.emplace_back(a, b);
+  }
+  ev[0] = t.spare.back().first;
+  ev[1] = t.spare.back().second;
+  t.spare.pop_back();
+  slot = s;
+  return 1;
+}
+
+int TimedKernel::commit() {
+  if (slot < 0) return ARMI_OK;
+  Timing& t = timing();
+  std::lock_guard<std::mutex> g(t.mu);
+  t.pending[slot].emplace_back(ev[0], ev[1]);
+  slot = -1;
+  return ARMI_OK;
 }
 
 int TimedLaunch::end() {
@@ -95,7 +128,9 @@ const char* armi_source_digest(void) { return ARMI_SOURCE_DIGEST; }
 int armi_scan_timing_enable(int enable) {
   armi::Timing& t = armi::timing();
   std::lock_guard<std::mutex> g(t.mu);
-  t.enabled = enable != 0;
+  t.enabled = enable > 0;
+  t.period = enable > 1 ? enable : 1;
+  for (auto& c : t.seen) c = 0;
   return ARMI_OK;
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string>
 
@@ -43,6 +44,35 @@ struct TimedLaunch {
   int begin(int slot, hipStream_t stream);  // 0 = not timed, 1 = timed, <0 = error (set)
   int end();
 };
+
+// One kernel's duration into a timing slot without marker packets around it: begin() hands out
+// the slot's event pair when timing is on (ev[0] = ev[1] = nullptr when off), the caller passes
+// them to hipExtLaunchKernelGGL, which binds them to the dispatch's own start / end timestamps,
+// and commit() files them. (Two hipEventRecord markers per launch cost ~6 us of a 61-us step at
+// 100k rows: each waits for the pipe to drain.)
+struct TimedKernel {
+  int slot = -1;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  // 0 = not timed (timing off, or the stream is being captured into a graph), 1 = timed,
+  // <0 = error (set)
+  int begin(int slot, hipStream_t stream);
+  int commit();
+};
+
+// kern<<<grid, block, lds, stream>>>(args...), its duration filed under `slot` when timing is on
+template <typename K, typename... Args>
+int timed_kernel(int slot, K kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+                 Args... args) {
+  TimedKernel tk;
+  const int on = tk.begin(slot, stream);
+  if (on < 0) return ARMI_ERR_HIP;
+  if (on)
+    hipExtLaunchKernelGGL(kern, grid, block, (std::uint32_t)lds, stream, tk.ev[0], tk.ev[1], 0u,
+                          args...);
+  else
+    kern<<<grid, block, lds, stream>>>(args...);
+  return tk.commit();
+}
 
 // Raises a kernel's dynamic-LDS limit to `bytes` (> 64 KiB needs it) on the current device, once
 // per (device, kernel): later searches issue stream work only (no runtime call per search, so the

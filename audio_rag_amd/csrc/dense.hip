@@ -2589,36 +2589,37 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
     }
     auto kern = i8 ? dense_gemm_scan_w4_kernel<DIM, 0, true> : dense_gemm_scan_w4_kernel<DIM, 0, false>;
     if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
-    armi::TimedLaunch tl;
-    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    kern<<<dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(), stream>>>(
-        idx->rows, idx->inv_norm32, i8 ? mask_i8 : row_mask, n_scan, gp.rows_per_range,
-        gp.n_ranges, gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound, idx->rows8,
-        idx->a32, idx->e32, idx->tile_ord, w.q8, w.qsc);
+    const int rc_l = armi::timed_kernel(
+        ARMI_TIMING_DENSE_SCAN, kern, dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(),
+        stream, idx->rows, idx->inv_norm32, i8 ? mask_i8 : row_mask, n_scan, gp.rows_per_range,
+        gp.n_ranges, gp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
+        (const int8_t*)idx->rows8, (const float*)idx->a32, (const float*)idx->e32,
+        (const int32_t*)idx->tile_ord, (const int8_t*)w.q8, (const float4*)w.qsc);
     ARMI_LAUNCHED("dense_gemm_scan_w4_kernel");
-    if (int rc = tl.end()) return rc;
+    if (rc_l) return rc_l;
   } else if (use_i8_filter(idx, k)) {
     kc = kc_i8(k);
     auto kern = use_nt_stream(idx) ? dense_scan_i8_kernel<DIM, false, true>
                                    : dense_scan_i8_kernel<DIM, false, false>;
     if (int rc = allow_lds(kern, scan_i8_lds_bytes<DIM>())) return rc;
-    armi::TimedLaunch tl;
-    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    kern<<<dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(), stream>>>(
-        idx->rows8, idx->a32, idx->e32, mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound,
-        idx->tile_ord, nullptr, nullptr, nullptr, nullptr, 0, sp.xcd_step);
+    const int rc_l = armi::timed_kernel(
+        ARMI_TIMING_DENSE_SCAN, kern, dim3(sp.grid), dim3(kThreads), scan_i8_lds_bytes<DIM>(),
+        stream, (const int8_t*)idx->rows8, (const float*)idx->a32, (const float*)idx->e32,
+        mask_i8, idx->n_rows, idx->n_tiles, sp.tiles_per_wg, sp.n_wg, sp.n_qb, queries, nq,
+        w.cand_key, w.cand_row, w.cand_bound, (const int32_t*)idx->tile_ord,
+        (const uint32_t*)nullptr, (const float*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, 0,
+        sp.xcd_step);
     ARMI_LAUNCHED("dense_scan_i8_kernel");
-    if (int rc = tl.end()) return rc;
+    if (rc_l) return rc_l;
   } else {
     if (int rc = allow_lds(dense_scan_kernel<DIM>, scan_lds_bytes<DIM>())) return rc;
-    armi::TimedLaunch tl;
-    if (tl.begin(ARMI_TIMING_DENSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-    dense_scan_kernel<DIM><<<dim3(sp.grid), dim3(kThreads), scan_lds_bytes<DIM>(), stream>>>(
-        idx->rows, idx->inv_norm32, row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg,
-        sp.n_wg, sp.n_qb, queries, nq, w.cand_key, w.cand_row, w.cand_bound);
+    const int rc_l = armi::timed_kernel(
+        ARMI_TIMING_DENSE_SCAN, dense_scan_kernel<DIM>, dim3(sp.grid), dim3(kThreads),
+        scan_lds_bytes<DIM>(), stream, (const uint16_t*)idx->rows, (const float*)idx->inv_norm32,
+        row_mask, idx->n_rows, idx->n_tiles, sp.tiles_per_wg, sp.n_wg, sp.n_qb, queries, nq,
+        w.cand_key, w.cand_row, w.cand_bound);
     ARMI_LAUNCHED("dense_scan_kernel");
-    if (int rc = tl.end()) return rc;
+    if (rc_l) return rc_l;
   }
   // one merge for every query of the call: per-pass merges would serialise a latency-bound
   // kernel per 64 queries (the multi-GPU step scans G*64 queries)

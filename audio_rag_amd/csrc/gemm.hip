@@ -455,11 +455,10 @@ int armi_enc_linear_f16(const uint16_t* x, const uint16_t* w, const float* bias,
   const int grid = (int)std::min<int64_t>(n_tiles, cus);
   auto kern = epilogue == ARMI_EPI_BIAS_GELU ? linear_f16_kernel<1> : linear_f16_kernel<0>;
   if (int rc = armi::allow_lds(kern, kLds)) return rc;
-  armi::TimedLaunch tl;
-  if (tl.begin(ARMI_TIMING_ENCODER_GEMM, stream) < 0) return ARMI_ERR_HIP;
-  kern<<<dim3(grid), dim3(kThreads), kLds, stream>>>(x, w, bias, out, m, n, k, n_tp, n_tiles);
+  const int rc_l = armi::timed_kernel(ARMI_TIMING_ENCODER_GEMM, kern, dim3(grid), dim3(kThreads),
+                                      kLds, stream, x, w, bias, out, m, n, k, n_tp, n_tiles);
   ARMI_LAUNCHED("linear_f16_kernel");
-  return tl.end();
+  return rc_l;
 }
 
 

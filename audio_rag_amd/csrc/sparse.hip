@@ -1975,15 +1975,16 @@ int armi_sparse_topk(const armi_sparse_index* idx, const int32_t* q_indptr,
           w.qcount, w.qof, pflags, w.coll_count, fp);
     ARMI_LAUNCHED("pass_terms_kernel");
     if (filter) {
-      armi::TimedLaunch tf;
-      if (tf.begin(ARMI_TIMING_SPARSE_SCAN, stream) < 0) return ARMI_ERR_HIP;
-      sparse_filter_scan_kernel<<<dim3(idx->n_ranges), dim3(kFThreads), kFLds, stream>>>(
-          idx->term_ptr, reinterpret_cast<const int2*>(idx->post), idx->long_of, idx->start_tab,
-          idx->n_rows, idx->range_rows, idx->n_ranges, row_mask, w.uterm, w.n_terms, idx->col8_of,
-          idx->dense_u8, idx->dense8_stride, idx->term_scale, w.fB, w.fscale, w.cand_key,
-          w.cand_row, w.cand_bound);
+      const int rc_f = armi::timed_kernel(
+          ARMI_TIMING_SPARSE_SCAN, sparse_filter_scan_kernel, dim3(idx->n_ranges), dim3(kFThreads),
+          kFLds, stream, (const int32_t*)idx->term_ptr, reinterpret_cast<const int2*>(idx->post),
+          (const int32_t*)idx->long_of, (const int32_t*)idx->start_tab, idx->n_rows,
+          idx->range_rows, idx->n_ranges, row_mask, (const int32_t*)w.uterm,
+          (const int32_t*)w.n_terms, (const int32_t*)idx->col8_of, (const uint8_t*)idx->dense_u8,
+          idx->dense8_stride, (const float*)idx->term_scale, (const uint16_t*)w.fB,
+          (const float*)w.fscale, w.cand_key, w.cand_row, w.cand_bound);
       ARMI_LAUNCHED("sparse_filter_scan_kernel");
-      if (int rc = tf.end()) return rc;
+      if (rc_f) return rc_f;
       sparse_filter_merge_kernel<<<dim3(nqp), dim3(256), 0, stream>>>(
           w.cand_key, w.cand_row, w.cand_bound, idx->n_ranges, q0, k, kc, idx->ordinal_base,
           w.felig, w.fterm, w.fw, w.fnt, idx->rare_tab, idx->dense_val, idx->dense_stride,

@@ -438,7 +438,10 @@ def main() -> None:
     for i in range(args.warmup):
         step(i)
     barrier()
-    _armi.call("armi_scan_timing_enable", 1)
+    # every 8th launch of the timed kernels carries its event pair (an event-bound dispatch costs
+    # ~5 us of a 61-us step at 100k rows; profiles/r06_timing_cost_ab.txt); ARMI_BENCH_TIMING
+    # overrides the period (0 = off, for that A/B)
+    _armi.call("armi_scan_timing_enable", int(os.environ.get("ARMI_BENCH_TIMING", "8")))
     for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN, _armi.TIMING_SPARSE_STAGE):
         _armi.call("armi_kernel_timing_read", slot, _armi.ctypes.byref(_armi.ctypes.c_double()),
                    _armi.ctypes.byref(_armi.ctypes.c_int64()))
@@ -457,6 +460,7 @@ def main() -> None:
         # events: the scans' launch times come from eager launches of the same kernels over the
         # same batches right after the timed region (the rerank, timed above, is not rerun).
         n_eager = min(args.steps, 20)
+        _armi.call("armi_scan_timing_enable", 1)  # (outside the timed region: every launch)
         for i in range(n_eager):
             j = i % n_q_batches
             hybrid(lambda: index.topk(queries[j], pre_k, workspace=ws),
@@ -474,6 +478,7 @@ def main() -> None:
             _armi.call("armi_kernel_timing_read", slot, _armi.ctypes.byref(v), _armi.ctypes.byref(c))
             sparse_timing[key] = (v.value, c.value)
         barrier()
+        _armi.call("armi_scan_timing_enable", 1)
         for i in range(min(args.steps, 20)):
             sindex.topk(*q_sparse[i % n_q_batches], pre_k, workspace=sws)
         barrier()
@@ -526,7 +531,7 @@ def main() -> None:
         return
 
     total_queries = world * batch * args.steps
-    scan_avg_ms = tot_ms.value / max(launches.value, 1)
+    scan_avg_ms = tot_ms.value / launches.value if launches.value else float("nan")
     shard_rows = hi - lo
     nq_scan = world * batch  # queries each rank's scan processes per step (all-gathered)
     form = index.scan_form(nq_scan, pre_k)  # which scan armi_dense_topk ran (include/armi.h)

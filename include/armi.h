@@ -168,9 +168,11 @@ int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
                                   hipStream_t stream);
 
 /* Live timing of the dominant kernels for roofline reporting (bench.py): while enabled, every
- * launch of a timed kernel is bracketed by a HIP event pair on the stream it is launched on.
- * _read synchronises on the recorded events of one slot, returns the summed kernel time and the
- * launch count, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
+ * enable-th launch of a timed kernel (enable = 1: every launch; 0 disables) carries a HIP event
+ * pair: a scan kernel's events are bound to its own dispatch (hipExtLaunchKernel: the kernel's
+ * start and end, no marker packets), a whole sparse call is bracketed by events on its stream.
+ * Launches under stream capture are not timed. _read synchronises on the recorded events of one
+ * slot, returns the summed time and the number of timed launches, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
  * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (the dominant scan of armi_sparse_topk: the MFMA
  * filter scan when the filter runs, else sparse_scan_kernel), ARMI_TIMING_ENCODER_GEMM (the
  * cross-encoder GEMMs of armi_enc_linear_f16), ARMI_TIMING_SPARSE_STAGE (a whole
