@@ -1706,7 +1706,10 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
     ARMI_HIP(tmp.alloc(&nbscan, (size_t)vocab + 1));
     ARMI_HIP(tmp.alloc(&fail, 1));
     ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->rare_of), std::max<size_t>(vocab, 1) * 8));
-    for (int div = 4;; div /= 2) {
+    // (ARMI_RARE_DIV, a test knob: postings per bucket targeted, default 4; tests raise it to
+    // force full bucket pairs and the overflow chains)
+    const char* dv = getenv("ARMI_RARE_DIV");
+    for (int div = dv ? std::max(1, atoi(dv)) : 4;; div /= 2) {
       rare_buckets_kernel<<<grid_for((int64_t)vocab + 1, 256), 256, 0, stream>>>(
           idx->term_ptr, idx->dense_of, vocab, div, nb);
       ARMI_LAUNCHED("rare_buckets_kernel");
@@ -1747,7 +1750,8 @@ int build_inverted(armi_sparse_index* idx, const int64_t* indptr, const int32_t*
   ARMI_HIP(hipMemsetAsync(tmax, 0, ((size_t)vocab + 1) * 4, stream));
   ARMI_HIP(hipMemsetAsync(n_neg, 0, 8, stream));
   if (nnz > 0) {
-    term_max_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(indices, values, nnz, vocab, tmax, n_neg);
+    term_max_kernel<<<grid_for(nnz, 256), 256, 0, stream>>>(
+        skeys, reinterpret_cast<const int2*>(idx->post), nnz, vocab, tmax, n_neg);
     ARMI_LAUNCHED("term_max_kernel");
   }
   ARMI_HIP(hipMalloc(reinterpret_cast<void**>(&idx->term_scale), std::max<size_t>(vocab, 1) * 4));

@@ -141,20 +141,35 @@ __device__ __forceinline__ uint16_t ru_half(double p) {
 // ---------------------------------------------------------------------------- index build
 
 // tmax[t] = bit pattern of the largest value of term t (values >= 0 order as their bits;
-// -0.0 counts as 0), n_neg = values < 0.
-__global__ void term_max_kernel(const int32_t* __restrict__ indices, const float* __restrict__ values,
+// -0.0 counts as 0), n_neg = values < 0. Over the postings sorted by term (sorted entry i: see
+// dense_fill): a wave reduces its runs of one term first, so only the first lane of a run issues
+// the atomic (the CSR-order form's atomics on the hot terms took 21 ms per 96M values).
+__global__ void term_max_kernel(const uint32_t* __restrict__ skeys, const int2* __restrict__ post,
                                 int64_t nnz, int32_t vocab, uint32_t* __restrict__ tmax,
                                 unsigned long long* __restrict__ n_neg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  uint32_t t = 0xffffffffu, m = 0u;
   bool neg = false;
   if (i < nnz) {
-    const float v = values[i];
-    const int32_t t = indices[i];
-    neg = v < 0.f;
-    if (!neg && v > 0.f && t >= 0 && t < vocab) atomicMax(&tmax[t], __float_as_uint(v));
+    t = skeys[i];
+    if (t < (uint32_t)vocab) {
+      const float v = __int_as_float(post[i + t].y);
+      neg = v < 0.f;
+      m = v > 0.f ? __float_as_uint(v) : 0u;
+    } else {
+      t = 0xffffffffu;
+    }
   }
-  const unsigned long long m = __ballot(neg);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_neg, (unsigned long long)__popcll(m));
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {  // segmented max over the wave's run of term t
+    const uint32_t mo = __shfl_down(m, d), to = __shfl_down(t, d);
+    if (lane + d < 64 && to == t) m = max(m, mo);
+  }
+  const uint32_t tp = __shfl_up(t, 1);
+  if ((lane == 0 || tp != t) && t != 0xffffffffu && m) atomicMax(&tmax[t], m);
+  const unsigned long long b = __ballot(neg);
+  if (lane == 0 && b) atomicAdd(n_neg, (unsigned long long)__popcll(b));
 }
 
 // s_t = the least fp32 >= max_t / 255 with 255 s_t >= max_t (checked in fp64)
@@ -249,8 +264,10 @@ __global__ void rare_of_kernel(const int32_t* __restrict__ nb, const int32_t* __
   rare_of[t] = nb[t] > 0 ? make_int2(scan[t], nb[t] - 1) : make_int2(-1, 0);
 }
 
-// every posting of a table term into the emptier of its two buckets (sorted entry i: see
-// dense_fill); fail counts postings that found both full (the build retries with more buckets)
+// every posting of a table term into the emptier of its two buckets; when both are full, into
+// the first bucket after the second (cyclically in the term's table) that has room (a chain the
+// lookup follows only when both of a row's buckets are full); fail counts postings that found the
+// whole table full (never at these loads; the build then retries with more buckets)
 __global__ void rare_insert_kernel(const int2* __restrict__ rare_of, const int2* __restrict__ post,
                                    const uint32_t* __restrict__ skeys, int64_t nnz, int32_t vocab,
                                    int32_t* __restrict__ fill, uint2* __restrict__ tab,
@@ -263,33 +280,34 @@ __global__ void rare_insert_kernel(const int2* __restrict__ rare_of, const int2*
   if (ro.x < 0) return;
   const int2 pv = post[i + t];
   const uint32_t h1 = rare_hash1((uint32_t)pv.x, t);
-  int64_t b1 = ro.x + (int64_t)(h1 & (uint32_t)ro.y);
-  int64_t b2 = ro.x + (int64_t)(rare_hash2(h1) & (uint32_t)ro.y);
-  if (fill[b2] < fill[b1]) {
-    const int64_t x = b1;
-    b1 = b2;
-    b2 = x;
-  }
-  int64_t b = b1;
-  int s = atomicAdd(&fill[b1], 1);
+  const uint32_t c1 = h1 & (uint32_t)ro.y, c2 = rare_hash2(h1) & (uint32_t)ro.y;
+  const uint32_t first = fill[ro.x + c2] < fill[ro.x + c1] ? c2 : c1;
+  uint32_t c = first;
+  int s = atomicAdd(&fill[ro.x + c], 1);
   if (s >= kRareSlots) {
-    b = b2;
-    s = atomicAdd(&fill[b2], 1);
-    if (s >= kRareSlots) {
-      atomicAdd(fail, 1);
-      return;
-    }
+    c = first == c1 ? c2 : c1;
+    s = atomicAdd(&fill[ro.x + c], 1);
   }
-  tab[b * kRareSlots + s] = make_uint2((uint32_t)pv.x, (uint32_t)pv.y);
+  for (uint32_t step = 1; s >= kRareSlots && step <= (uint32_t)ro.y; ++step) {
+    c = (c2 + step) & (uint32_t)ro.y;
+    s = atomicAdd(&fill[ro.x + c], 1);
+  }
+  if (s >= kRareSlots) {
+    atomicAdd(fail, 1);
+    return;
+  }
+  tab[((int64_t)ro.x + c) * kRareSlots + s] = make_uint2((uint32_t)pv.x, (uint32_t)pv.y);
 }
 
 // the value bits of row r in term table {base, mask} (t the term), 0 when r has no posting (a
-// zero value is stored as -0.0)
+// zero value is stored as -0.0): its two buckets in one round of loads; only when both are full
+// (slot 7 taken) and neither holds r, the chain after the second bucket up to a bucket with room
 __device__ __forceinline__ uint32_t rare_value(const uint2* __restrict__ tab, int32_t base,
                                                int32_t mask, uint32_t t, int32_t r) {
   const uint32_t h1 = rare_hash1((uint32_t)r, t);
+  const uint32_t c2 = rare_hash2(h1) & (uint32_t)mask;
   const uint4* p1 = reinterpret_cast<const uint4*>(tab + (base + (int64_t)(h1 & (uint32_t)mask)) * kRareSlots);
-  const uint4* p2 = reinterpret_cast<const uint4*>(tab + (base + (int64_t)(rare_hash2(h1) & (uint32_t)mask)) * kRareSlots);
+  const uint4* p2 = reinterpret_cast<const uint4*>(tab + (base + (int64_t)c2) * kRareSlots);
   uint4 v[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -302,7 +320,19 @@ __device__ __forceinline__ uint32_t rare_value(const uint2* __restrict__ tab, in
     bits = v[i].x == (uint32_t)r ? v[i].y : bits;
     bits = v[i].z == (uint32_t)r ? v[i].w : bits;
   }
-  return bits;
+  if (bits || v[3].z == 0xffffffffu || v[7].z == 0xffffffffu) return bits;
+  for (uint32_t step = 1; step <= (uint32_t)mask; ++step) {  // both full: the overflow chain
+    const uint4* p = reinterpret_cast<const uint4*>(
+        tab + (base + (int64_t)((c2 + step) & (uint32_t)mask)) * kRareSlots);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 w = p[i];
+      if (w.x == (uint32_t)r) return w.y;
+      if (w.z == (uint32_t)r) return w.w;
+    }
+    if (p[3].z == 0xffffffffu) return 0u;
+  }
+  return 0u;
 }
 
 // ---------------------------------------------------------------------------- per pass

@@ -203,3 +203,16 @@ def test_filter_prep_paths(gpu, oracle_mod, vocab):
     got = _run(idx, (qi2, qx2, qv2), 20, gpu)
     _same(got, oracle_mod.sparse_topk(*csr2, qi2, qx2, qv2, 20))
     assert ((got["flags"] & FILTERED) != 0).mean() >= 0.75, got["flags"]
+
+
+def test_filter_rare_tables_with_overflow_chains(gpu, oracle_mod, monkeypatch):
+    """The rescore's rare-term values come from per-term two-choice hash tables; built at 32
+    postings per 8-slot bucket (ARMI_RARE_DIV) nearly every bucket pair is full and most values
+    sit in the overflow chains: the answers must not change."""
+    monkeypatch.setenv("ARMI_RARE_DIV", "32")
+    csr, q = _synthetic(120_000, 64, gpu, seed=53)
+    idx = _index(csr, gpu)
+    for k in (5, 40):
+        got = _run(idx, q, k, gpu)
+        _same(got, oracle_mod.sparse_topk(*csr, *q, k))
+        assert ((got["flags"] & FILTERED) != 0).mean() >= 0.9
