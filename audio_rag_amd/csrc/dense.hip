@@ -1063,23 +1063,25 @@ void dense_gemm_scan_w4_kernel(
           float y;
           if constexpr (I8) {
             // D a32 + e32 c1 + c2 (divided by s_q). A dead row (inv 0, bias -FLT_MAX) gives -inf
-            // (c1 >= 1), clamped to -FLT_MAX: the row code would turn -inf into a NaN, which the
-            // chain below is not transparent to (a NaN moves b1 into b2)
-            y = __builtin_elementwise_maximumnum(
-                __builtin_fmaf((float)acc[m][n][j], inv[j],
-                               __builtin_fmaf(bias[j], qs_c1[n], qs_c2[n])),
-                -3.4028234663852886e38f);
+            // (c1 >= 1)
+            y = __builtin_fmaf((float)acc[m][n][j], inv[j],
+                               __builtin_fmaf(bias[j], qs_c1[n], qs_c2[n]));
           } else {
             y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
           }
-          // code m*16 + j (an inline constant) in the low 6 mantissa bits
-          const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
-          // (no NaN reaches the chain)
-          const float t = __builtin_elementwise_minimumnum(b1[n], e);
+          // code m*16 + j (an inline constant) in the low 6 mantissa bits, then clamped to
+          // >= -FLT_MAX: a coded -inf is a NaN (which the chain below is not transparent to) and
+          // becomes -FLT_MAX; the clamp's result is also canonical, so the v_med3_f32 below take
+          // it without canonicalising copies
+          const float e = __builtin_elementwise_maximumnum(
+              __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j)),
+              -3.4028234663852886e38f);
+          // (no NaN reaches the chain) b1 >= b2 >= b3: one max and two v_med3_f32 keep the
+          // best two and the third (was two min / three max)
+          const float nb3 = __builtin_amdgcn_fmed3f(b2[n], b3[n], e);
+          b2[n] = __builtin_amdgcn_fmed3f(b1[n], b2[n], e);
           b1[n] = __builtin_elementwise_maximumnum(b1[n], e);
-          const float t2 = __builtin_elementwise_minimumnum(b2[n], t);
-          b2[n] = __builtin_elementwise_maximumnum(b2[n], t);
-          b3[n] = __builtin_elementwise_maximumnum(b3[n], t2);
+          b3[n] = nb3;
         }
       }
     }
