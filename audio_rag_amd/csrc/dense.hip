@@ -101,6 +101,19 @@ constexpr int scan_lds_bytes() {
   return img > scratch ? img : scratch;
 }
 
+// dense_scan_i8_kernel's query image (round 6): the 64 fp16 query rows as they are in memory,
+// row q at q * (2 DIM + 16) B (the 16-B pad: the MFMA B reads of 16 lanes, queries r .. r + 15 at
+// one chunk, fall on 16 distinct 4-bank groups), copied by LDS-DMA (1-KB global_load_lds_dwordx4
+// pieces of one row, no register staging); the workgroup merge reuses the region.
+template <int DIM>
+constexpr int i8_qstride() { return DIM * 2 + 16; }
+template <int DIM>
+constexpr int i8_img_bytes() {
+  constexpr int img = kQB * i8_qstride<DIM>();
+  constexpr int scratch = kQB * 64 * 4 * 2 + kQB * 16 * 4;
+  return img > scratch ? img : scratch;
+}
+
 template <int DIM>
 __global__ __launch_bounds__(kThreads) void dense_scan_kernel(
     const uint16_t* __restrict__ rows, const float* __restrict__ inv_norm32,
@@ -394,8 +407,8 @@ __device__ __forceinline__ void scan_i8_body(
   int nq = min(kQB, q_stride - q0);
   const uint16_t* __restrict__ queries = queries_all + (size_t)q0 * DIM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  u32x4* qimg = reinterpret_cast<u32x4*>(smem);  // [KSTEPS][2][kQB] 16-byte fragments
-  float* qnorm = reinterpret_cast<float*>(smem + (size_t)KSTEPS * 2 * kQB * 16);  // [kQB] |q| up
+  constexpr int QS = i8_qstride<DIM>();  // query row stride of the image (B)
+  float* qnorm = reinterpret_cast<float*>(smem + (size_t)i8_img_bytes<DIM>());  // [kQB] |q| up
   float* qscale = qnorm + kQB;  // (unused slot, keeps the layout of scan_i8_lds_bytes)
   // (qscale + kQB: [8][kQB] unused slots, keep the layout of scan_i8_lds_bytes)
   int32_t* qsel = reinterpret_cast<int32_t*>(qscale + kQB + kQB * (kThreads / kQB));  // [kQB] COLLECT
@@ -480,33 +493,46 @@ __device__ __forceinline__ void scan_i8_body(
     }
   };
 
-  // 1. Per query: |q| rounded up (fp32 sum of 1024 squares: relative error < 2^-13), and the
-  //    fp16 fragment image (k-step s, half h: components 128(s>>3) + 64h + 8(s&7) .. +7, the
-  //    corpus chunks' order; 16-B chunk j = 16(s>>3) + 8h + (s&7) of the query row). Wave w
-  //    copies queries 8w .. 8w + 7: lane l takes query 8w + (l&7), chunk 8i + (l>>3) at step i,
-  //    so one load instruction reads 8 whole 128-B lines (8 chunks of each of 8 rows) and the
-  //    8-lane store groups write 8 adjacent 16-B slots (no bank conflict). Round 4 (r04ag stamps:
-  //    10.8 us of every launch) had lane = query, 64 lines per load instruction, each line
-  //    re-fetched by 8 instructions through a thrashed L1. All loads are in flight at once.
+  // 1. The query image by LDS-DMA: wave w copies queries 8w .. 8w + 7, each row as 1-KB pieces
+  //    (lane l: bytes 16 l of the piece; a short last piece masks its lanes off), all in flight
+  //    with the first tile's row loads issued behind them. Rows past the call's queries stay
+  //    unwritten (their MFMA columns are never read). Then |q| rounded up (fp32 sum of DIM squares,
+  //    relative error < 2^-13) from the image: lane l sums chunks (l >> 3) + 8 i of query
+  //    8w + (l & 7). (Round 4-5: register-staged copy into a chunk-major image, 7.5-8.2 us of
+  //    every launch; profiles/r06_i8_image_dma_ab.txt.)
   {
-    constexpr int PER = DIM / 64;  // load instructions per wave
-    const int q = 8 * wave + (lane & 7);
-    const int jl = lane >> 3;
-    u32x4 v[PER];
+    constexpr int PIECES = (DIM * 2 + 1023) / 1024;  // 1-KB pieces per query row
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-      v[i] = q < nq ? *reinterpret_cast<const u32x4*>(qrow(q) + 8 * (8 * i + jl))
-                    : u32x4{0u, 0u, 0u, 0u};
+    for (int qq = 0; qq < 8; ++qq) {
+      const int q = 8 * wave + qq;
+      if (q < nq) {  // wave-uniform
+        const unsigned char* src = reinterpret_cast<const unsigned char*>(qrow(q));
+#pragma unroll
+        for (int pc = 0; pc < PIECES; ++pc) {
+          constexpr int kTail = (DIM * 2) % 1024;
+          if (kTail == 0 || pc < PIECES - 1 || lane * 16 < kTail)
+            __builtin_amdgcn_global_load_lds(src + pc * 1024 + lane * 16,
+                                             (lds_ptr_t)(smem + q * QS + pc * 1024), 16, 0, 0);
+        }
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     prefetch_first();
     __builtin_amdgcn_sched_barrier(0);
+    // this wave's pieces are in LDS (it reads only its own rows below; the barrier after this
+    // block publishes them to the other waves)
+    if (t >= 0)  // (wave-uniform: the row loads behind the pieces were issued)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH * 4) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    constexpr int CH = DIM / 8;  // 16-B chunks per row
+    const int q = 8 * wave + (lane & 7);
     float ss = 0.0f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int j = 8 * i + jl;
-      const int sh = 2 * (8 * (j >> 4) + (j & 7)) + ((j >> 3) & 1);
-      qimg[sh * kQB + q] = v[i];
-      const half8 hv = __builtin_bit_cast(half8, v[i]);
+    for (int i = 0; i < CH / 8; ++i) {
+      const int j = 8 * i + (lane >> 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + q * QS + j * 16);
+      const half8 hv = __builtin_bit_cast(half8, v);
 #pragma unroll
       for (int c = 0; c < 8; ++c) ss += (float)hv[c] * (float)hv[c];
     }
@@ -556,9 +582,15 @@ __device__ __forceinline__ void scan_i8_body(
       bool has_next = false;
       float4 sv[4], ev[4];  // a32 / e32 of the lane's 16 rows (loaded mid-tile)
       const int32_t tord = tile_ord[t];  // ordinal of the tile's image row 0 (wave-uniform)
-      int qoff = h * kQB + r;
+      // the lane's two query rows in the image (queries r and 32 + r, chunk half h)
+      int qoff = r * QS + h * 128;
       asm volatile("" : "+v"(qoff));
-      const u32x4* qv = qimg + qoff;
+      const unsigned char* qb0 = smem + qoff;
+      const unsigned char* qb1 = qb0 + 32 * QS;
+      // k-step s: chunk 16 (s >> 3) + 8 h + (s & 7) of the row (the corpus chunks' order)
+      auto qfrag = [&](const unsigned char* b, int s) {
+        return *reinterpret_cast<const u32x4*>(b + (s >> 3) * 256 + (s & 7) * 16);
+      };
       f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
       for (int g = 0; g < GROUPS; ++g) {
@@ -613,12 +645,12 @@ __device__ __forceinline__ void scan_i8_body(
 #endif
           const int s = 8 * g + 2 * i;
 #if defined(ARMI_PROBE_BUILD) && ARMI_I8_ABL == 2  // timing only: no MFMAs
-          asm volatile("" :: "v"(f0), "v"(f1), "v"(qv[s * 2 * kQB]), "v"(qv[(s + 1) * 2 * kQB + 32]));
+          asm volatile("" :: "v"(f0), "v"(f1), "v"(qfrag(qb0, s)), "v"(qfrag(qb1, s + 1)));
 #else
-          acc0 = mfma16(f0, qv[s * 2 * kQB], acc0);
-          acc1 = mfma16(f0, qv[s * 2 * kQB + 32], acc1);
-          acc0 = mfma16(f1, qv[(s + 1) * 2 * kQB], acc0);
-          acc1 = mfma16(f1, qv[(s + 1) * 2 * kQB + 32], acc1);
+          acc0 = mfma16(f0, qfrag(qb0, s), acc0);
+          acc1 = mfma16(f0, qfrag(qb1, s), acc1);
+          acc0 = mfma16(f1, qfrag(qb0, s + 1), acc0);
+          acc1 = mfma16(f1, qfrag(qb1, s + 1), acc1);
 #endif
         }
       }
@@ -769,7 +801,7 @@ __global__ __launch_bounds__(kThreads) void dense_scan_i8_kernel(
 
 template <int DIM>
 constexpr int scan_i8_lds_bytes() {
-  return scan_lds_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB) + kQB * 8 + kWaves * 4;
+  return i8_img_bytes<DIM>() + kQB * 8 + kQB * 4 * (kThreads / kQB) + kQB * 8 + kWaves * 4;
 }
 
 // Multi-block scan for calls with more than 2 * kQB queries (the all-gathered batch of a sharded
