@@ -460,7 +460,9 @@ def main() -> None:
         # events: the scans' launch times come from eager launches of the same kernels over the
         # same batches right after the timed region (the rerank, timed above, is not rerun).
         n_eager = min(args.steps, 20)
-        _armi.call("armi_scan_timing_enable", 1)  # (outside the timed region: every launch)
+        # (outside the timed region: every launch; period 2 so that a sparse call times either
+        # its whole stage or its scan, never both)
+        _armi.call("armi_scan_timing_enable", 2 if sindex is not None else 1)
         for i in range(n_eager):
             j = i % n_q_batches
             hybrid(lambda: index.topk(queries[j], pre_k, workspace=ws),
@@ -478,8 +480,8 @@ def main() -> None:
             _armi.call("armi_kernel_timing_read", slot, _armi.ctypes.byref(v), _armi.ctypes.byref(c))
             sparse_timing[key] = (v.value, c.value)
         barrier()
-        _armi.call("armi_scan_timing_enable", 1)
-        for i in range(min(args.steps, 20)):
+        _armi.call("armi_scan_timing_enable", 2)  # stage and scan timed on alternate calls
+        for i in range(max(min(args.steps, 40), 8)):
             sindex.topk(*q_sparse[i % n_q_batches], pre_k, workspace=sws)
         barrier()
         for slot, key in ((_armi.TIMING_SPARSE_SCAN, "scan_alone"),

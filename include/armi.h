@@ -171,8 +171,10 @@ int armi_topk_merge_shards_packed(const void* packed, int64_t shard_stride,
  * enable-th launch of a timed kernel (enable = 1: every launch; 0 disables) carries a HIP event
  * pair: a scan kernel's events are bound to its own dispatch (hipExtLaunchKernel: the kernel's
  * start and end, no marker packets), a whole sparse call is bracketed by events on its stream.
- * Launches under stream capture are not timed. _read synchronises on the recorded events of one
- * slot, returns the summed time and the number of timed launches, and clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
+ * Launches under stream capture are not timed, and an armi_sparse_topk call whose whole stage is
+ * timed does not also time its scan (period 2 alternates them). _read synchronises on the
+ * recorded events of one slot, returns the summed time and the number of timed launches, and
+ * clears them. Slots: ARMI_TIMING_DENSE_SCAN (the dense scan kernel of
  * armi_dense_topk), ARMI_TIMING_SPARSE_SCAN (the dominant scan of armi_sparse_topk: the MFMA
  * filter scan when the filter runs, else sparse_scan_kernel), ARMI_TIMING_ENCODER_GEMM (the
  * cross-encoder GEMMs of armi_enc_linear_f16), ARMI_TIMING_SPARSE_STAGE (a whole

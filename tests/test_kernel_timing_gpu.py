@@ -1,8 +1,9 @@
 """Live kernel timing (armi_scan_timing_enable / armi_kernel_timing_read, what bench.py's roofline
 objects divide by): the timed launches carry their events on the dispatch itself
 (hipExtLaunchKernel), so a timed call answers exactly as an untimed one, every timed launch is
-counted once with a positive duration, a period n times every n-th launch of a slot, and nothing
-is recorded while timing is off."""
+counted once with a positive duration, a period n times every n-th launch of a slot, a sparse
+call times its whole stage or its scan (never both), and nothing is recorded while timing is
+off."""
 import ctypes
 
 import pytest
@@ -36,10 +37,11 @@ def test_timed_launches_counted_and_results_unchanged(gpu):
     try:
         outs = [(di.topk(q, 5), si.topk(*qs, 20)) for _ in range(3)]
         torch.cuda.synchronize()
-        for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_SCAN,
-                     _armi.TIMING_SPARSE_STAGE):
+        for slot in (_armi.TIMING_DENSE_SCAN, _armi.TIMING_SPARSE_STAGE):
             ms, n = _read(_armi, slot)
             assert n == 3 and ms > 0.0, (slot, n, ms)
+        # a call whose whole stage is timed does not also time its scan
+        assert _read(_armi, _armi.TIMING_SPARSE_SCAN)[1] == 0
     finally:
         _armi.call("armi_scan_timing_enable", 0)
     # a period of 2: every second launch of each slot is timed
@@ -50,7 +52,9 @@ def test_timed_launches_counted_and_results_unchanged(gpu):
             si.topk(*qs, 20)
         torch.cuda.synchronize()
         assert _read(_armi, _armi.TIMING_DENSE_SCAN)[1] == 2
-        assert _read(_armi, _armi.TIMING_SPARSE_STAGE)[1] == 2
+        assert _read(_armi, _armi.TIMING_SPARSE_STAGE)[1] == 2  # calls 0 and 2
+        ms, n = _read(_armi, _armi.TIMING_SPARSE_SCAN)  # the scans of calls 1 and 3: every 2nd
+        assert n == 1 and ms > 0.0
     finally:
         _armi.call("armi_scan_timing_enable", 0)
     for d, s in outs:
