@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record: the ARMI_FUSE_ON_SIDE switch was removed after this A/B, profiles/r06_rrf_stream_ab.txt)
 # Hybrid step A/B: RRF on the side stream (default) vs on the caller's stream (ARMI_FUSE_ON_SIDE=0)
 cd "$GRAFT_REPO_ROOT" || exit 1
 : > gpurun_out/fuse_ab.txt

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record: dense_tail_kernel and ARMI_DENSE_TAIL were removed after this A/B, profiles/r06_dense_tail_ab.txt)
 # Dense tail A/B: ARMI_DENSE_TAIL=1 (merge + collect pass + collect merge in one launch) vs 0
 # (three launches), interleaved, 1M and 100k rows; then the dense parity tests under the default.
 TAG=${1:-tail}
