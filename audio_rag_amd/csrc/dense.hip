@@ -1006,7 +1006,9 @@ void dense_gemm_scan_w4_kernel(
   // (one query per (lane, n), so the lane's and the workgroup's comparisons see one scale):
   // u = D a32 + e32 c1 + c2 with c1 = (|q| + eq) / s_q, c2 = eq / s_q, and s_q u is written to
   // the candidate lists. A zero query (s_q = 0: D = eq = |q| = 0) keeps scale 1, c1 = 1, c2 = 0
-  // (e32 >= 0 still bounds its 0 cosine; c1 >= 1 keeps a dead row's key at -inf / -FLT_MAX).
+  // (e32 >= 0 still bounds its 0 cosine). For an fp16 query 1 <= c1 < 2^20 (s_q >= max|q_i| / 254,
+  // |q| <= sqrt(DIM) max|q_i|), so a dead row's key (bias -1e30) stays finite and below -1e30;
+  // scales that are not finite (a query holding inf/NaN) fall back to the zero query's.
   float qs_s[4] = {1.f, 1.f, 1.f, 1.f}, qs_c1[4] = {1.f, 1.f, 1.f, 1.f},
         qs_c2[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (I8) {
@@ -1015,10 +1017,11 @@ void dense_gemm_scan_w4_kernel(
       const int q = q_base + wq * 128 + n * 32 + r;
       if (q < nq) {
         const float4 v = qsc[q];
-        if (v.x > 0.0f) {
+        const float c1 = v.z / v.x, c2 = v.y / v.x;
+        if (v.x > 0.0f && c1 < 1.0e20f && c2 < 1.0e20f) {
           qs_s[n] = v.x;
-          qs_c1[n] = v.z / v.x;
-          qs_c2[n] = v.y / v.x;
+          qs_c1[n] = c1;
+          qs_c2[n] = c2;
         }
       }
     }
@@ -1028,9 +1031,10 @@ void dense_gemm_scan_w4_kernel(
   // insertion per score and no lane masks): each score carries its row code m*16 + j in its 6 low
   // mantissa bits (a perturbation below 2^-18 |score|, covered by the certificate's kEncodeSlack),
   // so per lane and query block a max/min chain keeps the tile's best two scores WITH their rows
-  // and the largest score below them ("third"): 7 VALU per score. Rows outside the range or
-  // dropped by the filter (and rows the index marks invalid: NaN inverse norm) score -FLT_MAX
-  // instead. The two best join the lane list, third the discarded bound; a row leaves the
+  // and the largest score below them ("third"): three v_med3_f32 per score. Rows outside the range
+  // or dropped by the filter (and rows the index marks invalid: NaN inverse norm) score -FLT_MAX
+  // (I8: -1e30 c1 + c2) instead: every score is finite, so a coded score is never a NaN and the
+  // v_med3_f32 chain needs no clamp or canonicalising copy. The two best join the lane list, third the discarded bound; a row leaves the
   // candidates only at or below its lane-tile's third or by eviction from the list, both covered by
   // the bound, so dense_merge_kernel's certificate holds (it fails only where one lane-tile of 64
   // rows holds three of the top k).
@@ -1065,7 +1069,7 @@ void dense_gemm_scan_w4_kernel(
                    : "+v"(invw[0]), "+v"(invw[1]), "+v"(invw[2]), "+v"(invw[3]), "+v"(errw[0]),
                      "+v"(errw[1]), "+v"(errw[2]), "+v"(errw[3])::"memory");
       // score = fma(acc, inv, bias): (inv, 0) for a live row, (0, -FLT_MAX) otherwise; I8:
-      // inv = a32, bias = e32 (dead: e32 = -FLT_MAX, folded per query below)
+      // inv = a32, bias = e32 (dead: e32 = -1e30, folded per query below)
       float inv[16], bias[16];
       const uint32_t vb = valid >> (4 * h);
 #pragma unroll
@@ -1079,7 +1083,7 @@ void dense_gemm_scan_w4_kernel(
           const bool live = ((vb >> ((j & 3) + 8 * (j >> 2))) & 1u) && iv == iv;
           inv[j] = live ? iv : 0.0f;
           if constexpr (I8)
-            bias[j] = live ? __uint_as_float(e4v[e]) : -3.4028234663852886e38f;
+            bias[j] = live ? __uint_as_float(e4v[e]) : -1.0e30f;
           else
             bias[j] = live ? 0.0f : -3.4028234663852886e38f;
         }
@@ -1094,34 +1098,30 @@ void dense_gemm_scan_w4_kernel(
         for (int j = 0; j < 16; ++j) {
           float y;
           if constexpr (I8) {
-            // D a32 + e32 c1 + c2 (divided by s_q). A dead row (inv 0, bias -FLT_MAX) gives -inf
-            // (c1 >= 1)
+            // D a32 + e32 c1 + c2 (divided by s_q). A dead row (inv 0, bias -1e30) gives a
+            // finite score <= -1e30 (1 <= c1 < 2^20)
             y = __builtin_fmaf((float)acc[m][n][j], inv[j],
                                __builtin_fmaf(bias[j], qs_c1[n], qs_c2[n]));
           } else {
             y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
           }
-          // code m*16 + j (an inline constant) in the low 6 mantissa bits, then clamped to
-          // >= -FLT_MAX: a coded -inf is a NaN (which the chain below is not transparent to) and
-          // becomes -FLT_MAX; the clamp's result is also canonical, so the v_med3_f32 below take
-          // it without canonicalising copies
-          const float e = __builtin_elementwise_maximumnum(
-              __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j)),
-              -3.4028234663852886e38f);
-          // (no NaN reaches the chain) b1 >= b2 >= b3: one max and two v_med3_f32 keep the
-          // best two and the third (was two min / three max)
+          // code m*16 + j (an inline constant) in the low 6 mantissa bits (y is finite: the
+          // coded score is too). b1 >= b2 >= b3: three v_med3_f32 keep the best two and the
+          // third (the max as med3 against +FLT_MAX: the intrinsic takes the and-or's result
+          // as it is, where max / maximumnum insert a canonicalising copy)
+          const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
           const float nb3 = __builtin_amdgcn_fmed3f(b2[n], b3[n], e);
           b2[n] = __builtin_amdgcn_fmed3f(b1[n], b2[n], e);
-          b1[n] = __builtin_elementwise_maximumnum(b1[n], e);
+          b1[n] = __builtin_amdgcn_fmed3f(b1[n], e, 3.4028234663852886e38f);
           b3[n] = nb3;
         }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
     const int32_t rbase = (int32_t)(lo + tile * kG2Rows + wr * 128) + 4 * h;
-    // code m*16 + j -> row rbase + m*32 + (j & 3) + 8 (j >> 2); -FLT_MAX scores (no live row)
-    // stay out of the lists and the bound
-    constexpr float kDead = -1.0e38f;
+    // code m*16 + j -> row rbase + m*32 + (j & 3) + 8 (j >> 2); dead scores (no live row:
+    // <= -1e30, where live ones are below 2^40 in magnitude) stay out of the lists and the bound
+    constexpr float kDead = -1.0e29f;
     auto row_of = [&](float b) {
       const int32_t code = (int32_t)(__float_as_uint(b) & 63u);
       return rbase + ((code >> 4) << 5) + (code & 3) + ((code & 12) << 1);
