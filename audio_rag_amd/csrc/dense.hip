@@ -41,6 +41,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * 64;
@@ -1094,22 +1095,32 @@ void dense_gemm_scan_w4_kernel(
         // read here from AccVGPRs (else hipcc copies all 256 accumulators out at the loop exit),
         // after the previous block is folded (else the four blocks of m are read out together)
         asm volatile("" : "+a"(acc[m][n]) : "v"(b3[(n + 3) & 3]));
+        // scores two rows at a time (v_pk_fma_f32)
+        float y[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          float y;
+        for (int j = 0; j < 16; j += 2) {
+          const f32x2 iv2 = {inv[j], inv[j + 1]}, bs2 = {bias[j], bias[j + 1]};
+          f32x2 y2;
           if constexpr (I8) {
             // D a32 + e32 c1 + c2 (divided by s_q). A dead row (inv 0, bias -1e30) gives a
             // finite score <= -1e30 (1 <= c1 < 2^20)
-            y = __builtin_fmaf((float)acc[m][n][j], inv[j],
-                               __builtin_fmaf(bias[j], qs_c1[n], qs_c2[n]));
+            const f32x2 a2 = {(float)acc[m][n][j], (float)acc[m][n][j + 1]};
+            y2 = __builtin_elementwise_fma(
+                a2, iv2, __builtin_elementwise_fma(bs2, f32x2{qs_c1[n], qs_c1[n]},
+                                                   f32x2{qs_c2[n], qs_c2[n]}));
           } else {
-            y = __builtin_fmaf(acc[m][n][j], inv[j], bias[j]);
+            y2 = __builtin_elementwise_fma(f32x2{acc[m][n][j], acc[m][n][j + 1]}, iv2, bs2);
           }
+          y[j] = y2.x;
+          y[j + 1] = y2.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
           // code m*16 + j (an inline constant) in the low 6 mantissa bits (y is finite: the
           // coded score is too). b1 >= b2 >= b3: three v_med3_f32 keep the best two and the
           // third (the max as med3 against +FLT_MAX: the intrinsic takes the and-or's result
           // as it is, where max / maximumnum insert a canonicalising copy)
-          const float e = __uint_as_float((__float_as_uint(y) & ~63u) | (uint32_t)(m * 16 + j));
+          const float e = __uint_as_float((__float_as_uint(y[j]) & ~63u) | (uint32_t)(m * 16 + j));
           const float nb3 = __builtin_amdgcn_fmed3f(b2[n], b3[n], e);
           b2[n] = __builtin_amdgcn_fmed3f(b1[n], b2[n], e);
           b1[n] = __builtin_amdgcn_fmed3f(b1[n], e, 3.4028234663852886e38f);
