@@ -1,8 +1,9 @@
 """Per-kernel averages of rocprofv3 --pmc counter CSVs (sum over a dispatch's instances, averaged
 over dispatches). Usage: pmc_summary.py CSV [CSV ...] (kernels whose name contains 'sparse' or
-'pass_terms')."""
+'pass_terms', or $PMC_MATCH when set)."""
 import collections
 import csv
+import os
 import sys
 
 
@@ -13,7 +14,8 @@ def main() -> None:
         for r in csv.DictReader(open(path)):
             k = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")
             k = r["Kernel_Name"].split("::")[-1].split("(")[0] if "::" in r["Kernel_Name"] else k
-            if "sparse" not in k and "pass_terms" not in k:
+            match = os.environ.get("PMC_MATCH")
+            if (match not in k) if match else ("sparse" not in k and "pass_terms" not in k):
                 continue
             per[k][r["Counter_Name"]] += float(r["Counter_Value"])
             seen[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
