@@ -1162,13 +1162,9 @@ void dense_gemm_scan_w4_kernel(
     frags_ready(0);
     __builtin_amdgcn_sched_barrier(0);
     for (int tile = 0; tile < n_tiles; ++tile) {
-      // fresh accumulators per tile (a loop-invariant zero: no conditional reset in the k-loop,
-      // so the 256 accumulators stay put in AccVGPRs)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = acc_t{};
-      for (int kt = 0; kt < KT; ++kt) {
+      // one k-step; the tile's first starts the accumulators from the MFMAs' zero C operand (no
+      // 256 AccVGPR writes per tile)
+      auto kstep = [&](const int kt, auto first) {
         const int s = tile * KT + kt;
         // Stages past the last k-step are issued too (rows clamped into the store, never read),
         // so every wait keeps the same count and the loop carries no issue branches.
@@ -1178,8 +1174,12 @@ void dense_gemm_scan_w4_kernel(
         // MFMAs, so their latency hides behind the last 8); pieces 0-3 of stage s+3
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          if constexpr (!(ABL & 4))
-            acc[i >> 2][i & 3] = mma(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
+          if constexpr (!(ABL & 4)) {
+            if constexpr (decltype(first)::value)
+              acc[i >> 2][i & 3] = mma(fa[0][i >> 2], fb[0][i & 3], acc_t{});
+            else
+              acc[i >> 2][i & 3] = mma(fa[0][i >> 2], fb[0][i & 3], acc[i >> 2][i & 3]);
+          }
           if (i < 8) read_item(s, 1, i);
           if (!(ABL & 1) && i >= 8 && (i & 1)) issue_piece(s3, (i - 8) >> 1);
           __builtin_amdgcn_sched_barrier(0);
@@ -1205,7 +1205,9 @@ void dense_gemm_scan_w4_kernel(
 #pragma unroll
           for (int n = 0; n < 4; ++n) asm volatile("" : "+a"(acc[m][n]));
         __builtin_amdgcn_sched_barrier(0);
-      }
+      };
+      kstep(0, std::true_type{});
+      for (int kt = 1; kt < KT; ++kt) kstep(kt, std::false_type{});
       if constexpr (!(ABL & 2)) epilogue(tile);
       __builtin_amdgcn_sched_barrier(0);
     }
