@@ -2634,7 +2634,12 @@ int dense_topk_impl(const armi_index* idx, const uint16_t* queries, int nq, int 
                                                                                      w.q8, w.qsc);
       ARMI_LAUNCHED("query_i8_kernel");
     }
+#if defined(ARMI_PROBE_BUILD) && defined(ARMI_W4_ABL)  // timing-only ablations (results wrong)
+    auto kern = i8 ? dense_gemm_scan_w4_kernel<DIM, ARMI_W4_ABL, true>
+                   : dense_gemm_scan_w4_kernel<DIM, ARMI_W4_ABL, false>;
+#else
     auto kern = i8 ? dense_gemm_scan_w4_kernel<DIM, 0, true> : dense_gemm_scan_w4_kernel<DIM, 0, false>;
+#endif
     if (int rc = allow_lds(kern, gemm_w4_lds_bytes<DIM>())) return rc;
     const int rc_l = armi::timed_kernel(
         ARMI_TIMING_DENSE_SCAN, kern, dim3(gp.grid), dim3(kW4Threads), gemm_w4_lds_bytes<DIM>(),
