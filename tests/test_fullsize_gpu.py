@@ -287,6 +287,7 @@ def test_bge_m3_full_depth_matches_fp32(gpu):
              "kernel",
              "how is the learning rate schedule chosen for the convex objective in the support "
              "vector machine example and why does the professor prefer boosting trees"]
+    pairs = []  # (name, fp32 reference vector, GPU vector) for the retrieval bound below
     for text in texts:
         ids = e.tokenizer.encode(text)
         with torch.no_grad():
@@ -298,6 +299,7 @@ def test_bge_m3_full_depth_matches_fp32(gpu):
             cos = float(np.dot(ref, d) / np.linalg.norm(d))
             print(f"bge-m3 24 layers {name} L={len(ids)}: cos {cos:.6f}")
             assert cos >= 0.999, (name, cos)
+            pairs.append((name, ref, d))
             got = lex[0]
             clear = [t for t, w in ref_lex.items() if w > 0.05]
             assert all(t in got for t in clear), name
@@ -306,3 +308,53 @@ def test_bge_m3_full_depth_matches_fp32(gpu):
             # weights through a re-biased head)
             np.testing.assert_allclose([got[t] for t in clear], [ref_lex[t] for t in clear],
                                        rtol=5e-2, atol=5e-3)
+    _check_encode_error_bounds_topk(pairs, gpu)
+
+
+def _check_encode_error_bounds_topk(pairs, gpu, n_rows=200_000, k=10):
+    """How far the fp16 encode error can move dense top-k ids (retrieval/qdrant.py:281-332 after
+    embeddings/bge.py:137-157): with q the GPU vector rounded to fp16 and normalised, and r the fp32
+    reference, every row's cosine moves by at most eps = ||q - r|| (unit rows, Cauchy-Schwarz), so
+    a row may enter or leave the top-k only when its reference score is within 2 eps of the k-th.
+    Over a seeded corpus with 48 rows planted at cosines 0.90-0.99 around each reference (near-ties
+    at the top), the GPU top-k of q is checked against that bound; the fraction of ids shared with
+    the reference top-k is printed."""
+    from audio_rag_amd.retrieval.device import DenseIndex
+    from audio_rag_amd.synthetic import make_rows
+
+    base = make_rows(0, n_rows, DIM, gpu)
+    g = torch.Generator(device=gpu).manual_seed(11)
+    planted = []
+    for _, ref, _ in pairs[::2]:  # one reference per text (eager and graph share it)
+        r = torch.from_numpy(ref).to(gpu, torch.float32)
+        noise = torch.randn((48, DIM), generator=g, device=gpu)
+        noise -= (noise @ r)[:, None] * r[None, :]
+        noise /= noise.norm(dim=1, keepdim=True)
+        c = torch.linspace(0.90, 0.99, 48, device=gpu)[:, None]
+        planted.append((c * r[None, :] + torch.sqrt(1 - c * c) * noise).half())
+    rows = torch.cat([base] + planted)
+    perm = torch.randperm(rows.shape[0], generator=g, device=gpu)
+    rows = rows[perm].contiguous()
+    idx = DenseIndex(rows)
+    r64 = rows.double()
+    r64 /= r64.norm(dim=1, keepdim=True)
+    shared = []
+    for name, ref, d in pairs:
+        q16 = torch.from_numpy(d).to(gpu).half()
+        q = q16.double() / q16.double().norm()
+        r = torch.from_numpy(ref).to(gpu, torch.float64)
+        eps = float((q - r).norm())
+        s_ref = r64 @ r
+        want = torch.argsort(-s_ref, stable=True)[:k]  # ties by ordinal
+        out = idx.topk(q16[None, :], k)
+        got = out.ids[0].cpu()
+        assert int(out.count[0]) == k
+        kth = float(s_ref[want[-1]])
+        extra = set(got.tolist()) - set(want.cpu().tolist())
+        for i in extra:
+            assert kth - float(s_ref[i]) <= 2 * eps + 1e-12, (name, i, kth, float(s_ref[i]), eps)
+        shared.append(1 - len(extra) / k)
+        print(f"bge-m3 {name}: eps {eps:.2e}, top-{k} ids shared with the fp32 encode "
+              f"{shared[-1]:.2f} (ref gap k-th to k+1-th "
+              f"{kth - float(s_ref[torch.argsort(-s_ref, stable=True)[k]]):.2e})")
+
